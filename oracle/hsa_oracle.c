@@ -1,0 +1,490 @@
+/*
+ * hsa_oracle.c -- plain-C restatement of the HSA inexact-alignment path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see hsa_oracle.h).  Each function cites the
+ * reference file:line it restates.  It favours obviousness over speed: the rank
+ * structure is a flat prefix count every 32 characters, the stack is the
+ * reference's bucketed LIFO with realloc'd buckets.
+ *
+ * Parity pin: tests/test_oracle.py checks every function here against the
+ * golden vectors the compiled reference produced (tests/golden/).
+ */
+#include "hsa_oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MODE_GAPE 0x01
+#define MODE_LOGGAP 0x04
+#define MODE_NONSTOP 0x10
+#define ST_M 0
+#define ST_I 1
+#define ST_D 2
+
+typedef struct {
+    uint32_t T, isa0, C[5];
+    uint64_t *w;    /* $-less BWT, 32 codes per word, code j at bits 2j..2j+1 */
+    uint32_t *cnt;  /* cnt[b*4+c] = #c in codes [0, 32b) */
+} or_bwt_t;
+
+struct or_index {
+    or_bwt_t f, r;
+    uint64_t queries;   /* rank queries issued (statistics only) */
+};
+
+static void bwt_init(or_bwt_t *b, uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code)
+{
+    /* .bwt words: char j of word at bits 31-2j..30-2j (BWT.c:156-181, BWTConstruct.c:1209) */
+    uint64_t nw = ((uint64_t)T + 31) / 32;
+    b->T = T; b->isa0 = isa0;
+    memcpy(b->C, C, 5 * sizeof(uint32_t));
+    b->w = (uint64_t *)calloc(nw + 1, sizeof(uint64_t));
+    b->cnt = (uint32_t *)calloc((nw + 2) * 4, sizeof(uint32_t));
+    for (uint64_t p = 0; p < T; ++p) {
+        uint32_t c = (code[p >> 4] >> (30 - 2 * (p & 15))) & 3;
+        b->w[p >> 5] |= (uint64_t)c << (2 * (p & 31));
+    }
+    uint32_t acc[4] = {0, 0, 0, 0};
+    for (uint64_t q = 0; q <= nw; ++q) {
+        memcpy(b->cnt + q * 4, acc, sizeof acc);
+        for (uint64_t p = q * 32; p < q * 32 + 32 && p < T; ++p) acc[(b->w[q] >> (2 * (p & 31))) & 3]++;
+    }
+}
+
+or_index_t *or_index_create(uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code,
+                            uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *rcode)
+{
+    or_index_t *ix = (or_index_t *)calloc(1, sizeof(or_index_t));
+    bwt_init(&ix->f, T, isa0, C, code);
+    bwt_init(&ix->r, rT, risa0, rC, rcode);
+    return ix;
+}
+
+void or_index_free(or_index_t *ix)
+{
+    if (!ix) return;
+    free(ix->f.w); free(ix->f.cnt); free(ix->r.w); free(ix->r.cnt); free(ix);
+}
+
+void or_free(void *p) { free(p); }
+
+/* BWTAllOccValue (BWT.c:793-837): $ is not encoded, so an index past inverseSa0
+ * is shifted down by one (BWT.c:690); the sampled-Occ + SSE decode then equals the
+ * prefix count #{p < i' : code[p] == c} (checked at every i in [0, T+1] on the
+ * fixtures).  Here: prefix count at the 32-char word + popcount inside it. */
+static void occ4(const or_bwt_t *b, uint32_t i, uint32_t o[4])
+{
+    i -= (i > b->isa0);
+    uint32_t q = i >> 5, r = i & 31;
+    for (int c = 0; c < 4; ++c) o[c] = b->cnt[q * 4 + c];
+    if (r) {
+        uint64_t x = b->w[q] & ((1ull << (2 * r)) - 1);
+        uint64_t lo = x & 0x5555555555555555ull, hi = (x >> 1) & 0x5555555555555555ull;
+        uint32_t n3 = (uint32_t)__builtin_popcountll(lo & hi);
+        uint32_t n2 = (uint32_t)__builtin_popcountll(hi & ~lo);
+        uint32_t n1 = (uint32_t)__builtin_popcountll(lo & ~hi);
+        o[0] += r - n1 - n2 - n3; o[1] += n1; o[2] += n2; o[3] += n3;
+    }
+}
+
+void or_occ4(const or_index_t *ix, int dir, uint32_t i, uint32_t occ[4])
+{
+    occ4(dir ? &ix->r : &ix->f, i, occ);
+}
+
+/* BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235-272). */
+static void step_all(or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl,
+                     uint32_t ok[4], uint32_t ol[4], uint32_t ork[4], uint32_t orl[4])
+{
+    uint32_t oL[4], oR[4], oC[4];
+    (void)rk;
+    occ4(&ix->f, k, oL);
+    occ4(&ix->f, l + 1, oR);
+    ix->queries += 2;
+    oC[3] = 0;
+    for (int c = 2; c >= 0; --c) oC[c] = oC[c + 1] + oR[c + 1] - oL[c + 1];
+    for (int c = 0; c < 4; ++c) {
+        ok[c] = ix->f.C[c] + oL[c] + 1;
+        ol[c] = ix->f.C[c] + oR[c];
+        orl[c] = rl - oC[c];
+        ork[c] = orl[c] - (ol[c] - ok[c]);
+    }
+}
+
+void or_step_all(const or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl,
+                 uint32_t ok[4], uint32_t ol[4], uint32_t ork[4], uint32_t orl[4])
+{
+    step_all((or_index_t *)ix, k, l, rk, rl, ok, ol, ork, orl);
+}
+
+/* BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170): one character. */
+static void step1(or_index_t *ix, uint32_t c, uint32_t *k, uint32_t *l, uint32_t *rk, uint32_t *rl)
+{
+    uint32_t ok[4], ol[4], ork[4], orl[4];
+    step_all(ix, *k, *l, *rk, *rl, ok, ol, ork, orl);
+    *k = ok[c]; *l = ol[c]; *rk = ork[c]; *rl = orl[c];
+}
+
+/* bwt_match_exact (2BWT-Interface.c:365-388), including the write-back guard
+ * (:383-386): an output is only written if its incoming value is non-zero (Q1). */
+static int match_exact(or_index_t *ix, const uint8_t *seq, int len,
+                       uint32_t *sk, uint32_t *sl, uint32_t *srk, uint32_t *srl)
+{
+    uint32_t k = *sk, l = *sl, rk = *srk, rl = *srl;
+    for (int i = len - 1; i >= 0; i--) {
+        if (seq[i] > 3) return 0;
+        step1(ix, seq[i], &k, &l, &rk, &rl);
+        if (k > l) break;
+    }
+    if (k > l) return 0;
+    if (*sk) *sk = k;
+    if (*sl) *sl = l;
+    if (*srk) *srk = rk;
+    if (*srl) *srl = rl;
+    return (int)(l - k + 1);
+}
+
+/* bwt_cal_width, type 1 (bwtaln.c:73-98): forward extension on the REVERSE BWT
+ * with the FORWARD C[] (BWTSARangeForeward, 2BWT-Interface.c:121-132). */
+static int cal_width(or_index_t *ix, int len, const uint8_t *str, uint32_t *w)
+{
+    uint32_t k = 0, l = ix->f.T;
+    int bid = 0;
+    for (int i = 0; i < len; ++i) {
+        uint8_t c = str[i];
+        if (c < 4) {
+            uint32_t a[4], b[4];
+            occ4(&ix->r, k, a);
+            occ4(&ix->r, l + 1, b);
+            ix->queries += 2;
+            k = ix->f.C[c] + a[c] + 1;
+            l = ix->f.C[c] + b[c];
+        }
+        if (k > l || c > 3) { k = 0; l = ix->f.T; ++bid; }
+        w[2 * i] = l - k + 1;
+        w[2 * i + 1] = (uint32_t)bid;
+    }
+    w[2 * len] = 0;
+    w[2 * len + 1] = (uint32_t)++bid;
+    return bid;
+}
+
+int or_cal_width(const or_index_t *ix, int len, const uint8_t *str, uint32_t *width)
+{
+    return cal_width((or_index_t *)ix, len, str, width);
+}
+
+void or_init_opt(or_opt_t *o)
+{
+    memset(o, 0, sizeof *o);
+    o->s_mm = 3; o->s_gapo = 11; o->s_gape = 4;
+    o->max_diff = -1; o->max_gapo = 1; o->max_gape = 6;
+    o->indel_end_skip = 5; o->max_del_occ = 10; o->max_entries = 2000000;
+    o->mode = 0x01 | 0x02;
+    o->seed_len = 32; o->max_seed_diff = 2;
+    o->fnr = 0.04f; o->n_threads = 1; o->max_top2 = 30; o->trim_qual = 0;
+}
+
+int or_cal_maxdiff(int l, double err, double thres)
+{
+    double elambda = exp(-l * err);
+    double sum, y = 1.0;
+    int k, x = 1;
+    for (k = 1, sum = elambda; k < 1000; ++k) {
+        y *= l * err;
+        x *= k;
+        sum += elambda * y / x;
+        if (1.0 - sum < thres) return k;
+    }
+    return 2;
+}
+
+/* ---- bucketed LIFO (bwtgap.c:13-92) ---- */
+typedef struct {
+    uint32_t info;          /* score<<21 | i */
+    uint8_t n_mm, n_gapo, n_gape, state;
+    uint32_t k, l, rk, rl;
+    int last_diff_pos;
+} ent_t;
+typedef struct { int n, m; ent_t *a; } bucket_t;
+typedef struct { int n_stacks, best, n_entries; bucket_t *b; } stack_t_;
+
+#define SCORE(o, m, g, e) ((m) * (o)->s_mm + (g) * (o)->s_gapo + (e) * (o)->s_gape)
+
+static stack_t_ *stack_new(int n_stacks)
+{
+    stack_t_ *s = (stack_t_ *)calloc(1, sizeof *s);
+    s->n_stacks = n_stacks;
+    s->b = (bucket_t *)calloc(n_stacks, sizeof(bucket_t));
+    for (int i = 0; i < n_stacks; ++i) { s->b[i].m = 4; s->b[i].a = (ent_t *)calloc(4, sizeof(ent_t)); }
+    return s;
+}
+
+static void stack_del(stack_t_ *s)
+{
+    for (int i = 0; i < s->n_stacks; ++i) free(s->b[i].a);
+    free(s->b); free(s);
+}
+
+static void stack_reset(stack_t_ *s)
+{
+    for (int i = 0; i < s->n_stacks; ++i) s->b[i].n = 0;
+    s->best = s->n_stacks; s->n_entries = 0;
+}
+
+static void push(stack_t_ *s, int i, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl,
+                 int n_mm, int n_gapo, int n_gape, int state, int is_diff, const or_opt_t *o)
+{
+    int score = SCORE(o, n_mm, n_gapo, n_gape);
+    if (score < 0 || score >= s->n_stacks) {
+        fprintf(stderr, "oracle: push score %d outside %d buckets (undefined in the reference)\n", score, s->n_stacks);
+        abort();
+    }
+    bucket_t *q = s->b + score;
+    if (q->n == q->m) { q->m <<= 1; q->a = (ent_t *)realloc(q->a, sizeof(ent_t) * q->m); }
+    ent_t *p = q->a + q->n;
+    p->info = (uint32_t)score << 21 | (uint32_t)i;
+    p->k = k; p->l = l; p->rk = rk; p->rl = rl;
+    p->n_mm = (uint8_t)n_mm; p->n_gapo = (uint8_t)n_gapo; p->n_gape = (uint8_t)n_gape;
+    p->state = (uint8_t)state;
+    p->last_diff_pos = is_diff ? i : 0;
+    ++q->n; ++s->n_entries;
+    if (s->best > score) s->best = score;
+}
+
+static void pop(stack_t_ *s, ent_t *e)
+{
+    bucket_t *q = s->b + s->best;
+    *e = q->a[q->n - 1];
+    --q->n; --s->n_entries;
+    if (q->n == 0 && s->n_entries) {
+        int i;
+        for (i = s->best + 1; i < s->n_stacks; ++i) if (s->b[i].n) break;
+        s->best = i;
+    } else if (s->n_entries == 0) s->best = s->n_stacks;
+}
+
+/* gap_shadow (bwtgap.c:94-105) */
+static void shadow(uint32_t x, uint32_t max, int last_diff_pos, uint32_t *w)
+{
+    int j = 0;
+    for (int i = 0; i < last_diff_pos; ++i) {
+        if (w[2 * i] > x) w[2 * i] -= x;
+        else if (w[2 * i] == x) { w[2 * i + 1] = 1; w[2 * i] = max - (uint32_t)(++j); }
+    }
+}
+
+static int int_log2(uint32_t v)   /* bwtgap.c:107-116 */
+{
+    int c = 0;
+    if (v & 0xffff0000u) { v >>= 16; c |= 16; }
+    if (v & 0xff00) { v >>= 8; c |= 8; }
+    if (v & 0xf0) { v >>= 4; c |= 4; }
+    if (v & 0xc) { v >>= 2; c |= 2; }
+    if (v & 0x2) c |= 1;
+    return c;
+}
+
+typedef struct { int n, m; uint32_t *a; } hitv_t;   /* 9 words per hit */
+
+/* bwt_match_gap (bwtgap.c:118-331).  width/width_seed are 2*(len+1) word arrays. */
+static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const uint8_t *seq, int len,
+                      int strand, uint32_t *width, const uint32_t *width_seed, hitv_t *out,
+                      uint64_t *pops)
+{
+    int best_score = SCORE(opt, opt->max_diff + 1, opt->max_gapo + 1, opt->max_gape + 1);
+    int best_diff = opt->max_diff + 1, max_diff = opt->max_diff;
+    int best_cnt = 0, n_aln = 0;
+    const uint32_t T = ix->f.T;
+    out->n = 0;
+    stack_reset(st);
+    push(st, len, 0, T, 0, T, 0, 0, 0, 0, 0, opt);
+    while (st->n_entries) {
+        ent_t e;
+        int i, m, m_seed = 0, hit = 0, allow_diff, allow_M, tmp;
+        uint32_t k, l, rk, rl, sk[4], sl[4], srk[4], srl[4], occ;
+        if (st->n_entries > opt->max_entries) break;
+        pop(st, &e);
+        if (pops) ++*pops;
+        k = e.k; l = e.l; rk = e.rk; rl = e.rl;
+        i = (int)(e.info & 0xffff);
+        if (!(opt->mode & MODE_NONSTOP) && (int)(e.info >> 21) > best_score + opt->s_mm) break;
+        m = max_diff - (e.n_mm + e.n_gapo);
+        if (opt->mode & MODE_GAPE) m -= e.n_gape;
+        if (m < 0) continue;
+        if (width_seed) {
+            m_seed = opt->max_seed_diff - (e.n_mm + e.n_gapo);
+            if (opt->mode & MODE_GAPE) m_seed -= e.n_gape;
+        }
+        if (i > 0 && m < (int)width[2 * (i - 1) + 1]) continue;
+        if (i == 0) hit = 1;
+        else if (m == 0 && (e.state == ST_M || (opt->mode & MODE_GAPE) || e.n_gape == opt->max_gape)) {
+            if (match_exact(ix, seq, i, &k, &l, &rk, &rl)) hit = 1;
+            else continue;
+        }
+        if (hit) {
+            int score = SCORE(opt, e.n_mm, e.n_gapo, e.n_gape);
+            int do_add = 1;
+            if (n_aln == 0) {
+                best_score = score;
+                best_diff = e.n_mm + e.n_gapo;
+                if (opt->mode & MODE_GAPE) best_diff += e.n_gape;
+                if (!(opt->mode & MODE_NONSTOP))
+                    max_diff = (best_diff + 1 > opt->max_diff) ? opt->max_diff : best_diff + 1;
+            }
+            if (score == best_score) best_cnt += (int)(l - k + 1);
+            else if (best_cnt > opt->max_top2) break;
+            if (e.n_gapo) {
+                int j;
+                for (j = 0; j != n_aln; ++j)
+                    if (out->a[9 * j + 1] == k && out->a[9 * j + 2] == l) break;
+                if (j < n_aln) do_add = 0;
+            }
+            if (do_add) {
+                shadow(l - k + 1, T, e.last_diff_pos, width);
+                if (out->n == out->m) {
+                    out->m = out->m ? out->m * 2 : 16;
+                    out->a = (uint32_t *)realloc(out->a, sizeof(uint32_t) * 9 * out->m);
+                }
+                uint32_t *p = out->a + 9 * out->n;
+                p[0] = (uint32_t)e.n_mm | (uint32_t)e.n_gapo << 16 | (uint32_t)e.n_gape << 24;
+                p[1] = k; p[2] = l; p[3] = rk; p[4] = rl;
+                p[5] = (uint32_t)(strand & 3) << 30;     /* type 0 */
+                p[6] = 0; p[7] = 0;
+                p[8] = (uint32_t)score;
+                ++out->n; ++n_aln;
+            }
+            continue;
+        }
+        --i;
+        step_all(ix, k, l, rk, rl, sk, sl, srk, srl);
+        occ = l - k + 1;
+        allow_diff = allow_M = 1;
+        if (i > 0) {
+            int ii = i - (len - opt->seed_len);
+            if ((int)width[2 * (i - 1) + 1] > m - 1) allow_diff = 0;
+            else if ((int)width[2 * (i - 1) + 1] == m - 1 && (int)width[2 * i + 1] == m - 1 &&
+                     width[2 * (i - 1)] == width[2 * i]) allow_M = 0;
+            if (width_seed && ii > 0) {
+                if ((int)width_seed[2 * (ii - 1) + 1] > m_seed - 1) allow_diff = 0;
+                else if ((int)width_seed[2 * (ii - 1) + 1] == m_seed - 1 && (int)width_seed[2 * ii + 1] == m_seed - 1 &&
+                         width_seed[2 * (ii - 1)] == width_seed[2 * ii]) allow_M = 0;
+            }
+        }
+        tmp = (opt->mode & MODE_LOGGAP) ? int_log2(e.n_gape + e.n_gapo) / 2 + 1 : e.n_gapo + e.n_gape;
+        if (allow_diff && i >= opt->indel_end_skip + tmp && len - i >= opt->indel_end_skip + tmp) {
+            if (e.state == ST_M) {
+                if (e.n_gapo < opt->max_gapo) {
+                    push(st, i, k, l, rk, rl, e.n_mm, e.n_gapo + 1, e.n_gape, ST_I, 1, opt);
+                    for (int j = 0; j != 4; ++j)
+                        if (sk[j] <= sl[j])
+                            push(st, i + 1, sk[j], sl[j], srk[j], srl[j], e.n_mm, e.n_gapo + 1, e.n_gape, ST_D, 1, opt);
+                }
+            } else if (e.state == ST_I) {
+                if (e.n_gape < opt->max_gape)
+                    push(st, i, k, l, rk, rl, e.n_mm, e.n_gapo, e.n_gape + 1, ST_I, 1, opt);
+            } else if (e.state == ST_D) {
+                if (e.n_gape < opt->max_gape) {
+                    if (e.n_gape + e.n_gapo < max_diff || occ < (uint32_t)opt->max_del_occ) {
+                        for (int j = 0; j != 4; ++j)
+                            if (sk[j] <= sl[j])
+                                push(st, i + 1, sk[j], sl[j], srk[j], srl[j], e.n_mm, e.n_gapo, e.n_gape + 1, ST_D, 1, opt);
+                    }
+                }
+            }
+        }
+        if (allow_diff && allow_M) {
+            for (int j = 1; j <= 4; ++j) {
+                int c = (seq[i] + j) & 3;
+                int is_mm = (j != 4 || seq[i] > 3);
+                if (sk[c] <= sl[c])
+                    push(st, i, sk[c], sl[c], srk[c], srl[c], e.n_mm + is_mm, e.n_gapo, e.n_gape, ST_M, is_mm, opt);
+            }
+        } else if (seq[i] < 4) {
+            int c = seq[i] & 3;
+            if (sk[c] <= sl[c])
+                push(st, i, sk[c], sl[c], srk[c], srl[c], e.n_mm, e.n_gapo, e.n_gape, ST_M, 0, opt);
+        }
+    }
+}
+
+static void revcomp(int len, const uint8_t *s, uint8_t *d)   /* seq_reverse(.., 1), bwaseqio.c:73-84 */
+{
+    for (int i = 0; i < len; ++i) {
+        uint8_t c = s[len - 1 - i];
+        d[i] = c < 4 ? (uint8_t)(3 - c) : c;
+    }
+}
+
+/* bwa_cal_sa_reg_gap (bwtaln.c:246-417).  `opt` is the caller's option block and
+ * is mutated exactly as the reference mutates it through aux->opt. */
+long or_cal_sa_reg_gap(const or_index_t *cix, int n, const uint32_t *lens, const uint8_t *codes,
+                       or_opt_t *opt, int32_t *n_aln, uint32_t *flags, uint32_t **hits_out,
+                       uint64_t *stats)
+{
+    or_index_t *ix = (or_index_t *)cix;
+    or_opt_t local = *opt;                 /* :254, copied before the GAPE clear */
+    or_opt_t *cur = opt;                   /* aux->opt (:259) */
+    int max_len = 0;
+    uint64_t pops = 0, q0 = ix->queries;
+    opt->mode &= ~MODE_GAPE;               /* :261 */
+    for (int i = 0; i < n; ++i) if ((int)lens[i] > max_len) max_len = (int)lens[i];
+    if (opt->fnr > 0.0) local.max_diff = or_cal_maxdiff(max_len, 0.02, opt->fnr);
+    if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;
+    stack_t_ *st = stack_new(SCORE(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1));
+    uint32_t *wb = (uint32_t *)calloc(2 * (max_len + 1), sizeof(uint32_t));
+    uint32_t *ws = (uint32_t *)calloc(2 * (max_len + 1), sizeof(uint32_t));
+    uint8_t *rc = (uint8_t *)calloc(max_len + 1, 1);
+    hitv_t hv = {0, 0, NULL}, all = {0, 0, NULL};
+    size_t off = 0;
+    for (int r = 0; r < n; ++r) {
+        const uint8_t *seq = codes + off;
+        int len = (int)lens[r];
+        off += lens[r];
+        n_aln[r] = 0;
+        flags[r] = 0;
+        int nN = 0;
+        for (int j = 0; j < len; ++j) if (seq[j] > 3) ++nN;
+        if (nN > local.max_diff) { flags[r] = 2; continue; }          /* :314-317 */
+        if (len >= 15) {                                               /* :324-325 (memcmp of 15) */
+            int a = 1, t = 1;
+            for (int j = 0; j < 15; ++j) { a &= seq[j] == 0; t &= seq[j] == 3; }
+            if (a || t) continue;
+        }
+        if (opt->fnr > 0.0) cur->max_diff = or_cal_maxdiff(len, 0.02, opt->fnr);   /* :330-331 */
+        cur->seed_len = opt->seed_len < len ? opt->seed_len : 0x7fffffff;          /* :332 */
+        revcomp(len, seq, rc);
+        int found = 0;
+        for (int s = 1; s >= 0; --s) {                                 /* :343 rc first */
+            const uint8_t *sq = s ? rc : seq;
+            int has_seed = len > cur->seed_len;
+            if (has_seed) cal_width(ix, opt->seed_len, sq + (len - cur->seed_len), ws);
+            else if (cur->max_diff > 0) {
+                fprintf(stderr, "oracle: read %d len %d <= seed_len: undefined in the reference (Q5)\n", r, len);
+            }
+            cal_width(ix, len, sq, wb);
+            match_gap(ix, st, cur, sq, len, s, wb, has_seed ? ws : NULL, &hv, &pops);
+            if (hv.n) { found = hv.n; break; }
+        }
+        if (!found) {                                                  /* :362-369 */
+            flags[r] |= 1;
+            cur = &local;
+            continue;
+        }
+        hv.a[6] = 0; hv.a[7] = (uint32_t)(len - 1);                   /* :371-372 */
+        n_aln[r] = found;
+        if (all.n + found > all.m) {
+            all.m = (all.n + found) * 2 + 16;
+            all.a = (uint32_t *)realloc(all.a, sizeof(uint32_t) * 9 * all.m);
+        }
+        memcpy(all.a + 9 * all.n, hv.a, sizeof(uint32_t) * 9 * found);
+        all.n += found;
+    }
+    free(wb); free(ws); free(rc); free(hv.a);
+    stack_del(st);
+    if (stats) { stats[0] = ix->queries - q0; stats[1] = pops; }
+    *hits_out = all.a ? all.a : (uint32_t *)calloc(9, sizeof(uint32_t));
+    return all.n;
+}

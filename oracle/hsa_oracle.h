@@ -1,0 +1,64 @@
+/*
+ * hsa_oracle.h -- CPU restatement of the HSA inexact-alignment path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this; the product library (hsa_amd/csrc) never links
+ * it and must fail loudly instead of falling back to it.
+ *
+ * Pinned against golden vectors produced by the compiled reference
+ * (oracle/_ref via tools/make_golden.py -> tests/golden/ npz files).
+ */
+#ifndef HSA_ORACLE_H
+#define HSA_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Option block with the field order/meaning of gap_opt_t (bwtaln.h:133-143). */
+typedef struct {
+    int s_mm, s_gapo, s_gape;
+    int mode;
+    int indel_end_skip, max_del_occ, max_entries;
+    float fnr;
+    int max_diff, max_gapo, max_gape;
+    int max_seed_diff, seed_len;
+    int n_threads;
+    int max_top2;
+    int trim_qual;
+} or_opt_t;
+
+typedef struct or_index or_index_t;
+
+/* Build from the reference's .bwt words (2-bit MSB-first, BWT.c:156-181) of the
+ * forward and reverse BWT.  Copies what it needs. */
+or_index_t *or_index_create(uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code,
+                            uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *rcode);
+void or_index_free(or_index_t *ix);
+
+/* BWTAllOccValue (BWT.c:793); dir 0 = forward BWT, 1 = reverse BWT. */
+void or_occ4(const or_index_t *ix, int dir, uint32_t i, uint32_t occ[4]);
+/* BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235). */
+void or_step_all(const or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl,
+                 uint32_t ok[4], uint32_t ol[4], uint32_t ork[4], uint32_t orl[4]);
+/* bwt_cal_width type 1 (bwtaln.c:73-98); width is 2*(len+1) words {w, bid}. */
+int or_cal_width(const or_index_t *ix, int len, const uint8_t *str, uint32_t *width);
+
+void or_init_opt(or_opt_t *o);                      /* gap_init_opt, bwtaln.c:21-44 */
+int or_cal_maxdiff(int l, double err, double thres); /* bwa_cal_maxdiff, bwtaln.c:46-58 */
+
+/* bwa_cal_sa_reg_gap (bwtaln.c:246-417) over one batch, with its side effects on
+ * *opt.  hits: 9 u32 per bwt_aln1_t (bwtaln.h:41-50 layout); flags bit0 = the read
+ * would go to bwt_splice_match (its splice hits are NOT produced here);
+ * bit1 = the read was skipped by the N filter.  Stats optional (may be NULL):
+ * [0] rank queries, [1] pops.  Returns total hits; *hits is malloc'd. */
+long or_cal_sa_reg_gap(const or_index_t *ix, int n, const uint32_t *lens, const uint8_t *codes,
+                       or_opt_t *opt, int32_t *n_aln, uint32_t *flags, uint32_t **hits,
+                       uint64_t *stats);
+void or_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

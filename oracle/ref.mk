@@ -1,0 +1,39 @@
+# Builds the REFERENCE (BioinformaticsArchive/HSA) from its own sources where
+# they lie under /root/reference, into oracle/_ref/ only.  Test infrastructure:
+# the outputs are the oracle's pin (golden vectors) and the optional CPU baseline;
+# nothing under oracle/ is linked into the product library.
+#
+# Flags = reference Makefile:3 minus -static, plus -fgnu89-inline (SURVEY §4.3:
+# without it gcc 11 fails to link bwt_array.c's C99 inline definitions) and -fPIC.
+REF      ?= /root/reference
+OUT      ?= $(CURDIR)/_ref
+CC       ?= gcc
+REFFLAGS  = -w -g -O3 -funroll-loops -march=nocona -maccumulate-outgoing-args \
+            -fno-stack-protector -msse3 -fgnu89-inline -fPIC
+REFOBJS   = bwtaln bwtgap BWT BWTConstruct utils dictionary DNACount HSP iniparser \
+            inistrlib MemManager MiscUtilities QSufSort 2BWT-Builder TextConverter Timing \
+            bamlite 2BWT-Interface bwaseqio r250 cs2nt bwtse kstring stdaln bwt_array
+OBJS      = $(addprefix $(OUT)/obj/,$(addsuffix .o,$(REFOBJS)))
+
+all: $(OUT)/HSA $(OUT)/ref_probe
+
+$(OUT)/obj/%.o: $(REF)/%.c
+	@mkdir -p $(OUT)/obj
+	$(CC) -c $(REFFLAGS) -I$(REF) $< -o $@
+
+$(OUT)/libhsaref.a: $(OBJS)
+	rm -f $@ && ar rcs $@ $(OBJS)
+
+$(OUT)/HSA: $(OUT)/obj/main.o $(OUT)/libhsaref.a
+	$(CC) $(REFFLAGS) $^ -lm -lz -o $@
+
+# ref_probe.c is ours; it drives the reference's bwa_cal_sa_reg_gap batch by batch
+# and records which reads reached bwt_splice_match via --wrap.
+$(OUT)/ref_probe: ref_probe.c $(OUT)/libhsaref.a
+	$(CC) $(REFFLAGS) -I$(REF) ref_probe.c $(OUT)/libhsaref.a \
+	    -Wl,--wrap=bwt_splice_match -lm -lz -o $@
+
+clean:
+	rm -rf $(OUT)
+
+.PHONY: all clean

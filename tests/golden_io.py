@@ -1,0 +1,67 @@
+"""Loading the committed golden fixtures (tests/golden/, made by tools/make_golden.py)."""
+import json
+import os
+
+import numpy as np
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+INDEX = {"tiny": os.path.join(GOLD, "index", "tiny.fa"), "rep": os.path.join(GOLD, "index", "rep.fa")}
+
+
+def cases():
+    with open(os.path.join(GOLD, "manifest_tiny.json")) as f:
+        return json.load(f)
+
+
+def load_case(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    d["args"] = str(d["args"]).split()
+    d["index"] = str(d["index"])
+    d["batch"] = int(d["batch"])
+    return d
+
+
+def split_hits(n_aln, hits):
+    """Per-read list of (n_aln, 9) uint32 arrays."""
+    out, o = [], 0
+    for na in n_aln:
+        na = max(int(na), 0)
+        out.append(hits[o:o + na])
+        o += na
+    return out
+
+
+def parse_opts(args, base):
+    """Apply `HSA aln`-style flags (bwtaln.c:539-575) to an option dict."""
+    o = dict(base)
+    i = 0
+    opte = -1
+    while i < len(args):
+        a = args[i]
+        v = args[i + 1] if i + 1 < len(args) else "0"
+        if a == "-n":
+            if "." in v:
+                o["fnr"], o["max_diff"] = float(v), -1
+            else:
+                o["max_diff"], o["fnr"] = int(v), -1.0
+            i += 1
+        elif a in ("-o", "-M", "-O", "-E", "-d", "-i", "-l", "-k", "-m", "-R", "-B", "-e"):
+            key = {"-o": "max_gapo", "-M": "s_mm", "-O": "s_gapo", "-E": "s_gape", "-d": "max_del_occ",
+                   "-i": "indel_end_skip", "-l": "seed_len", "-k": "max_seed_diff", "-m": "max_entries",
+                   "-R": "max_top2", "-B": None, "-e": "opte"}[a]
+            if key == "opte":
+                opte = int(v)
+            elif key:
+                o[key] = int(v)
+            i += 1
+        elif a == "-L":
+            o["mode"] |= 0x04
+        elif a == "-N":
+            o["mode"] |= 0x10
+            o["max_top2"] = 0x7FFFFFFF
+        i += 1
+    if opte > 0:
+        o["max_gape"] = opte
+        o["mode"] &= ~0x01
+    return o

@@ -1,0 +1,121 @@
+"""ctypes binding of oracle/liboracle.so -- the CPU restatement (test infrastructure).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+
+OPT_FIELDS = [("s_mm", C.c_int), ("s_gapo", C.c_int), ("s_gape", C.c_int), ("mode", C.c_int),
+              ("indel_end_skip", C.c_int), ("max_del_occ", C.c_int), ("max_entries", C.c_int),
+              ("fnr", C.c_float), ("max_diff", C.c_int), ("max_gapo", C.c_int), ("max_gape", C.c_int),
+              ("max_seed_diff", C.c_int), ("seed_len", C.c_int), ("n_threads", C.c_int),
+              ("max_top2", C.c_int), ("trim_qual", C.c_int)]
+
+
+class Opt(C.Structure):
+    _fields_ = OPT_FIELDS
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in OPT_FIELDS}
+
+    @classmethod
+    def from_dict(cls, d):
+        o = cls()
+        for k, _ in OPT_FIELDS:
+            setattr(o, k, d[k])
+        return o
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "liboracle.so"], check=True,
+                           capture_output=True)
+        L = C.CDLL(LIB)
+        u32p = np.ctypeslib.ndpointer(np.uint32, flags="C")
+        L.or_index_create.restype = C.c_void_p
+        L.or_index_create.argtypes = [C.c_uint32, C.c_uint32, u32p, u32p, C.c_uint32, C.c_uint32, u32p, u32p]
+        L.or_index_free.argtypes = [C.c_void_p]
+        L.or_occ4.argtypes = [C.c_void_p, C.c_int, C.c_uint32, u32p]
+        L.or_step_all.argtypes = [C.c_void_p] + [C.c_uint32] * 4 + [u32p] * 4
+        L.or_cal_width.argtypes = [C.c_void_p, C.c_int, np.ctypeslib.ndpointer(np.uint8, flags="C"), u32p]
+        L.or_init_opt.argtypes = [C.POINTER(Opt)]
+        L.or_cal_maxdiff.argtypes = [C.c_int, C.c_double, C.c_double]
+        L.or_cal_sa_reg_gap.restype = C.c_long
+        L.or_cal_sa_reg_gap.argtypes = [C.c_void_p, C.c_int, u32p, np.ctypeslib.ndpointer(np.uint8, flags="C"),
+                                        C.POINTER(Opt), np.ctypeslib.ndpointer(np.int32, flags="C"), u32p,
+                                        C.POINTER(C.POINTER(C.c_uint32)), np.ctypeslib.ndpointer(np.uint64, flags="C")]
+        L.or_free.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def default_opt():
+    o = Opt()
+    lib().or_init_opt(C.byref(o))
+    return o.as_dict()
+
+
+class OracleIndex:
+    def __init__(self, fwd, rev):
+        self.fwd, self.rev = fwd, rev
+        self.h = lib().or_index_create(fwd.T, fwd.isa0, fwd.C, fwd.code, rev.T, rev.isa0, rev.C, rev.code)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_index_free(self.h)
+            self.h = None
+
+    def occ4(self, d, i):
+        o = np.zeros(4, np.uint32)
+        lib().or_occ4(self.h, d, i, o)
+        return o
+
+    def step_all(self, k, l, rk, rl):
+        out = [np.zeros(4, np.uint32) for _ in range(4)]
+        lib().or_step_all(self.h, k, l, rk, rl, *out)
+        return out
+
+    def cal_width(self, seq):
+        seq = np.ascontiguousarray(seq, np.uint8)
+        w = np.zeros(2 * (len(seq) + 1), np.uint32)
+        lib().or_cal_width(self.h, len(seq), seq, w)
+        return w.reshape(-1, 2)
+
+    def cal_sa_reg_gap(self, lens, codes, opt: Opt):
+        """One batch; returns (n_aln, flags, hits(H,9), stats[queries, pops]); mutates opt."""
+        n = len(lens)
+        n_aln = np.zeros(n, np.int32)
+        flags = np.zeros(n, np.uint32)
+        stats = np.zeros(2, np.uint64)
+        hp = C.POINTER(C.c_uint32)()
+        tot = lib().or_cal_sa_reg_gap(self.h, n, np.ascontiguousarray(lens, np.uint32),
+                                       np.ascontiguousarray(codes, np.uint8), C.byref(opt),
+                                       n_aln, flags, C.byref(hp), stats)
+        hits = np.ctypeslib.as_array(hp, shape=(max(tot, 1) * 9,))[:tot * 9].reshape(tot, 9).copy()
+        lib().or_free(hp)
+        return n_aln, flags, hits, stats
+
+    def run_batches(self, lens, codes, opt_dict, batch):
+        """bwa_aln_core's batch loop (bwtaln.c:477-506) over all reads."""
+        opt = Opt.from_dict(opt_dict)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+        outs = []
+        for b0 in range(0, len(lens), batch):
+            b1 = min(b0 + batch, len(lens))
+            outs.append(self.cal_sa_reg_gap(lens[b0:b1], codes[offs[b0]:offs[b1]], opt))
+        n_aln = np.concatenate([o[0] for o in outs])
+        flags = np.concatenate([o[1] for o in outs])
+        hits = np.concatenate([o[2] for o in outs]) if outs else np.zeros((0, 9), np.uint32)
+        stats = sum(o[3] for o in outs)
+        return n_aln, flags, hits, stats

@@ -1,0 +1,91 @@
+"""Pin the CPU restatement (oracle/) against the compiled reference's golden vectors."""
+import numpy as np
+import pytest
+
+from golden_io import INDEX, cases, load_case, parse_opts, split_hits
+from hsa_amd import index_io
+from oracle_ctypes import OracleIndex, default_opt
+
+_IDX = {}
+
+
+def oracle_index(name):
+    if name not in _IDX:
+        _IDX[name] = OracleIndex(*index_io.read_index(INDEX[name]))
+    return _IDX[name]
+
+
+def test_occ_matches_reference_all_positions():
+    from golden_io import GOLD
+    g = np.load(f"{GOLD}/tiny_occ.npz")
+    ix = oracle_index("tiny")
+    for d in (0, 1):
+        got = np.stack([ix.occ4(d, int(p)) for p in g["pos"]])
+        assert np.array_equal(got, g["occ"][d]), f"dir {d}"
+
+
+def test_occ_is_prefix_count():
+    """BWTOccValue == #{p < i - [i > isa0] : code[p] == c} (BWT.c:682-716)."""
+    fwd, rev = index_io.read_index(INDEX["rep"])
+    ix = oracle_index("rep")
+    for d, b in enumerate((fwd, rev)):
+        codes = index_io.unpack_codes(b)
+        pref = np.zeros((b.T + 1, 4), np.int64)
+        for c in range(4):
+            pref[1:, c] = np.cumsum(codes == c)
+        for i in list(range(0, 400)) + list(range(b.T - 300, b.T + 2)) + [b.isa0, b.isa0 + 1]:
+            j = i - (i > b.isa0)
+            assert np.array_equal(ix.occ4(d, i), pref[j]), (d, i)
+
+
+def test_width_matches_reference():
+    from golden_io import GOLD
+    g = np.load(f"{GOLD}/tiny_width.npz")
+    ix = oracle_index("tiny")
+    o = 0
+    w = g["width"]
+    for L in g["lens"]:
+        L = int(L)
+        seq = g["codes"][o:o + L]
+        got = ix.cal_width(seq)
+        exp = w[:L + 1]
+        w = w[L + 1:]
+        o += L
+        assert np.array_equal(got, exp)
+
+
+def test_step_consistency():
+    """rev_l - rev_k == l - k for every child of a bidirectional step (2BWT-Interface.c:266-269)."""
+    ix = oracle_index("tiny")
+    T = ix.fwd.T
+    k, l, rk, rl = 0, T, 0, T
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        ok, ol, ork, orl = ix.step_all(k, l, rk, rl)
+        for c in range(4):
+            if ok[c] <= ol[c]:
+                assert int(orl[c]) - int(ork[c]) == int(ol[c]) - int(ok[c])
+        c = int(rng.integers(4))
+        if ok[c] > ol[c]:
+            k, l, rk, rl = 0, T, 0, T
+        else:
+            k, l, rk, rl = int(ok[c]), int(ol[c]), int(ork[c]), int(orl[c])
+
+
+@pytest.mark.parametrize("name", sorted(cases().keys()))
+def test_batch_matches_reference(name):
+    """bwa_cal_sa_reg_gap restatement vs the reference on every golden case.
+
+    Reads the reference sent to bwt_splice_match (flags bit0) must be flagged the
+    same way; their splice hits are out of the oracle's scope, every
+    other read's hit list must be identical word for word, order included."""
+    g = load_case(name)
+    ix = oracle_index(g["index"])
+    opt = parse_opts(g["args"], default_opt())
+    n_aln, flags, hits, _ = ix.run_batches(g["lens"], g["codes"], opt, g["batch"])
+    exp_splice = (g["flags"] & 1).astype(bool)
+    assert np.array_equal((flags & 1).astype(bool), exp_splice)
+    got = split_hits(n_aln, hits)
+    exp = split_hits(g["n_aln"], g["hits"])
+    bad = [i for i in range(len(got)) if not exp_splice[i] and not np.array_equal(got[i], exp[i])]
+    assert not bad, f"{len(bad)} reads differ, first {bad[:5]}: got {got[bad[0]]} exp {exp[bad[0]]}"

@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the COMPILED REFERENCE.
+
+Test infrastructure.  Runs in the build container only (it needs
+/root/reference through oracle/_ref, built by `make -C oracle -f ref.mk`).
+Every fixture is data: synthetic inputs plus the reference's outputs on them.
+
+    python tools/make_golden.py            # tiny fixtures (committed)
+    python tools/make_golden.py --ecoli    # E.coli-sized digests (committed)
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from hsa_amd import synth  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref")
+GOLD = os.path.join(ROOT, "tests", "golden")
+INDEX_EXT = ["bwt", "fmv", "rev.bwt", "rev.fmv", "sa", "pac", "rev.pac", "ann"]
+
+
+def sh(*args, **kw):
+    return subprocess.run(list(args), check=True, capture_output=True, text=True, **kw)
+
+
+def build_index(fa: str) -> None:
+    d = os.path.dirname(fa)
+    sh(os.path.join(REF, "HSA"), "index", os.path.basename(fa), cwd=d)
+
+
+def run_aln(prefix: str, seqs: list[np.ndarray], args: list[str], work: str):
+    rb = os.path.join(work, "reads.bin")
+    ob = os.path.join(work, "out.bin")
+    synth.write_reads_bin(rb, seqs)
+    r = sh(os.path.join(REF, "ref_probe"), "aln", prefix, rb, ob, *args)
+    secs = float(r.stdout.strip().splitlines()[-1])
+    raw = open(ob, "rb").read()
+    n = int(np.frombuffer(raw[4:8], dtype=np.uint32)[0])
+    off = 8
+    n_aln = np.zeros(n, np.int32)
+    flags = np.zeros(n, np.uint32)
+    hits = []
+    for i in range(n):
+        na, fl = np.frombuffer(raw[off:off + 8], dtype=np.int32)
+        off += 8
+        n_aln[i] = na
+        flags[i] = fl
+        if na > 0:
+            hits.append(np.frombuffer(raw[off:off + 36 * na], dtype=np.uint32).reshape(na, 9))
+            off += 36 * na
+    hits = np.concatenate(hits) if hits else np.zeros((0, 9), np.uint32)
+    return n_aln, flags, hits, secs
+
+
+def pack_reads(seqs):
+    lens = np.array([len(s) for s in seqs], dtype=np.uint32)
+    codes = np.concatenate([np.asarray(s, np.uint8) for s in seqs]) if seqs else np.zeros(0, np.uint8)
+    return lens, codes
+
+
+def save_case(name, index, seqs, args, batch, n_aln, flags, hits):
+    lens, codes = pack_reads(seqs)
+    np.savez_compressed(os.path.join(GOLD, name + ".npz"), lens=lens, codes=codes,
+                        n_aln=n_aln, flags=flags, hits=hits,
+                        args=np.array(" ".join(args)), batch=np.int64(batch),
+                        index=np.array(index))
+    print(f"{name}: {len(seqs)} reads, {int((n_aln > 0).sum())} with hits, "
+          f"{hits.shape[0]} hits, {int(flags.sum())} splice calls")
+
+
+def hits_digest(n_aln, flags, hits) -> str:
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(n_aln, np.int32).tobytes())
+    h.update(np.ascontiguousarray(flags, np.uint32).tobytes())
+    h.update(np.ascontiguousarray(hits, np.uint32).tobytes())
+    return h.hexdigest()
+
+
+def repeat_genome(T: int, seed: int) -> np.ndarray:
+    """A repeat-rich text: random background, tandem repeats and near-copies."""
+    g = synth.genome_codes(T, seed).copy()
+    rng_words = synth.genome_words(4096, seed + 1)
+    bits = ((rng_words[:, None] >> (np.arange(0, 64, 2, dtype=np.uint64))) & np.uint64(3)).reshape(-1)
+    bits = bits.astype(np.int64)
+    p = 1000
+    k = 0
+    while p + 1200 < T:
+        kind = k % 3
+        if kind == 0:      # microsatellite (tandem unit 1-6 bp) of 60-200 bp
+            u = 1 + bits[k] % 6
+            unit = g[p:p + u].copy()
+            n = 60 + (bits[k + 1] * 16 + bits[k + 2]) % 140
+            g[p + u:p + u + n] = np.resize(unit, n)
+        elif kind == 1:    # exact copy of an earlier 300 bp segment
+            src = (bits[k + 3] * 997 + 31 * k) % max(p - 300, 1)
+            g[p:p + 300] = g[src:src + 300]
+        else:              # near-copy with 3 substitutions
+            src = (bits[k + 4] * 1231 + 17 * k) % max(p - 300, 1)
+            g[p:p + 300] = g[src:src + 300]
+            for j in range(3):
+                q = p + (bits[k + 5 + j] * 64 + bits[k + 8 + j]) % 300
+                g[q] = (g[q] + 1) % 4
+        p += 1500 + (bits[k + 11] * 256) % 900
+        k += 1
+    return g
+
+
+def edge_reads(genome, records, seed):
+    """Reads that hit the filters and odd branches of bwa_cal_sa_reg_gap."""
+    out = []
+    base, _ = synth.make_reads(genome, records, 40, 100, seed, max_mm=2)
+    for i in range(40):
+        r = base[i].copy()
+        if i % 8 == 0:
+            r[10] = 4                 # one N
+        elif i % 8 == 1:
+            r[5:11] = 4               # many N: skipped by the #N > max_diff filter (bwtaln.c:314)
+        elif i % 8 == 2:
+            r[:15] = 0                # first 15 all A (bwtaln.c:324)
+        elif i % 8 == 3:
+            r[:15] = 3                # first 15 all T
+        elif i % 8 == 4:
+            r[50] = 5                 # '-' maps to code 5 (bwaseqio.c:12)
+        elif i % 8 == 5:
+            r[97] = 4                 # N near the end of the read
+        elif i % 8 == 6:
+            r[:] = synth.genome_codes(100, seed * 31 + i)   # random: unmappable -> splice
+        out.append(r)
+    short, _ = synth.make_reads(genome, records, 6, 36, seed + 1, max_mm=2)
+    out += [short[i] for i in range(6)]
+    for L in (37, 50, 64, 75, 120, 150):
+        rr, _ = synth.make_reads(genome, records, 2, L, seed + L, max_mm=3)
+        out += [rr[0], rr[1]]
+    return out
+
+
+def tiny_cases(work):
+    T, seed = 200003, 7
+    g = synth.genome_codes(T, seed)
+    rec = synth.record_layout(T, 3)
+    fa = os.path.join(work, "tiny.fa")
+    synth.write_fasta(fa, g, rec)
+    build_index(fa)
+    idir = os.path.join(GOLD, "index")
+    os.makedirs(idir, exist_ok=True)
+    for e in INDEX_EXT:
+        shutil.copy(f"{fa}.index.{e}", os.path.join(idir, f"tiny.fa.index.{e}"))
+    prefix = fa
+
+    Tr = 50001
+    gr = repeat_genome(Tr, 11)
+    recr = synth.record_layout(Tr, 1)
+    far = os.path.join(work, "rep.fa")
+    synth.write_fasta(far, gr, recr)
+    build_index(far)
+    for e in INDEX_EXT:
+        shutil.copy(f"{far}.index.{e}", os.path.join(idir, f"rep.fa.index.{e}"))
+
+    cases = []
+    r, _ = synth.make_reads(g, rec, 2000, 36, 1)
+    cases.append(("tiny_exact36_n0", "tiny", list(r), ["-n", "0"], 100000))
+    r, _ = synth.make_reads(g, rec, 2000, 100, 5, max_mm=4)
+    cases.append(("tiny_mm100_n4o0", "tiny", list(r), ["-n", "4", "-o", "0"], 100000))
+    r, _ = synth.make_reads(g, rec, 1500, 100, 6, indel=True, max_mm_indel=2)
+    cases.append(("tiny_gap100_n4o1", "tiny", list(r), ["-n", "4", "-o", "1"], 100000))
+    # multi-batch with unmappable reads sprinkled in: the Q2 regime switch (bwtaln.c:363)
+    r, _ = synth.make_reads(g, rec, 1200, 100, 8, indel=True, max_mm_indel=2)
+    seqs = list(r)
+    for j in (3, 250, 611, 900):
+        seqs[j] = synth.genome_codes(100, 1000 + j)
+    cases.append(("tiny_gap100_n4o1_b400", "tiny", seqs, ["-n", "4", "-o", "1", "-B", "400"], 400))
+    # default options (-n 0.04 => per-length max_diff, GAPE semantics) on edge reads
+    seqs = edge_reads(g, rec, 21)
+    cases.append(("tiny_edge_default", "tiny", seqs, [], 100000))
+    cases.append(("tiny_edge_n3o1e3L", "tiny", seqs, ["-n", "3", "-o", "1", "-e", "3", "-L"], 100000))
+    r, _ = synth.make_reads(g, rec, 300, 75, 9, max_mm=3)
+    seqs = list(r)
+    cases.append(("tiny_opts_scores", "tiny", seqs, ["-n", "3", "-o", "1", "-M", "2", "-O", "7", "-E", "3", "-d", "3", "-i", "3"], 100000))
+    cases.append(("tiny_opts_seed", "tiny", seqs, ["-n", "4", "-o", "0", "-l", "20", "-k", "1"], 100000))
+    cases.append(("tiny_opts_maxentries", "tiny", seqs, ["-n", "4", "-o", "1", "-m", "40"], 100000))
+    # repeat-rich text: top-2 accounting, duplicate-hit suppression in tandem repeats, gap_shadow
+    r, _ = synth.make_reads(gr, recr, 800, 100, 12, max_mm=3)
+    cases.append(("rep_mm100_n4o1", "rep", list(r), ["-n", "4", "-o", "1"], 100000))
+    r, _ = synth.make_reads(gr, recr, 600, 60, 13, indel=True, max_mm_indel=1)
+    cases.append(("rep_gap60_default", "rep", list(r), [], 100000))
+    cases.append(("rep_gap60_R2", "rep", list(r), ["-n", "3", "-o", "1", "-R", "2"], 100000))
+    cases.append(("rep_gap60_nonstop", "rep", list(r)[:200], ["-n", "2", "-o", "1", "-N"], 100000))
+
+    manifest = {}
+    for name, idx, seqs, args, batch in cases:
+        pfx = prefix if idx == "tiny" else far
+        n_aln, flags, hits, secs = run_aln(pfx, seqs, args, work)
+        save_case(name, idx, seqs, args, batch, n_aln, flags, hits)
+        manifest[name] = {"index": idx, "args": args, "batch": batch, "n": len(seqs),
+                          "sha256": hits_digest(n_aln, flags, hits), "ref_seconds": secs}
+
+    # rank golden: BWTAllOccValue at boundary and random positions of both BWTs
+    isa0 = int(np.fromfile(f"{prefix}.index.bwt", dtype=np.uint32, count=1)[0])
+    risa0 = int(np.fromfile(f"{prefix}.index.rev.bwt", dtype=np.uint32, count=1)[0])
+    pos = set(range(0, 300)) | set(range(T - 300, T + 2))
+    for b in (isa0, risa0):
+        pos |= set(range(max(b - 3, 0), b + 4))
+    for m in range(0, T, 256):
+        pos |= {max(m - 129, 0), max(m - 128, 0), max(m - 127, 0), max(m - 1, 0), m, m + 1, min(m + 127, T + 1), min(m + 128, T + 1)}
+    rnd = (synth._u(99, 3000, 0) % np.uint64(T + 2)).astype(np.int64)
+    pos |= set(int(x) for x in rnd)
+    pos = np.array(sorted(p for p in pos if 0 <= p <= T + 1), dtype=np.uint32)
+    pb = os.path.join(work, "pos.bin")
+    with open(pb, "wb") as f:
+        f.write(np.uint32(len(pos)).tobytes())
+        f.write(pos.tobytes())
+    sh(os.path.join(REF, "ref_probe"), "occ", prefix, pb, os.path.join(work, "occ.bin"))
+    occ = np.fromfile(os.path.join(work, "occ.bin"), dtype=np.uint32).reshape(2, len(pos), 4)
+    np.savez_compressed(os.path.join(GOLD, "tiny_occ.npz"), pos=pos, occ=occ)
+    print(f"tiny_occ: {len(pos)} positions")
+
+    # width golden (bwt_cal_width type 1) on a few reads incl. N
+    seqs = edge_reads(g, rec, 21)[:24]
+    rb = os.path.join(work, "wr.bin")
+    synth.write_reads_bin(rb, seqs)
+    sh(os.path.join(REF, "ref_probe"), "width", prefix, rb, os.path.join(work, "w.bin"))
+    w = np.fromfile(os.path.join(work, "w.bin"), dtype=np.uint32).reshape(-1, 2)
+    lens, codes = pack_reads(seqs)
+    np.savez_compressed(os.path.join(GOLD, "tiny_width.npz"), lens=lens, codes=codes, width=w)
+    print(f"tiny_width: {len(seqs)} reads")
+
+    with open(os.path.join(GOLD, "manifest_tiny.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+
+
+def ecoli_cases(work):
+    """E.coli-sized (config 1 and two heavier flavours): digests only."""
+    T, seed = 4641652, 42
+    g = synth.genome_codes(T, seed)
+    rec = synth.record_layout(T, 1)
+    fa = os.path.join(work, "ecoli.fa")
+    synth.write_fasta(fa, g, rec)
+    build_index(fa)
+    man = {"genome": {"T": T, "seed": seed, "records": 1}, "index_sha256": {}}
+    for e in ["bwt", "fmv", "rev.bwt", "rev.fmv", "sa", "pac", "rev.pac"]:
+        man["index_sha256"][e] = hashlib.sha256(open(f"{fa}.index.{e}", "rb").read()).hexdigest()
+    cases = [("ecoli_exact36_n0", 10000, 36, 1, dict(), ["-n", "0"]),
+             ("ecoli_mm100_n4o0", 10000, 100, 5, dict(max_mm=4), ["-n", "4", "-o", "0"]),
+             ("ecoli_gap100_n4o1", 4000, 100, 6, dict(indel=True, max_mm_indel=2), ["-n", "4", "-o", "1"])]
+    for name, n, L, s, kw, args in cases:
+        r, _ = synth.make_reads(g, rec, n, L, s, **kw)
+        n_aln, flags, hits, secs = run_aln(fa, list(r), args, work)
+        man[name] = {"n": n, "L": L, "read_seed": s, "kw": kw, "args": args,
+                     "sha256": hits_digest(n_aln, flags, hits), "ref_seconds": secs,
+                     "reads_with_hits": int((n_aln > 0).sum()), "hits": int(hits.shape[0]),
+                     "splice_calls": int(flags.sum())}
+        print(name, man[name])
+    with open(os.path.join(GOLD, "manifest_ecoli.json"), "w") as f:
+        json.dump(man, f, indent=1, sort_keys=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ecoli", action="store_true")
+    a = ap.parse_args()
+    if not os.path.exists(os.path.join(REF, "ref_probe")):
+        sys.exit("build oracle/_ref first: make -C oracle -f ref.mk")
+    os.makedirs(GOLD, exist_ok=True)
+    with tempfile.TemporaryDirectory() as work:
+        if a.ecoli:
+            ecoli_cases(work)
+        else:
+            tiny_cases(work)
+
+
+if __name__ == "__main__":
+    main()
