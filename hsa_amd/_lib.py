@@ -1,0 +1,257 @@
+"""ctypes binding of libhsa_gpu.so (the MI355X search core and its drop-in C ABI).
+
+The library is built in-tree (hsa_amd/libhsa_gpu.so, `make -C hsa_amd/csrc`).
+There is no fallback: if the library or a GPU is missing every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhsa_gpu.so")
+
+HSA_F_FALLBACK = 1
+HSA_F_OVERFLOW = 2
+HSA_RF_NFILTER = 0x10
+HSA_RF_POLYAT = 0x20
+
+EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
+    "hsa_device_count", "hsa_last_error", "hsa_index_create", "hsa_index_create_device", "hsa_index_free",
+    "hsa_index_bytes", "hsa_index_device", "hsa_occ4_batch", "hsa_step_batch", "hsa_width_batch",
+    "hsa_search_batch", "hsa_search_device", "hsa_configure", "hsa_free", "hsa_synth_genome_device",
+    "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
+    "hsa_cal_sa_reg_gap_flat",
+]
+
+
+class HsaError(RuntimeError):
+    pass
+
+
+class GapOpt(C.Structure):
+    """gap_opt_t (bwtaln.h:133-143)."""
+    _fields_ = [("s_mm", C.c_int), ("s_gapo", C.c_int), ("s_gape", C.c_int), ("mode", C.c_int),
+                ("indel_end_skip", C.c_int), ("max_del_occ", C.c_int), ("max_entries", C.c_int),
+                ("fnr", C.c_float), ("max_diff", C.c_int), ("max_gapo", C.c_int), ("max_gape", C.c_int),
+                ("max_seed_diff", C.c_int), ("seed_len", C.c_int), ("n_threads", C.c_int),
+                ("max_top2", C.c_int), ("trim_qual", C.c_int)]
+
+    @classmethod
+    def default(cls):
+        """gap_init_opt (bwtaln.c:21-44)."""
+        return cls(s_mm=3, s_gapo=11, s_gape=4, mode=0x03, indel_end_skip=5, max_del_occ=10,
+                   max_entries=2000000, fnr=0.04, max_diff=-1, max_gapo=1, max_gape=6,
+                   max_seed_diff=2, seed_len=32, n_threads=1, max_top2=30, trim_qual=0)
+
+    @classmethod
+    def from_dict(cls, d):
+        o = cls()
+        for k, _ in cls._fields_:
+            setattr(o, k, d[k])
+        return o
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Regime(C.Structure):
+    _fields_ = [(k, C.c_int32) for k in ("s_mm", "s_gapo", "s_gape", "mode", "indel_end_skip", "max_del_occ",
+                                         "max_entries", "max_gapo", "max_gape", "max_seed_diff", "max_top2",
+                                         "n_stacks")]
+
+
+JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("max_diff", "<i4"), ("seed_len", "<i4"),
+                      ("regime", "<i4")])
+
+
+class Stats(C.Structure):
+    _fields_ = [("rank_queries", C.c_uint64), ("blocks_loaded", C.c_uint64), ("pops", C.c_uint64),
+                ("overflow_reruns", C.c_uint64), ("kernel_ms", C.c_double), ("main_kernel_ms", C.c_double),
+                ("main_launches", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class DeviceBatch(C.Structure):
+    _fields_ = [("d_jobs", C.c_void_p), ("n_jobs", C.c_int), ("d_codes", C.c_void_p), ("d_n_aln", C.c_void_p),
+                ("d_flags", C.c_void_p), ("d_hit_off", C.c_void_p), ("d_hits", C.c_void_p),
+                ("hit_cap", C.c_uint64), ("d_counters", C.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HsaError(f"{LIB_PATH} is missing: build it with `make -C hsa_amd/csrc` (no CPU fallback exists)")
+    L = C.CDLL(LIB_PATH)
+    u32 = np.ctypeslib.ndpointer(np.uint32, flags="C")
+    u64 = np.ctypeslib.ndpointer(np.uint64, flags="C")
+    i32 = np.ctypeslib.ndpointer(np.int32, flags="C")
+    u8 = np.ctypeslib.ndpointer(np.uint8, flags="C")
+    vp = C.c_void_p
+    L.hsa_device_count.restype = C.c_int
+    L.hsa_last_error.restype = C.c_char_p
+    L.hsa_index_create.argtypes = [C.c_int, C.c_uint32, C.c_uint32, u32, u32, C.c_uint32, C.c_uint32, u32, u32,
+                                   C.POINTER(vp)]
+    L.hsa_index_create_device.argtypes = [C.c_int, C.c_uint32, C.c_uint32, u32, vp, C.c_uint32, C.c_uint32, u32, vp,
+                                          C.POINTER(vp)]
+    L.hsa_index_free.argtypes = [vp]
+    L.hsa_index_bytes.restype = C.c_size_t
+    L.hsa_index_bytes.argtypes = [vp]
+    L.hsa_occ4_batch.argtypes = [vp, C.c_int, C.c_size_t, u32, u32]
+    L.hsa_step_batch.argtypes = [vp, C.c_size_t, u32, u32]
+    L.hsa_width_batch.argtypes = [vp, C.c_size_t, u64, u32, u8, C.c_size_t, u32]
+    L.hsa_search_batch.restype = C.c_long
+    L.hsa_search_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, C.c_int, u8, C.c_size_t, i32, u32, u64,
+                                   C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(Stats)]
+    L.hsa_search_device.argtypes = [vp, C.POINTER(Regime), C.c_int, C.POINTER(DeviceBatch), vp]
+    L.hsa_configure.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.hsa_free.argtypes = [vp]
+    L.hsa_synth_genome_device.argtypes = [C.c_int, C.c_uint64, C.c_uint64, vp]
+    L.hsa_build_bwt_device.argtypes = [C.c_int, C.c_uint64, vp, C.c_int, vp, C.POINTER(C.c_uint32), u32]
+    L.hsa_cal_sa_reg_gap_flat.restype = C.c_long
+    L.hsa_cal_sa_reg_gap_flat.argtypes = [vp, C.POINTER(GapOpt), C.c_int, u32, u64, u8, C.c_size_t, i32, u32, u64,
+                                          C.POINTER(C.POINTER(C.c_uint32)), i32, C.POINTER(Stats)]
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc < 0:
+        raise HsaError(f"libhsa_gpu error {rc}: {lib().hsa_last_error().decode()}")
+    return rc
+
+
+def device_count() -> int:
+    return lib().hsa_device_count()
+
+
+def configure(waves_per_cu=0, pool_entries=0, hit_cap=0):
+    check(lib().hsa_configure(waves_per_cu, pool_entries, hit_cap))
+
+
+def _take_hits(hp, n):
+    if n == 0:
+        lib().hsa_free(hp)
+        return np.zeros((0, 9), np.uint32)
+    arr = np.ctypeslib.as_array(hp, shape=(n * 9,)).reshape(n, 9).copy()
+    lib().hsa_free(hp)
+    return arr
+
+
+class GpuIndex:
+    """The bidirectional index resident in HBM as rank blocks (one device)."""
+
+    def __init__(self, fwd, rev, device: int = 0):
+        self.T = fwd.T
+        self.fwd_meta = fwd
+        h = C.c_void_p()
+        check(lib().hsa_index_create(device, fwd.T, fwd.isa0, np.ascontiguousarray(fwd.C, np.uint32),
+                                     np.ascontiguousarray(fwd.code, np.uint32), rev.T, rev.isa0,
+                                     np.ascontiguousarray(rev.C, np.uint32),
+                                     np.ascontiguousarray(rev.code, np.uint32), C.byref(h)))
+        self.h = h
+
+    @classmethod
+    def from_device_codes(cls, T, isa0, Cf, d_code, rT, risa0, Cr, d_rcode, device=0):
+        self = cls.__new__(cls)
+        self.T = T
+        h = C.c_void_p()
+        check(lib().hsa_index_create_device(device, T, isa0, np.ascontiguousarray(Cf, np.uint32), d_code, rT, risa0,
+                                            np.ascontiguousarray(Cr, np.uint32), d_rcode, C.byref(h)))
+        self.h = h
+        return self
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().hsa_index_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def nbytes(self) -> int:
+        return int(lib().hsa_index_bytes(self.h))
+
+    def occ4(self, d, pos):
+        pos = np.ascontiguousarray(pos, np.uint32)
+        out = np.zeros((len(pos), 4), np.uint32)
+        check(lib().hsa_occ4_batch(self.h, d, len(pos), pos, out))
+        return out
+
+    def step_all(self, klrr):
+        klrr = np.ascontiguousarray(klrr, np.uint32).reshape(-1, 4)
+        out = np.zeros((len(klrr), 16), np.uint32)
+        check(lib().hsa_step_batch(self.h, len(klrr), klrr, out))
+        return out.reshape(-1, 4, 4)   # [n][k, l, rk, rl][c]
+
+    def widths(self, lens, codes):
+        lens = np.ascontiguousarray(lens, np.uint32)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
+        tot = int(np.sum(2 * (lens.astype(np.int64) + 1)))
+        out = np.zeros(tot, np.uint32)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        check(lib().hsa_width_batch(self.h, len(lens), offs, lens, codes, len(codes), out))
+        return out
+
+    def search(self, regimes, jobs, codes):
+        """Raw search over a job table (JOB_DTYPE)."""
+        jobs = np.ascontiguousarray(jobs, JOB_DTYPE)
+        n = len(jobs)
+        rg = (Regime * len(regimes))(*regimes)
+        n_aln = np.zeros(n, np.int32)
+        flags = np.zeros(n, np.uint32)
+        hoff = np.zeros(n, np.uint64)
+        hp = C.POINTER(C.c_uint32)()
+        st = Stats()
+        codes = np.ascontiguousarray(codes, np.uint8)
+        tot = check(lib().hsa_search_batch(self.h, rg, len(regimes), jobs.ctypes.data, n, codes, len(codes), n_aln,
+                                           flags, hoff, C.byref(hp), C.byref(st)))
+        return n_aln, flags, hoff, _take_hits(hp, tot), st.as_dict()
+
+    def cal_sa_reg_gap(self, lens, codes, opt: GapOpt):
+        """bwa_cal_sa_reg_gap semantics over one batch (mutates opt like the reference)."""
+        lens = np.ascontiguousarray(lens, np.uint32)
+        n = len(lens)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64) if n else \
+            np.zeros(0, np.uint64)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        n_aln = np.zeros(n, np.int32)
+        flags = np.zeros(n, np.uint32)
+        hoff = np.zeros(n, np.uint64)
+        sp = np.zeros(2 * n + 2, np.int32)
+        hp = C.POINTER(C.c_uint32)()
+        st = Stats()
+        tot = check(lib().hsa_cal_sa_reg_gap_flat(self.h, C.byref(opt), n, lens, offs, codes, len(codes), n_aln,
+                                                  flags, hoff, C.byref(hp), sp, C.byref(st)))
+        hits = _take_hits(hp, tot)
+        return n_aln, flags, hoff, hits, st.as_dict()
+
+    def run_batches(self, lens, codes, opt_dict, batch):
+        """bwa_aln_core's batch loop (bwtaln.c:477-506); hits regrouped in read order."""
+        opt = GapOpt.from_dict(opt_dict)
+        lens = np.asarray(lens, np.uint32)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+        na_all, fl_all, per_read, stats = [], [], [], []
+        for b0 in range(0, len(lens), batch):
+            b1 = min(b0 + batch, len(lens))
+            na, fl, ho, hits, st = self.cal_sa_reg_gap(lens[b0:b1], codes[offs[b0]:offs[b1]], opt)
+            for j in range(b1 - b0):
+                per_read.append(hits[int(ho[j]):int(ho[j]) + max(int(na[j]), 0)])
+            na_all.append(na)
+            fl_all.append(fl)
+            stats.append(st)
+        n_aln = np.concatenate(na_all) if na_all else np.zeros(0, np.int32)
+        flags = np.concatenate(fl_all) if fl_all else np.zeros(0, np.uint32)
+        return n_aln, flags, per_read, stats

@@ -1,0 +1,391 @@
+/*
+ * bwtaln_gpu.c -- host side of the drop-in: bwa_cal_sa_reg_gap (bwtaln.c:246-417)
+ * on top of the MI355X search core (hsa_gpu.h).
+ *
+ * What stays on the host is the part of bwa_cal_sa_reg_gap that is sequential by
+ * construction and costs O(read length): the option-block side effects, the two
+ * read filters, and the choice of option regime per read.  The searches
+ * themselves (widths + bwt_match_gap on both strands) run on the GPU.
+ *
+ * The option regimes.  The reference copies local_opt = *opt
+ * (:254) BEFORE clearing BWA_MODE_GAPE through aux->opt (:261), writes per-read
+ * max_diff/seed_len through aux->opt (:330-332), and after the first read that
+ * falls back to splicing points aux->opt at local_opt for the rest of the call
+ * (:363).  So a call runs reads [0, f] with regime A (the caller's block) and
+ * reads (f, n) with regime B (local_opt), f being the first fallback read.  f is
+ * only known after searching, hence: search a first chunk in regime A, find f,
+ * search the rest in regime B.  When the two regimes cannot differ for any read
+ * (same effective options, equal read lengths) the whole call is one launch.
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/hsa_bwtaln.h"
+
+_Static_assert(sizeof(bwt_aln1_t) == 36, "bwt_aln1_t layout");
+_Static_assert(sizeof(gap_opt_t) == 64, "gap_opt_t layout");
+_Static_assert(sizeof(bwa_seq_t) == 208, "bwa_seq_t layout");
+_Static_assert(sizeof(bwt_aux_t) == 96, "bwt_aux_t layout");
+_Static_assert(sizeof(BWT) == 128, "BWT layout");
+_Static_assert(sizeof(Idx2BWT) == 544, "Idx2BWT layout");
+_Static_assert(sizeof(gap_entry_t) == 28, "gap_entry_t layout");
+
+#define BWA_AVG_ERR 0.02
+#define SEED_NONE 0x7fffffff
+#define CHUNK0 8192
+
+/* bwa_cal_maxdiff (bwtaln.c:46-58) */
+static int cal_maxdiff(int l, double err, double thres)
+{
+    double elambda = exp(-l * err);
+    double sum, y = 1.0;
+    int k, x = 1;
+    for (k = 1, sum = elambda; k < 1000; ++k) {
+        y *= l * err;
+        x *= k;
+        sum += elambda * y / x;
+        if (1.0 - sum < thres) return k;
+    }
+    return 2;
+}
+
+static int aln_score(const gap_opt_t *o, int m, int g, int e) { return m * o->s_mm + g * o->s_gapo + e * o->s_gape; }
+
+static hsa_regime_t regime_of(const gap_opt_t *o, int n_stacks)
+{
+    hsa_regime_t r;
+    memset(&r, 0, sizeof r);
+    r.s_mm = o->s_mm; r.s_gapo = o->s_gapo; r.s_gape = o->s_gape;
+    r.mode = o->mode & (BWA_MODE_GAPE | BWA_MODE_LOGGAP | BWA_MODE_NONSTOP);
+    /* without gap opens no entry ever leaves state M: GAPE and LOGGAP are inert */
+    if (o->max_gapo == 0) r.mode &= ~(BWA_MODE_GAPE | BWA_MODE_LOGGAP);
+    r.indel_end_skip = o->indel_end_skip; r.max_del_occ = o->max_del_occ; r.max_entries = o->max_entries;
+    r.max_gapo = o->max_gapo; r.max_gape = o->max_gape;
+    r.max_seed_diff = o->max_seed_diff; r.max_top2 = o->max_top2;
+    r.n_stacks = n_stacks;
+    return r;
+}
+
+/* The mutable option fields the per-read loop reads and writes. */
+typedef struct { int opt_max_diff, opt_seed, loc_max_diff, loc_seed; } optstate_t;
+
+enum { K_JOB = 0, K_NFILTER = 1, K_POLYAT = 2 };
+
+/* One read of the bwtaln.c:303-337 prologue under regime `cur` (0 = A, 1 = B). */
+static int plan_read(const gap_opt_t *caller, int cur, optstate_t *st, const uint8_t *seq, int len,
+                     int32_t *max_diff, int32_t *seed_len)
+{
+    int nN = 0;
+    for (int j = 0; j < len; ++j) nN += seq[j] > 3;
+    if (nN > st->loc_max_diff) return K_NFILTER;                      /* :314-317 */
+    if (len >= 15) {                                                    /* :324-325 */
+        int a = 1, t = 1;
+        for (int j = 0; j < 15; ++j) { a &= seq[j] == 0; t &= seq[j] == 3; }
+        if (a || t) return K_POLYAT;
+    }
+    int *md = cur ? &st->loc_max_diff : &st->opt_max_diff;
+    int *sl = cur ? &st->loc_seed : &st->opt_seed;
+    if (caller->fnr > 0.0) *md = cal_maxdiff(len, BWA_AVG_ERR, caller->fnr);   /* :330-331 */
+    *sl = st->opt_seed < len ? st->opt_seed : SEED_NONE;                       /* :332 */
+    *max_diff = *md;
+    *seed_len = *sl;
+    return K_JOB;
+}
+
+typedef struct {
+    uint32_t *h; size_t n, cap;
+} hitbuf_t;
+
+static int hb_append(hitbuf_t *b, const uint32_t *src, size_t n)
+{
+    if (b->n + n > b->cap) {
+        size_t c = (b->n + n) * 2 + 64;
+        uint32_t *p = (uint32_t *)realloc(b->h, c * 36);
+        if (!p) return -1;
+        b->h = p; b->cap = c;
+    }
+    memcpy(b->h + b->n * 9, src, n * 36);
+    b->n += n;
+    return 0;
+}
+
+/* Search the reads [r0, r1) whose kind is K_JOB; results into the per-read outputs. */
+static int search_range(hsa_index_t *ix, const hsa_regime_t *rg, int r0, int r1, const int8_t *kind,
+                        const int32_t *jmd, const int32_t *jsl, int regime, const uint32_t *lens, const uint64_t *offs,
+                        const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags, uint64_t *hit_off,
+                        hitbuf_t *hb, hsa_stats_t *stats)
+{
+    int n = 0;
+    for (int r = r0; r < r1; ++r) n += kind[r] == K_JOB;
+    if (n == 0) return 0;
+    hsa_job_t *jobs = (hsa_job_t *)malloc(sizeof(hsa_job_t) * n);
+    int *map = (int *)malloc(sizeof(int) * n);
+    int32_t *na = (int32_t *)malloc(sizeof(int32_t) * n);
+    uint32_t *fl = (uint32_t *)malloc(sizeof(uint32_t) * n);
+    uint64_t *ho = (uint64_t *)malloc(sizeof(uint64_t) * n);
+    int q = 0;
+    for (int r = r0; r < r1; ++r) {
+        if (kind[r] != K_JOB) continue;
+        jobs[q].off = offs[r]; jobs[q].len = lens[r]; jobs[q].max_diff = jmd[r]; jobs[q].seed_len = jsl[r];
+        jobs[q].regime = 0;
+        map[q++] = r;
+    }
+    uint32_t *h = NULL;
+    hsa_stats_t s1;
+    long tot = hsa_search_batch(ix, rg + regime, 1, jobs, n, codes, codes_len, na, fl, ho, &h, &s1);
+    if (tot < 0) { free(jobs); free(map); free(na); free(fl); free(ho); return (int)tot; }
+    size_t base = hb->n;
+    if (hb_append(hb, h, (size_t)tot)) { hsa_free(h); free(jobs); free(map); free(na); free(fl); free(ho); return HSA_E_MEM; }
+    hsa_free(h);
+    for (int j = 0; j < n; ++j) {
+        int r = map[j];
+        n_aln[r] = na[j]; flags[r] = fl[j]; hit_off[r] = ho[j] + base;
+    }
+    if (stats) {
+        stats->rank_queries += s1.rank_queries; stats->blocks_loaded += s1.blocks_loaded; stats->pops += s1.pops;
+        stats->overflow_reruns += s1.overflow_reruns; stats->kernel_ms += s1.kernel_ms;
+        stats->main_kernel_ms += s1.main_kernel_ms; stats->main_launches += s1.main_launches;
+    }
+    free(jobs); free(map); free(na); free(fl); free(ho);
+    return 0;
+}
+
+long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint32_t *lens, const uint64_t *offs,
+                             const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
+                             uint64_t *hit_off, uint32_t **hits, int32_t *splice_opt, hsa_stats_t *stats)
+{
+    *hits = NULL;
+    if (stats) memset(stats, 0, sizeof *stats);
+    gap_opt_t local = *opt;                                 /* :254 */
+    opt->mode &= ~BWA_MODE_GAPE;                            /* :261 through aux->opt */
+    int max_len = 0, same_len = 1;
+    for (int r = 0; r < n; ++r) {
+        if ((int)lens[r] > max_len) max_len = (int)lens[r];
+        if (lens[r] != lens[0]) same_len = 0;
+    }
+    if (opt->fnr > 0.0) local.max_diff = cal_maxdiff(max_len, BWA_AVG_ERR, opt->fnr);
+    if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;
+    const int n_stacks = aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
+    hsa_regime_t rg[2] = {regime_of(opt, n_stacks), regime_of(&local, n_stacks)};
+    const int equivalent = same_len && memcmp(&rg[0], &rg[1], sizeof rg[0]) == 0;
+
+    int8_t *kind = (int8_t *)malloc((size_t)n + 1);
+    int32_t *jmd = (int32_t *)malloc(sizeof(int32_t) * ((size_t)n + 1));
+    int32_t *jsl = (int32_t *)malloc(sizeof(int32_t) * ((size_t)n + 1));
+    hitbuf_t hb = {NULL, 0, 0};
+    const optstate_t st0 = {opt->max_diff, opt->seed_len, local.max_diff, local.seed_len};
+    optstate_t st = st0;
+    int rc = 0, pos = 0, cur = 0, f_switch = -1;
+    for (int r = 0; r < n; ++r) { n_aln[r] = 0; flags[r] = 0; hit_off[r] = 0; }
+
+    while (pos < n && rc == 0) {
+        if (cur == 0) {
+            const int end = equivalent ? n : (pos + CHUNK0 < n ? pos + CHUNK0 : n);
+            const optstate_t saved = st;
+            for (int r = pos; r < end; ++r)
+                kind[r] = (int8_t)plan_read(opt, 0, &st, codes + offs[r], (int)lens[r], &jmd[r], &jsl[r]);
+            rc = search_range(ix, rg, pos, end, kind, jmd, jsl, 0, lens, offs, codes, codes_len, n_aln, flags,
+                              hit_off, &hb, stats);
+            if (rc) break;
+            int f = -1;
+            for (int r = pos; r < end; ++r)
+                if (kind[r] == K_JOB && (flags[r] & HSA_F_FALLBACK)) { f = r; break; }
+            if (f >= 0) f_switch = f;
+            if (f < 0 || equivalent) { pos = end; continue; }
+            /* regime switch after read f: reads (f, end) are searched again in regime B */
+            st = saved;
+            for (int r = pos; r <= f; ++r)
+                kind[r] = (int8_t)plan_read(opt, 0, &st, codes + offs[r], (int)lens[r], &jmd[r], &jsl[r]);
+            for (int r = f + 1; r < end; ++r) { n_aln[r] = 0; flags[r] = 0; hit_off[r] = 0; }
+            cur = 1;
+            pos = f + 1;
+        } else {
+            for (int r = pos; r < n; ++r)
+                kind[r] = (int8_t)plan_read(opt, 1, &st, codes + offs[r], (int)lens[r], &jmd[r], &jsl[r]);
+            rc = search_range(ix, rg, pos, n, kind, jmd, jsl, 1, lens, offs, codes, codes_len, n_aln, flags,
+                              hit_off, &hb, stats);
+            pos = n;
+        }
+    }
+    if (rc == 0) {
+        /* replay the sequential prologue with the now-known switch point: final
+         * option state, and the local_opt fields each fallback read's splice sees */
+        optstate_t s = st0;
+        int c = 0;
+        for (int r = 0; r < n; ++r) {
+            int32_t a, b;
+            const int k = plan_read(opt, c, &s, codes + offs[r], (int)lens[r], &a, &b);
+            if (k == K_NFILTER) flags[r] = HSA_RF_NFILTER;
+            else if (k == K_POLYAT) flags[r] = HSA_RF_POLYAT;
+            if (splice_opt) { splice_opt[2 * r] = s.loc_max_diff; splice_opt[2 * r + 1] = s.loc_seed; }
+            if (r == f_switch) c = 1;
+        }
+        opt->max_diff = s.opt_max_diff;
+        opt->seed_len = s.opt_seed;
+        *hits = hb.h ? hb.h : (uint32_t *)calloc(9, 4);
+    } else {
+        free(hb.h);
+    }
+    free(kind); free(jmd); free(jsl);
+    return rc ? rc : (long)hb.n;
+}
+
+/* ------------------------------------------------------------------ reference ABI */
+
+#define MAX_ATTACH 16
+static struct { const Idx2BWT *key; hsa_index_t *ix; } g_att[MAX_ATTACH];
+static pthread_mutex_t g_att_mu = PTHREAD_MUTEX_INITIALIZER;
+static int g_device = 0;
+
+static hsa_index_t *lookup(const Idx2BWT *bi)
+{
+    for (int i = 0; i < MAX_ATTACH; ++i) if (g_att[i].key == bi) return g_att[i].ix;
+    return NULL;
+}
+
+int hsa_gpu_set_devices(int n)
+{
+    int have = hsa_device_count();
+    if (n < 1 || n > have) return HSA_E_ARG;
+    return 0;
+}
+
+/* Upload the bidirectional BWT of a loaded Idx2BWT once (hook after BWTLoad2BWT). */
+int hsa_gpu_attach(const Idx2BWT *bi)
+{
+    pthread_mutex_lock(&g_att_mu);
+    if (lookup(bi)) { pthread_mutex_unlock(&g_att_mu); return 0; }
+    int slot = -1;
+    for (int i = 0; i < MAX_ATTACH; ++i) if (!g_att[i].key) { slot = i; break; }
+    if (slot < 0) { pthread_mutex_unlock(&g_att_mu); return HSA_E_ARG; }
+    const BWT *f = bi->bwt, *r = bi->rev_bwt;
+    hsa_index_t *ix = NULL;
+    int rc = hsa_index_create(g_device, f->textLength, f->inverseSa0, f->cumulativeFreq, f->bwtCode,
+                              r->textLength, r->inverseSa0, r->cumulativeFreq, r->bwtCode, &ix);
+    if (rc == 0) { g_att[slot].key = bi; g_att[slot].ix = ix; }
+    pthread_mutex_unlock(&g_att_mu);
+    return rc;
+}
+
+void hsa_gpu_detach(const Idx2BWT *bi)
+{
+    pthread_mutex_lock(&g_att_mu);
+    for (int i = 0; i < MAX_ATTACH; ++i)
+        if (g_att[i].key == bi) { hsa_index_free(g_att[i].ix); g_att[i].key = NULL; g_att[i].ix = NULL; }
+    pthread_mutex_unlock(&g_att_mu);
+}
+
+/* gap_init_stack layout (bwtgap.c:13-27), for the host's bwt_splice_match */
+static gap_stack_t *ref_stack_new(int n_stacks)
+{
+    gap_stack_t *s = (gap_stack_t *)calloc(1, sizeof(gap_stack_t));
+    s->n_stacks = n_stacks;
+    s->stacks = (gap_stack1_t *)calloc(n_stacks, sizeof(gap_stack1_t));
+    for (int i = 0; i < n_stacks; ++i) {
+        s->stacks[i].m_entries = 4;
+        s->stacks[i].stack = (gap_entry_t *)calloc(4, sizeof(gap_entry_t));
+    }
+    return s;
+}
+
+static void ref_stack_free(gap_stack_t *s)
+{
+    for (int i = 0; i < s->n_stacks; ++i) free(s->stacks[i].stack);
+    free(s->stacks);
+    free(s);
+}
+
+static void fatal(const char *what, long rc)
+{
+    /* the reference's convention for unrecoverable errors: message + exit(1) */
+    fprintf(stderr, "[bwa_cal_sa_reg_gap] %s failed (%ld): %s\n", what, rc, hsa_last_error());
+    exit(1);
+}
+
+void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, const gap_opt_t *copt,
+                        struct bwt_array_t *arr)
+{
+    (void)tid;
+    gap_opt_t *opt = (gap_opt_t *)copt;     /* mutated, as the reference does through aux->opt */
+    hsa_index_t *ix = lookup(bi_bwt);
+    if (!ix) {
+        long rc = hsa_gpu_attach(bi_bwt);
+        if (rc) fatal("hsa_gpu_attach", rc);
+        ix = lookup(bi_bwt);
+    }
+    uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)n_seqs + 1));
+    uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n_seqs + 1));
+    size_t tot = 0;
+    int max_len = 0;
+    for (int i = 0; i < n_seqs; ++i) {
+        lens[i] = seqs[i].len; offs[i] = tot; tot += seqs[i].len;
+        if ((int)seqs[i].len > max_len) max_len = (int)seqs[i].len;
+    }
+    uint8_t *codes = (uint8_t *)malloc(tot + 1);
+    for (int i = 0; i < n_seqs; ++i) memcpy(codes + offs[i], seqs[i].seq, seqs[i].len);
+    int32_t *n_aln = (int32_t *)malloc(sizeof(int32_t) * ((size_t)n_seqs + 1));
+    uint32_t *flags = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)n_seqs + 1));
+    uint64_t *hoff = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n_seqs + 1));
+    int32_t *sp = (int32_t *)malloc(sizeof(int32_t) * 2 * ((size_t)n_seqs + 1));
+    gap_opt_t local = *opt;                 /* local_opt as of :254, before the call mutates *opt */
+    uint32_t *hits = NULL;
+    long nh = hsa_cal_sa_reg_gap_flat(ix, opt, n_seqs, lens, offs, codes, tot, n_aln, flags, hoff, &hits, sp, NULL);
+    if (nh < 0) fatal("GPU search", nh);
+    if (opt->fnr > 0.0) local.max_diff = cal_maxdiff(max_len, BWA_AVG_ERR, opt->fnr);
+    if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;
+
+    /* splice fallback state, built lazily (bwtaln.c:264-291) */
+    bwt_aux_t aux;
+    memset(&aux, 0, sizeof aux);
+    int have_splice = bwt_splice_match != NULL;
+    for (int i = 0; i < n_seqs; ++i) {
+        bwa_seq_t *p = seqs + i;
+        if (flags[i] & HSA_RF_NFILTER) continue;               /* untouched (:314-317) */
+        p->sa = 0; p->type = 0; p->c1 = p->c2 = 0; p->n_aln = 0; p->aln = 0;
+        if (flags[i] & HSA_RF_POLYAT) continue;
+        if (n_aln[i] > 0) {
+            int cap = n_aln[i] > 10 ? n_aln[i] : 10;           /* bwt_match_gap's calloc'd array */
+            p->aln = (bwt_aln1_t *)calloc(cap, sizeof(bwt_aln1_t));
+            memcpy(p->aln, hits + hoff[i] * 9, sizeof(bwt_aln1_t) * n_aln[i]);
+            p->n_aln = n_aln[i];
+            continue;
+        }
+        if (!(flags[i] & HSA_F_FALLBACK) || !have_splice) continue;
+        if (!aux.stack) {
+            aux.bi_bwt = (Idx2BWT *)bi_bwt;
+            aux.arr = arr;
+            aux.max_len = max_len;
+            aux.width_back = (bwt_width_t *)calloc(max_len + 1, sizeof(bwt_width_t));
+            aux.width_fore = (bwt_width_t *)calloc(max_len + 1, sizeof(bwt_width_t));
+            aux.width_seed = (bwt_width_t *)calloc(max_len + 1, sizeof(bwt_width_t));
+            aux.rc_seq = (ubyte_t *)calloc(max_len + 1, 1);
+            aux.stack = ref_stack_new(local.s_mm * (local.max_diff + 1) + local.s_gapo * (local.max_gapo + 1) +
+                                      local.s_gape * (local.max_gape + 1));
+        }
+        gap_opt_t lo = local;                                   /* aux->opt = &local_opt (:363) */
+        lo.max_diff = sp[2 * i];
+        lo.seed_len = sp[2 * i + 1];
+        aux.opt = &lo;
+        aux.seq = p->seq;
+        aux.len = (int)p->len;
+        aux.strand = 0;
+        memset(aux.rc_seq, 0, (size_t)max_len);
+        for (int j = 0; j < (int)p->len; ++j) {
+            ubyte_t c = p->seq[p->len - 1 - j];
+            aux.rc_seq[j] = c < 4 ? (ubyte_t)(3 - c) : c;
+        }
+        int na = 0;
+        p->aln = bwt_splice_match(&aux, &na);
+        p->n_aln = na;
+        if (na == 0) { free(p->aln); p->aln = NULL; }
+    }
+    if (aux.stack) {
+        free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);
+        ref_stack_free(aux.stack);
+    }
+    hsa_free(hits);
+    free(lens); free(offs); free(codes); free(n_aln); free(flags); free(hoff); free(sp);
+}

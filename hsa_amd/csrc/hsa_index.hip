@@ -1,0 +1,411 @@
+// hsa_index.hip -- device index (rank blocks) and the rank/step/width primitives.
+//
+// The reference keeps, per BWT direction, a 2-bit code array plus two sampled
+// Occ tables (occValue every 256 chars as 16-bit pairs, occValueMajor every 65 536;
+// BWT.c:1018-1059) and answers a rank with two dependent-ish loads and an SSE
+// popcount (BWT.c:532-679).  Here one 64-byte block carries both the absolute
+// counts and the 192 codes they cover, so one rank query = one 64-byte fetch.
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hsa_device.h"
+#include "hsa_internal.h"
+
+static thread_local char g_err[1024] = "";
+int g_waves_per_cu = 16;
+int g_pool_entries = 8192;
+int g_hit_cap = 64;
+
+void hsa_set_error(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+extern "C" const char *hsa_last_error(void) { return g_err; }
+
+extern "C" int hsa_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" void hsa_free(void *p) { free(p); }
+
+extern "C" int hsa_configure(int waves_per_cu, int pool_entries, int hit_cap)
+{
+    if (waves_per_cu > 0) g_waves_per_cu = waves_per_cu;
+    if (pool_entries > 0) {
+        if (pool_entries > 65535) { hsa_set_error("pool_entries > 65535"); return HSA_E_ARG; }
+        g_pool_entries = pool_entries;
+    }
+    if (hit_cap > 0) g_hit_cap = hit_cap;
+    return 0;
+}
+
+int hsa_grow(void **p, size_t *cap, size_t need)
+{
+    if (need <= *cap && *p) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    size_t n = need + need / 4 + 4096;
+    if (hipMalloc(p, n) != hipSuccess) {
+        *p = nullptr; *cap = 0;
+        hsa_set_error("hipMalloc(%zu) failed", n);
+        return HSA_E_MEM;
+    }
+    *cap = n;
+    return 0;
+}
+
+void hsa_scratch_free(SearchScratch &s)
+{
+    (void)hipFree(s.width); (void)hipFree(s.pool); (void)hipFree(s.nxt); (void)hipFree(s.hbuf);
+    s = SearchScratch();
+}
+
+int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t wcap, size_t pcap, size_t hcap)
+{
+    if (lanes <= s.lanes && wcap <= s.wcap && pcap <= s.pcap && hcap <= s.hcap && s.width) return 0;
+    lanes = lanes > s.lanes ? lanes : s.lanes;
+    wcap = wcap > s.wcap ? wcap : s.wcap;
+    pcap = pcap > s.pcap ? pcap : s.pcap;
+    hcap = hcap > s.hcap ? hcap : s.hcap;
+    hsa_scratch_free(s);
+    if (hipMalloc(&s.width, lanes * wcap * sizeof(uint2)) != hipSuccess ||
+        hipMalloc(&s.pool, lanes * pcap * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(&s.nxt, lanes * pcap * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&s.hbuf, lanes * hcap * 9 * sizeof(uint32_t)) != hipSuccess) {
+        hsa_set_error("scratch allocation failed (lanes %zu, pool %zu, hits %zu)", lanes, pcap, hcap);
+        hsa_scratch_free(s);
+        return HSA_E_MEM;
+    }
+    s.lanes = lanes; s.wcap = wcap; s.pcap = pcap; s.hcap = hcap;
+    return 0;
+}
+
+// ---------------------------------------------------------------- layout build
+__global__ void k_msb_to_lsb(uint32_t *w, size_t n, uint32_t T)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t x = w[i];
+    x = (x >> 16) | (x << 16);
+    x = ((x & 0xFF00FF00u) >> 8) | ((x & 0x00FF00FFu) << 8);
+    x = ((x & 0xF0F0F0F0u) >> 4) | ((x & 0x0F0F0F0Fu) << 4);
+    x = ((x & 0xCCCCCCCCu) >> 2) | ((x & 0x33333333u) << 2);
+    if (i == n - 1 && (T & 15)) x &= (1u << (2 * (T & 15))) - 1u;   // BWTClearTrailingBwtCode
+    w[i] = x;
+}
+
+struct U4 { uint32_t a, b, c, d; };
+struct U4Plus {
+    __host__ __device__ U4 operator()(const U4 &x, const U4 &y) const
+    {
+        return U4{x.a + y.a, x.b + y.b, x.c + y.c, x.d + y.d};
+    }
+};
+
+__global__ void k_block_counts(const uint32_t *__restrict__ code, size_t nwords, uint32_t T, size_t nblk,
+                               U4 *__restrict__ cnt)
+{
+    size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    uint32_t n1 = 0, n2 = 0, n3 = 0;
+    for (int q = 0; q < 12; ++q) {
+        size_t wi = b * 12 + q;
+        uint32_t v = wi < nwords ? code[wi] : 0u;
+        uint32_t lo = v & 0x55555555u, hi = (v >> 1) & 0x55555555u;
+        n3 += __popc(lo & hi); n1 += __popc(lo); n2 += __popc(hi);
+    }
+    n1 -= n3; n2 -= n3;
+    uint64_t s = (uint64_t)b * HSA_BLK_CHARS;
+    uint32_t valid = s >= T ? 0u : (uint32_t)((T - s) < HSA_BLK_CHARS ? (T - s) : HSA_BLK_CHARS);
+    cnt[b] = U4{valid - n1 - n2 - n3, n1, n2, n3};
+}
+
+__global__ void k_block_write(const uint32_t *__restrict__ code, size_t nwords, size_t nblk,
+                              const U4 *__restrict__ pre, uint4 *__restrict__ blk)
+{
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // one thread per dword of output
+    size_t b = t >> 4, d = t & 15;
+    if (b >= nblk) return;
+    uint32_t v;
+    if (d < 4) {
+        U4 p = pre[b];
+        v = d == 0 ? p.a : d == 1 ? p.b : d == 2 ? p.c : p.d;
+    } else {
+        size_t wi = b * 12 + (d - 4);
+        v = wi < nwords ? code[wi] : 0u;
+    }
+    reinterpret_cast<uint32_t *>(blk)[t] = v;
+}
+
+static int build_blocks(hsa_index *ix, int dir, uint32_t T, const uint32_t *d_code_lsb, hipStream_t st)
+{
+    size_t nwords = ((size_t)T + 15) / 16;
+    size_t nblk = (size_t)T / HSA_BLK_CHARS + 2;
+    U4 *cnt = nullptr, *pre = nullptr;
+    void *tmp = nullptr;
+    size_t tmp_bytes = 0;
+    HSA_HIP(hipMalloc(&cnt, nblk * sizeof(U4)));
+    HSA_HIP(hipMalloc(&pre, nblk * sizeof(U4)));
+    HSA_HIP(hipMalloc(&ix->blk[dir], nblk * 64));
+    ix->nblk[dir] = nblk;
+    k_block_counts<<<(unsigned)((nblk + 255) / 256), 256, 0, st>>>(d_code_lsb, nwords, T, nblk, cnt);
+    HSA_HIP(hipGetLastError());
+    U4 zero{0, 0, 0, 0};
+    HSA_HIP(rocprim::exclusive_scan(tmp, tmp_bytes, cnt, pre, zero, nblk, U4Plus(), st));
+    HSA_HIP(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16));
+    HSA_HIP(rocprim::exclusive_scan(tmp, tmp_bytes, cnt, pre, zero, nblk, U4Plus(), st));
+    size_t nthr = nblk * 16;
+    k_block_write<<<(unsigned)((nthr + 255) / 256), 256, 0, st>>>(d_code_lsb, nwords, nblk, pre, ix->blk[dir]);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipStreamSynchronize(st));
+    (void)hipFree(tmp); (void)hipFree(cnt); (void)hipFree(pre);
+    return 0;
+}
+
+static int index_init(int device, hsa_index **out)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        hsa_set_error("no HIP device visible");
+        return HSA_E_NODEV;
+    }
+    if (device < 0 || device >= n) { hsa_set_error("device %d out of range (%d)", device, n); return HSA_E_ARG; }
+    HSA_HIP(hipSetDevice(device));
+    hsa_index *ix = new hsa_index();
+    ix->device = device;
+    hipDeviceProp_t prop;
+    HSA_HIP(hipGetDeviceProperties(&prop, device));
+    ix->n_cu = prop.multiProcessorCount;
+    HSA_HIP(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking));
+    HSA_HIP(hipEventCreate(&ix->ev0));
+    HSA_HIP(hipEventCreate(&ix->ev1));
+    HSA_HIP(hipMalloc(&ix->d_ctr, 16 * sizeof(uint64_t)));
+    *out = ix;
+    return 0;
+}
+
+extern "C" int hsa_index_create_device(int device, uint32_t T, uint32_t isa0, const uint32_t C[5],
+                                       const uint32_t *d_code_lsb, uint32_t rT, uint32_t risa0,
+                                       const uint32_t rC[5], const uint32_t *d_rcode_lsb, hsa_index_t **out)
+{
+    hsa_index *ix = nullptr;
+    int rc = index_init(device, &ix);
+    if (rc) return rc;
+    ix->T = T; ix->isa0 = isa0; memcpy(ix->C, C, sizeof ix->C);
+    ix->rT = rT; ix->risa0 = risa0; memcpy(ix->rC, rC, sizeof ix->rC);
+    if ((rc = build_blocks(ix, 0, T, d_code_lsb, ix->stream)) ||
+        (rc = build_blocks(ix, 1, rT, d_rcode_lsb, ix->stream))) {
+        hsa_index_free(ix);
+        return rc;
+    }
+    *out = ix;
+    return 0;
+}
+
+extern "C" int hsa_index_create(int device, uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code,
+                                uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *rcode,
+                                hsa_index_t **out)
+{
+    if (!code || !rcode || !C || !rC || !out) { hsa_set_error("null argument"); return HSA_E_ARG; }
+    if (C[4] != T || rC[4] != rT) { hsa_set_error("C[4] must equal the text length"); return HSA_E_ARG; }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) { hsa_set_error("no HIP device visible"); return HSA_E_NODEV; }
+    HSA_HIP(hipSetDevice(device));
+    size_t nw = ((size_t)T + 15) / 16, rnw = ((size_t)rT + 15) / 16;
+    uint32_t *d = nullptr, *rd = nullptr;
+    HSA_HIP(hipMalloc(&d, nw * 4 + 64));
+    HSA_HIP(hipMalloc(&rd, rnw * 4 + 64));
+    HSA_HIP(hipMemcpy(d, code, nw * 4, hipMemcpyHostToDevice));
+    HSA_HIP(hipMemcpy(rd, rcode, rnw * 4, hipMemcpyHostToDevice));
+    k_msb_to_lsb<<<(unsigned)((nw + 255) / 256), 256>>>(d, nw, T);
+    k_msb_to_lsb<<<(unsigned)((rnw + 255) / 256), 256>>>(rd, rnw, rT);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipDeviceSynchronize());
+    int rc = hsa_index_create_device(device, T, isa0, C, d, rT, risa0, rC, rd, out);
+    (void)hipFree(d); (void)hipFree(rd);
+    return rc;
+}
+
+extern "C" void hsa_index_free(hsa_index_t *ix)
+{
+    if (!ix) return;
+    (void)hipSetDevice(ix->device);
+    (void)hipFree(ix->blk[0]); (void)hipFree(ix->blk[1]);
+    hsa_scratch_free(ix->main); hsa_scratch_free(ix->big);
+    (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr);
+    if (ix->ev0) (void)hipEventDestroy(ix->ev0);
+    if (ix->ev1) (void)hipEventDestroy(ix->ev1);
+    if (ix->stream) (void)hipStreamDestroy(ix->stream);
+    delete ix;
+}
+
+extern "C" size_t hsa_index_bytes(const hsa_index_t *ix) { return (ix->nblk[0] + ix->nblk[1]) * 64; }
+extern "C" int hsa_index_device(const hsa_index_t *ix) { return ix->device; }
+
+// ---------------------------------------------------------------- primitives
+__global__ void k_occ4(RankDir d, const uint32_t *pos, size_t n, uint32_t *out)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t o[4];
+    hsa_occ4(d, pos[i], o);
+    out[4 * i] = o[0]; out[4 * i + 1] = o[1]; out[4 * i + 2] = o[2]; out[4 * i + 3] = o[3];
+}
+
+extern "C" int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t *pos, uint32_t *occ)
+{
+    if (dir < 0 || dir > 1) { hsa_set_error("dir"); return HSA_E_ARG; }
+    HSA_HIP(hipSetDevice(ix->device));
+    int rc;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, n * 4 + 16)) || (rc = hsa_grow(&ix->d_out, &ix->d_out_cap, n * 16 + 16)))
+        return rc;
+    HSA_HIP(hipMemcpyAsync(ix->d_in, pos, n * 4, hipMemcpyHostToDevice, ix->stream));
+    RankDir d{ix->blk[dir], dir ? ix->risa0 : ix->isa0};
+    if (n) k_occ4<<<(unsigned)((n + 255) / 256), 256, 0, ix->stream>>>(d, (const uint32_t *)ix->d_in, n, (uint32_t *)ix->d_out);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipMemcpyAsync(occ, ix->d_out, n * 16, hipMemcpyDeviceToHost, ix->stream));
+    HSA_HIP(hipStreamSynchronize(ix->stream));
+    return 0;
+}
+
+// BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235-272)
+__global__ void k_step(RankDir d, const uint32_t *C, const uint32_t *in, size_t n, uint32_t *out)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = in[4 * i], l = in[4 * i + 1], rl = in[4 * i + 3];
+    uint32_t a[4], b[4];
+    hsa_occ_pair(d, k, l + 1, a, b);
+    uint32_t oc[4];
+    oc[3] = 0;
+    for (int c = 2; c >= 0; --c) oc[c] = oc[c + 1] + b[c + 1] - a[c + 1];
+    uint32_t *o = out + 16 * i;
+    for (int c = 0; c < 4; ++c) {
+        uint32_t nk = C[c] + a[c] + 1, nl = C[c] + b[c];
+        uint32_t nrl = rl - oc[c];
+        o[c] = nk; o[4 + c] = nl; o[12 + c] = nrl; o[8 + c] = nrl - (nl - nk);
+    }
+}
+
+extern "C" int hsa_step_batch(hsa_index_t *ix, size_t n, const uint32_t *klrr, uint32_t *out16)
+{
+    HSA_HIP(hipSetDevice(ix->device));
+    int rc;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, n * 16 + 64)) || (rc = hsa_grow(&ix->d_out, &ix->d_out_cap, n * 64 + 16)))
+        return rc;
+    HSA_HIP(hipMemcpyAsync(ix->d_in, klrr, n * 16, hipMemcpyHostToDevice, ix->stream));
+    uint32_t *dC = (uint32_t *)((char *)ix->d_in + ((n * 16 + 15) / 16) * 16);
+    HSA_HIP(hipMemcpyAsync(dC, ix->C, 5 * 4, hipMemcpyHostToDevice, ix->stream));
+    RankDir d{ix->blk[0], ix->isa0};
+    if (n) k_step<<<(unsigned)((n + 255) / 256), 256, 0, ix->stream>>>(d, dC, (const uint32_t *)ix->d_in, n, (uint32_t *)ix->d_out);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipMemcpyAsync(out16, ix->d_out, n * 64, hipMemcpyDeviceToHost, ix->stream));
+    HSA_HIP(hipStreamSynchronize(ix->stream));
+    return 0;
+}
+
+// bwt_cal_width type 1 (bwtaln.c:73-98), one read per thread (test primitive;
+// the search kernel has its own interleaved version).
+__global__ void k_width(RankDir rev, uint32_t T, const uint32_t *C, const uint64_t *offs, const uint32_t *lens,
+                        const uint64_t *woff, const uint8_t *codes, size_t n, uint32_t *w)
+{
+    size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint8_t *s = codes + offs[r];
+    uint32_t len = lens[r], k = 0, l = T;
+    int bid = 0;
+    uint32_t *o = w + woff[r];
+    for (uint32_t i = 0; i < len; ++i) {
+        uint8_t c = s[i];
+        if (c < 4) {
+            uint32_t a[4], b[4];
+            hsa_occ_pair(rev, k, l + 1, a, b);
+            k = C[c] + a[c] + 1;
+            l = C[c] + b[c];
+        }
+        if (k > l || c > 3) { k = 0; l = T; ++bid; }
+        o[2 * i] = l - k + 1;
+        o[2 * i + 1] = (uint32_t)bid;
+    }
+    o[2 * len] = 0;
+    o[2 * len + 1] = (uint32_t)(bid + 1);
+}
+
+extern "C" int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
+                               const uint8_t *codes, size_t codes_len, uint32_t *width_out)
+{
+    HSA_HIP(hipSetDevice(ix->device));
+    uint64_t *woff = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+    uint64_t tot = 0;
+    for (size_t i = 0; i < n; ++i) { woff[i] = tot; tot += 2 * ((uint64_t)lens[i] + 1); }
+    size_t inb = n * 8 + n * 4 + n * 8 + codes_len + 5 * 4 + 256;
+    int rc;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, inb)) || (rc = hsa_grow(&ix->d_out, &ix->d_out_cap, tot * 4 + 16))) {
+        free(woff);
+        return rc;
+    }
+    char *p = (char *)ix->d_in;
+    uint64_t *d_offs = (uint64_t *)p; p += n * 8;
+    uint64_t *d_woff = (uint64_t *)p; p += n * 8;
+    uint32_t *d_lens = (uint32_t *)p; p += n * 4;
+    uint32_t *d_C = (uint32_t *)p; p += 32;
+    uint8_t *d_codes = (uint8_t *)p;
+    HSA_HIP(hipMemcpyAsync(d_offs, offs, n * 8, hipMemcpyHostToDevice, ix->stream));
+    HSA_HIP(hipMemcpyAsync(d_woff, woff, n * 8, hipMemcpyHostToDevice, ix->stream));
+    HSA_HIP(hipMemcpyAsync(d_lens, lens, n * 4, hipMemcpyHostToDevice, ix->stream));
+    HSA_HIP(hipMemcpyAsync(d_C, ix->C, 20, hipMemcpyHostToDevice, ix->stream));
+    HSA_HIP(hipMemcpyAsync(d_codes, codes, codes_len, hipMemcpyHostToDevice, ix->stream));
+    RankDir rev{ix->blk[1], ix->risa0};
+    if (n) k_width<<<(unsigned)((n + 63) / 64), 64, 0, ix->stream>>>(rev, ix->T, d_C, d_offs, d_lens, d_woff, d_codes, n, (uint32_t *)ix->d_out);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipMemcpyAsync(width_out, ix->d_out, tot * 4, hipMemcpyDeviceToHost, ix->stream));
+    HSA_HIP(hipStreamSynchronize(ix->stream));
+    free(woff);
+    return 0;
+}
+
+// ---------------------------------------------------------------- synthetic genome
+// Same stream as hsa_amd/synth.py genome_words(): word w = splitmix64(seed*golden ^ w),
+// 32 bases per u64, base j at bits 2j..2j+1; emitted as LSB-first u32 (16 bases).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void k_synth(uint64_t T, uint64_t seed, uint32_t *out)
+{
+    uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t nw = (T + 31) / 32;
+    if (w >= nw) return;
+    uint64_t x = splitmix64((seed * 0x9E3779B97F4A7C15ull) ^ w);
+    uint64_t rem = T - w * 32;
+    if (rem < 32) x &= (1ull << (2 * rem)) - 1ull;
+    uint64_t lo_words = (T + 15) / 16;
+    out[2 * w] = (uint32_t)x;
+    if (2 * w + 1 < lo_words) out[2 * w + 1] = (uint32_t)(x >> 32);
+}
+
+extern "C" int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, uint32_t *d_code_lsb)
+{
+    HSA_HIP(hipSetDevice(device));
+    uint64_t nw = (T + 31) / 32;
+    k_synth<<<(unsigned)((nw + 255) / 256), 256>>>(T, seed, d_code_lsb);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipDeviceSynchronize());
+    return 0;
+}

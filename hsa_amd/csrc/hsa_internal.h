@@ -1,0 +1,52 @@
+// hsa_internal.h -- host-side internals shared by the library's HIP sources.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/hsa_gpu.h"
+
+void hsa_set_error(const char *fmt, ...);
+
+#define HSA_HIP(call)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            hsa_set_error("%s:%d %s: %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+            return HSA_E_HIP;                                                               \
+        }                                                                                   \
+    } while (0)
+
+// Per-launch scratch of the search kernel: grows, never shrinks.
+struct SearchScratch {
+    size_t lanes = 0, wcap = 0, pcap = 0, hcap = 0;
+    uint2 *width = nullptr;      // lanes * wcap
+    uint4 *pool = nullptr;       // lanes * pcap
+    uint16_t *nxt = nullptr;     // lanes * pcap
+    uint32_t *hbuf = nullptr;    // lanes * hcap * 9
+};
+
+struct hsa_index {
+    int device = 0;
+    uint32_t T = 0, isa0 = 0, C[5] = {0, 0, 0, 0, 0};
+    uint32_t rT = 0, risa0 = 0, rC[5] = {0, 0, 0, 0, 0};
+    uint4 *blk[2] = {nullptr, nullptr};
+    size_t nblk[2] = {0, 0};
+    hipStream_t stream = nullptr;
+    int n_cu = 0;
+    SearchScratch main, big;
+    // staging for the host-pointer batch API
+    void *d_in = nullptr; size_t d_in_cap = 0;
+    void *d_out = nullptr; size_t d_out_cap = 0;
+    uint64_t *d_ctr = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+int hsa_grow(void **p, size_t *cap, size_t need);
+int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t wcap, size_t pcap, size_t hcap);
+void hsa_scratch_free(SearchScratch &s);
+
+// Knobs (hsa_configure).
+extern int g_waves_per_cu;
+extern int g_pool_entries;
+extern int g_hit_cap;

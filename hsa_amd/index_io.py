@@ -101,3 +101,30 @@ def write_bwt_files(prefix: str, T: int, isa0: int, C: np.ndarray, codes: np.nda
 
 def exists(prefix: str) -> bool:
     return all(os.path.exists(f"{prefix}.index.{e}") for e in ("bwt", "rev.bwt"))
+
+
+def read_pac(prefix: str, T: int | None = None) -> np.ndarray:
+    """Forward text from prefix.index.pac: 4 codes per byte, first code in the high
+    bits, then (T%4==0 ? a 0 byte : nothing) and a final byte T%4 (HSP.c:313-323)."""
+    raw = np.fromfile(prefix + ".index.pac", dtype=np.uint8)
+    if T is None:
+        with open(prefix + ".index.ann") as f:
+            T = int(f.readline().split()[0])
+    sh = np.array([6, 4, 2, 0], np.uint8)
+    codes = ((raw[:, None] >> sh[None, :]) & 3).reshape(-1)
+    return codes[:T].astype(np.uint8)
+
+
+def pack_lsb_u32(codes: np.ndarray) -> np.ndarray:
+    """2-bit codes -> 16 per u32, code j at bits 2j..2j+1 (the device text layout)."""
+    n = len(codes)
+    nw = (n + 15) // 16
+    pad = np.zeros(nw * 16, np.uint64)
+    pad[:n] = codes
+    sh = (2 * np.arange(16)).astype(np.uint64)
+    return (pad.reshape(nw, 16) << sh[None, :]).sum(axis=1).astype(np.uint32)
+
+
+def unpack_lsb_u32(words: np.ndarray, n: int) -> np.ndarray:
+    sh = (2 * np.arange(16)).astype(np.uint32)
+    return ((words[:, None] >> sh[None, :]) & np.uint32(3)).astype(np.uint8).reshape(-1)[:n]

@@ -1,0 +1,163 @@
+/*
+ * hsa_bwtaln.h -- the drop-in boundary: reference-compatible entry points and
+ * struct layouts of the HSA `aln` search path, implemented on the MI355X core.
+ *
+ * Linking libhsa_gpu.so in place of the reference's definitions (see
+ * INTEGRATION.md) keeps the host program unchanged:
+ *
+ *   bwa_cal_sa_reg_gap   replaces bwtaln.c:246  (declared bwtaln.h:199-200)
+ *   hsa_gpu_attach       new hook, called once after BWTLoad2BWT (bwtaln.c:467)
+ *   hsa_gpu_detach       new hook, before BWTFree2BWT (bwtaln.c:527)
+ *   hsa_gpu_set_devices  new hook (multi-GPU: reads of one call are split over devices)
+ *
+ * The structs below are declared here only so that the library reads and writes
+ * the host's objects at the right offsets; their layouts are those of the
+ * reference on x86-64 (sizes checked by static asserts in bwtaln_gpu.c and by
+ * tests/test_abi.py against the compiled reference).
+ */
+#ifndef HSA_BWTALN_H
+#define HSA_BWTALN_H
+#include <stdint.h>
+#include "hsa_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef uint32_t bwtint_t;       /* 2BWT-Interface.h:26 */
+typedef unsigned char ubyte_t;
+
+/* BWT.h:61-83 (only textLength, inverseSa0, cumulativeFreq and bwtCode are read) */
+typedef struct BWT {
+    unsigned int textLength, saInterval, inverseSaInterval, inverseSa0;
+    unsigned int *cumulativeFreq, *bwtCode, *occValue, *occValueMajor, *saValue, *inverseSa, *cachedSaIndex;
+    unsigned int cachedSaIndexNumOfChar;
+    unsigned int *saValueOnBoundary, *decodeTable;
+    unsigned int decodeTableGenerated, bwtSizeInWord, occSizeInWord, occMajorSizeInWord, saValueSizeInWord,
+                 inverseSaSizeInWord, cachedSaIndexSizeInWord;
+} BWT;
+
+struct HSP;
+struct MMPool;
+/* 2BWT-Interface.h:29-36 */
+typedef struct _Idx2BWT {
+    struct MMPool *mmPool;
+    BWT *bwt, *rev_bwt;
+    struct HSP *hsp;
+    unsigned char charMap[256], complementMap[256];
+} Idx2BWT;
+
+/* bwtaln.h:36-39 */
+typedef struct { bwtint_t w; int bid; } bwt_width_t;
+
+/* bwtaln.h:41-50 -- the hit record (36 bytes) */
+typedef struct {
+    uint32_t n_mm:16, n_gapo:8, n_gape:8;
+    bwtint_t k, l;
+    bwtint_t rev_k, rev_l;
+    bwtint_t type:30, strand:2;
+    int start, end;
+    int score;
+} bwt_aln1_t;
+
+/* bwtaln.h:52-68 -- the reference's stack, allocated here only to hand to the
+ * host's bwt_splice_match */
+typedef struct {
+    uint32_t info;
+    uint32_t n_mm:8, n_gapo:8, n_gape:8, state:2, n_seed_mm:6;
+    bwtint_t k, l, rev_k, rev_l;
+    int last_diff_pos;
+} gap_entry_t;
+typedef struct { int n_entries, m_entries; gap_entry_t *stack; } gap_stack1_t;
+typedef struct { int n_stacks, best, n_entries; gap_stack1_t *stacks; } gap_stack_t;
+
+typedef uint32_t bwa_cigar_t;
+struct bwt_multi1_t;
+/* bwtaln.h:93-120 (208 bytes) */
+typedef struct {
+    char *name;
+    ubyte_t *seq, *rseq, *qual;
+    uint32_t len:19, strand:1, type:3, dummy:1, extra_flag:8;
+    uint32_t n_mm:8, n_gapo:8, n_gape:8, mapQ:8;
+    int score;
+    int clip_len;
+    int n_aln;
+    bwt_aln1_t *aln;
+    int start, end;
+    int n_multi;
+    struct bwt_multi1_t *multi;
+    bwtint_t sa, ori_pos, occ_pos;
+    uint32_t seq_id;
+    uint64_t c1:28, c2:28, seQ:8;
+    int n_cigar;
+    bwa_cigar_t *cigar;
+    int tid;
+    char bc[64];
+    uint32_t full_len:20, nm:12;
+    char *md;
+} bwa_seq_t;
+
+/* bwtaln.h:122-131 mode bits */
+#define BWA_MODE_GAPE       0x01
+#define BWA_MODE_COMPREAD   0x02
+#define BWA_MODE_LOGGAP     0x04
+#define BWA_MODE_NONSTOP    0x10
+
+/* bwtaln.h:133-143 (64 bytes) */
+typedef struct {
+    int s_mm, s_gapo, s_gape;
+    int mode;
+    int indel_end_skip, max_del_occ, max_entries;
+    float fnr;
+    int max_diff, max_gapo, max_gape;
+    int max_seed_diff, seed_len;
+    int n_threads;
+    int max_top2;
+    int trim_qual;
+} gap_opt_t;
+
+struct bwt_array_t;
+/* bwtaln.h:156-169 (96 bytes) */
+typedef struct _bwt_aux_t {
+    Idx2BWT *bi_bwt;
+    bwt_width_t *width_back, *width_fore, *width_seed;
+    ubyte_t *seq, *rc_seq;
+    gap_opt_t *opt;
+    gap_stack_t *stack;
+    struct bwt_array_t *arr;
+    int start, end;
+    int strand;
+    int len;
+    int max_len;
+} bwt_aux_t;
+
+/* ---- drop-in entry points (reference ABI) ---- */
+void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, const gap_opt_t *opt,
+                        struct bwt_array_t *arr);
+int  hsa_gpu_attach(const Idx2BWT *bi_bwt);
+void hsa_gpu_detach(const Idx2BWT *bi_bwt);
+int  hsa_gpu_set_devices(int n);
+
+/* The host's splice fallback (bwtgap.c:748).  Weak: when the host program does
+ * not provide it, reads without a hit are left with n_aln = 0. */
+bwt_aln1_t *bwt_splice_match(bwt_aux_t *aux, int *n_aln) __attribute__((weak));
+
+/* ---- flat form of bwa_cal_sa_reg_gap for bindings (plain arrays) ----
+ * Same semantics and the same side effects on *opt.  Per-read flags:
+ *   HSA_F_FALLBACK   no hit on either strand (the reference calls bwt_splice_match)
+ *   HSA_RF_NFILTER   skipped by the #N > max_diff filter (bwtaln.c:314-317); the
+ *                    reference leaves such a bwa_seq_t untouched
+ *   HSA_RF_POLYAT    skipped by the first-15-bases filter (bwtaln.c:324-325)
+ * splice_opt (optional, n entries): max_diff and seed_len of the option block the
+ * reference hands to bwt_splice_match for each fallback read.  Hits: 9 u32 per
+ * bwt_aln1_t, *hits malloc'd (hsa_free). */
+#define HSA_RF_NFILTER  0x10u
+#define HSA_RF_POLYAT   0x20u
+long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint32_t *lens, const uint64_t *offs,
+                             const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
+                             uint64_t *hit_off, uint32_t **hits, int32_t *splice_opt, hsa_stats_t *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,135 @@
+/*
+ * hsa_gpu.h -- C ABI of the MI355X search core (libhsa_gpu.so).
+ *
+ * Plain pointers and sizes only.  This is the layer the reference-compatible
+ * entry points (include/hsa_bwtaln.h) are built on, and the layer the Python
+ * tests/bench bind with ctypes.
+ *
+ * What each group replaces in the reference:
+ *   hsa_index_*        -- BWTLoad2BWT's in-memory BWT + Occ tables (2BWT-Interface.c:13,
+ *                         BWT.c:107): uploaded once to HBM and re-laid out into 64-byte
+ *                         rank blocks (4 x u32 counts + 192 two-bit codes).
+ *   hsa_occ4_batch     -- BWTAllOccValue (BWT.c:793) for a batch of positions.
+ *   hsa_step_batch     -- BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235).
+ *   hsa_width_batch    -- bwt_cal_width type 1 (bwtaln.c:73-98).
+ *   hsa_search_batch   -- the per-read loop of bwa_cal_sa_reg_gap (bwtaln.c:303-373):
+ *                         rc strand then forward strand, bwt_cal_width x2 and
+ *                         bwt_match_gap (bwtgap.c:118-331) per strand.
+ *
+ * Errors: every call returns 0 on success or a negative HSA_E* code and leaves a
+ * message readable with hsa_last_error().  The library never falls back to a CPU
+ * path: without a usable gfx950 device the calls fail.
+ */
+#ifndef HSA_GPU_H
+#define HSA_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HSA_E_HIP     (-1)   /* a HIP runtime call failed */
+#define HSA_E_ARG     (-2)   /* invalid argument / unsupported option range */
+#define HSA_E_NODEV   (-3)   /* no GPU visible */
+#define HSA_E_MEM     (-4)   /* device allocation failed */
+
+/* Search options of one regime (the fields of gap_opt_t the search reads,
+ * bwtaln.h:133-143).  max_diff and seed_len are per read (hsa_job_t). */
+typedef struct {
+    int32_t s_mm, s_gapo, s_gape;
+    int32_t mode;                 /* BWA_MODE_* bits: GAPE 0x1, LOGGAP 0x4, NONSTOP 0x10 */
+    int32_t indel_end_skip, max_del_occ, max_entries;
+    int32_t max_gapo, max_gape;
+    int32_t max_seed_diff, max_top2;
+    int32_t n_stacks;             /* aln_score(max_diff+1, max_gapo+1, max_gape+1) of the batch's local_opt */
+} hsa_regime_t;
+
+/* One read to search.  `off` indexes the codes buffer given to hsa_search_batch. */
+typedef struct {
+    uint64_t off;
+    uint32_t len;
+    int32_t max_diff;             /* value of aux->opt->max_diff for this read */
+    int32_t seed_len;             /* aux->opt->seed_len after bwtaln.c:332 (0x7fffffff = none) */
+    int32_t regime;               /* index into the regime array (0 or 1) */
+} hsa_job_t;
+
+/* Per-read result flags. */
+#define HSA_F_FALLBACK  1u        /* no hit on either strand: caller runs bwt_splice_match */
+#define HSA_F_OVERFLOW  2u        /* internal: per-lane stack/hit capacity exceeded (re-run) */
+
+typedef struct hsa_index hsa_index_t;
+
+int         hsa_device_count(void);
+const char *hsa_last_error(void);
+
+/* Upload a bidirectional index.  code/rcode are the .bwt payload words (2-bit,
+ * MSB-first, ceil(T/16) words; BWT.c:156-181).  C/rC are cumulativeFreq[0..4]. */
+int  hsa_index_create(int device, uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code,
+                      uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *rcode,
+                      hsa_index_t **out);
+/* Same, from codes already resident on the device (LSB-first 2-bit, 16 per u32). */
+int  hsa_index_create_device(int device, uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *d_code_lsb,
+                             uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *d_rcode_lsb,
+                             hsa_index_t **out);
+void hsa_index_free(hsa_index_t *ix);
+size_t hsa_index_bytes(const hsa_index_t *ix);
+int  hsa_index_device(const hsa_index_t *ix);
+
+/* Rank/step/width primitives over host arrays (tests and tools). */
+int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t *pos, uint32_t *occ4_out);
+int hsa_step_batch(hsa_index_t *ix, size_t n, const uint32_t *klrr, uint32_t *out16);
+int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
+                    const uint8_t *codes, size_t codes_len, uint32_t *width_out /* 2*(len+1) words per read, packed */);
+
+/* Search statistics (summed over the call). */
+typedef struct {
+    uint64_t rank_queries;        /* Occ evaluations the reference would issue (2 per step) */
+    uint64_t blocks_loaded;       /* 64-byte rank blocks actually fetched */
+    uint64_t pops;                /* gap_pop calls */
+    uint64_t overflow_reruns;     /* reads re-run with large per-read capacity */
+    double   kernel_ms;           /* device time of the search kernels (HIP events) */
+    double   main_kernel_ms;      /* device time of the main (first) search launch */
+    uint64_t main_launches;
+} hsa_stats_t;
+
+/* Search `n_jobs` reads.  Host pointers; `codes` holds the 0..255 read codes.
+ * Outputs: n_aln[j], flags[j], hit_off[j] (offset in hits, in records) and the
+ * packed hits, 9 u32 per record in bwt_aln1_t layout (bwtaln.h:41-50), written to
+ * *hits (malloc'd by the library; free with hsa_free).  Returns total hits >= 0. */
+long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes,
+                      const hsa_job_t *jobs, int n_jobs, const uint8_t *codes, size_t codes_len,
+                      int32_t *n_aln, uint32_t *flags, uint64_t *hit_off, uint32_t **hits,
+                      hsa_stats_t *stats);
+
+/* Device-resident variant for throughput runs: jobs/codes already on the device,
+ * outputs stay on the device (d_hits capacity in records).  Launches on `stream`
+ * (a hipStream_t; NULL = the library's stream) and does not synchronise. */
+typedef struct {
+    const hsa_job_t *d_jobs; int n_jobs;
+    const uint8_t *d_codes;
+    int32_t *d_n_aln; uint32_t *d_flags; uint64_t *d_hit_off;
+    uint32_t *d_hits; uint64_t hit_cap;
+    uint64_t *d_counters;         /* >= 8 u64 of device scratch, zeroed by the call */
+} hsa_device_batch_t;
+int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes,
+                      const hsa_device_batch_t *b, void *stream);
+/* Kernel geometry/capacity knobs (0 = default). */
+int hsa_configure(int waves_per_cu, int pool_entries, int hit_cap);
+
+void hsa_free(void *p);
+
+/* Synthetic workload helpers (bench data generation on the device). */
+int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, uint32_t *d_code_lsb);
+
+/* Suffix-array based BWT construction on the device for a text given as LSB-first
+ * 2-bit codes (16 per u32).  Produces the $-less BWT codes (LSB-first) and
+ * inverseSa0 = rank of suffix 0 among T+1 suffixes incl. '$' (BWT.h:61-83).
+ * `reverse` builds the BWT of the reversed text. */
+int hsa_build_bwt_device(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse,
+                         uint32_t *d_bwt_lsb, uint32_t *isa0, uint32_t C[5]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

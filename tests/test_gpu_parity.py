@@ -1,0 +1,100 @@
+"""GPU parity: the HIP path (through the C ABI) against the compiled reference's
+golden vectors and the CPU restatement (oracle).  Integer work: bit-exact."""
+import numpy as np
+import pytest
+
+from golden_io import GOLD, INDEX, cases, load_case, parse_opts, split_hits
+from hsa_amd import index_io
+
+pytestmark = pytest.mark.gpu
+
+_GPU = {}
+
+
+def gpu_index(name):
+    from hsa_amd._lib import GpuIndex
+    if name not in _GPU:
+        _GPU[name] = GpuIndex(*index_io.read_index(INDEX[name]))
+    return _GPU[name]
+
+
+def test_rank_matches_reference():
+    g = np.load(f"{GOLD}/tiny_occ.npz")
+    ix = gpu_index("tiny")
+    for d in (0, 1):
+        assert np.array_equal(ix.occ4(d, g["pos"]), g["occ"][d]), f"dir {d}"
+
+
+def test_rank_all_positions_prefix_count():
+    fwd, rev = index_io.read_index(INDEX["rep"])
+    ix = gpu_index("rep")
+    for d, b in enumerate((fwd, rev)):
+        codes = index_io.unpack_codes(b)
+        pref = np.zeros((b.T + 1, 4), np.int64)
+        for c in range(4):
+            pref[1:, c] = np.cumsum(codes == c)
+        pos = np.arange(b.T + 2, dtype=np.int64)
+        exp = pref[pos - (pos > b.isa0)]
+        assert np.array_equal(ix.occ4(d, pos.astype(np.uint32)), exp)
+
+
+def test_width_matches_reference():
+    g = np.load(f"{GOLD}/tiny_width.npz")
+    ix = gpu_index("tiny")
+    assert np.array_equal(ix.widths(g["lens"], g["codes"]), g["width"].reshape(-1))
+
+
+def test_step_matches_oracle():
+    from oracle_ctypes import OracleIndex
+    fwd, rev = index_io.read_index(INDEX["tiny"])
+    ox = OracleIndex(fwd, rev)
+    ix = gpu_index("tiny")
+    rng = np.random.default_rng(5)
+    T = fwd.T
+    q = []
+    k, l, rk, rl = 0, T, 0, T
+    for _ in range(3000):
+        q.append((k, l, rk, rl))
+        ok, ol, ork, orl = ox.step_all(k, l, rk, rl)
+        c = int(rng.integers(4))
+        if ok[c] > ol[c] or rng.random() < 0.05:
+            k, l, rk, rl = 0, T, 0, T
+        else:
+            k, l, rk, rl = int(ok[c]), int(ol[c]), int(ork[c]), int(orl[c])
+    q = np.array(q, np.uint32)
+    got = ix.step_all(q)
+    for j in range(0, len(q), 97):
+        exp = np.stack(ox.step_all(*[int(x) for x in q[j]]))
+        assert np.array_equal(got[j], exp)
+
+
+def _compare(name, pool_entries=0):
+    from hsa_amd._lib import GapOpt, configure
+    from oracle_ctypes import default_opt
+    g = load_case(name)
+    ix = gpu_index(g["index"])
+    if pool_entries:
+        configure(pool_entries=pool_entries)
+    try:
+        n_aln, flags, per_read, _ = ix.run_batches(g["lens"], g["codes"], parse_opts(g["args"], default_opt()),
+                                                   g["batch"])
+    finally:
+        if pool_entries:
+            configure(pool_entries=8192)
+    exp_splice = (g["flags"] & 1).astype(bool)
+    got_splice = (flags & 1).astype(bool)
+    assert np.array_equal(got_splice, exp_splice), np.nonzero(got_splice != exp_splice)[0][:10]
+    exp = split_hits(g["n_aln"], g["hits"])
+    bad = [i for i in range(len(exp)) if not exp_splice[i] and not np.array_equal(per_read[i], exp[i])]
+    assert not bad, f"{len(bad)} reads differ; first {bad[0]}: got {per_read[bad[0]]} exp {exp[bad[0]]}"
+
+
+@pytest.mark.parametrize("name", sorted(cases().keys()))
+def test_search_matches_reference(name):
+    _compare(name)
+
+
+@pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "rep_mm100_n4o1"])
+def test_overflow_rerun_is_exact(name):
+    """A tiny per-lane pool forces most reads through the large-capacity re-run."""
+    _compare(name, pool_entries=64)
