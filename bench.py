@@ -1,0 +1,280 @@
+#!/usr/bin/env python3
+"""Throughput of the HSA inexact-alignment path on MI355X (the driver's contract).
+
+Workload (BASELINE.json configs[1]): 100 bp synthetic reads with 0-4 substitutions,
+50 % reverse-complemented, searched with `-n 4 -o 0` against a synthetic
+hg19-sized bidirectional index (3 000 000 005 bp in 24 records).  A "step" is one
+bwa_cal_sa_reg_gap batch of 100 000 reads (bwtaln.c:477); the default 10 steps
+are the 1 M-read workload.  Reads, job table and outputs are resident in HBM for
+the timed region; each step is one launch of the persistent search kernel.
+
+Multi-GPU (torch.distributed.run, one rank per GPU): every rank holds the whole
+index, searches its own K batches of reads (weak scaling, no collective on the data
+path), and the per-rank hit lists are gathered to rank 0 over RCCL after timing.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+GENOME_T = 3_000_000_005
+GENOME_SEED = 1234
+RECORDS = 24
+READ_LEN = 100
+BATCH = 100_000
+METRIC = "aligned reads/sec, 100bp synthetic vs hg19-sized 2BWT, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
+BYTES_PER_QUERY = 64    # one 64-byte rank block per Occ query
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_index(T, seed, device):
+    import torch
+    from hsa_amd import _lib
+    L = _lib.lib()
+    nw = (T + 15) // 16
+    text = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
+    _lib.check(L.hsa_synth_genome_device(device, T, seed, text.data_ptr()))
+    res = {}
+    for rev in (0, 1):
+        bw = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
+        isa0 = C.c_uint32()
+        Cc = np.zeros(5, np.uint32)
+        t0 = time.time()
+        _lib.check(L.hsa_build_bwt_device(device, T, text.data_ptr(), rev, bw.data_ptr(), C.byref(isa0), Cc))
+        log(f"[bench] BWT{' (reverse)' if rev else ''} of {T} bp built on the device in {time.time() - t0:.1f} s")
+        res[rev] = (bw, int(isa0.value), Cc)
+    del text
+    gi = _lib.GpuIndex.from_device_codes(T, res[0][1], res[0][2], res[0][0].data_ptr(), T, res[1][1], res[1][2],
+                                         res[1][0].data_ptr(), device=device)
+    return gi, res
+
+
+def host_oracle_index(res, T):
+    """The CPU restatement's index, from the device-built BWT (MSB-first .bwt words)."""
+    from hsa_amd import index_io
+    from oracle_ctypes import OracleIndex
+    metas = []
+    for rev in (0, 1):
+        bw, isa0, Cc = res[rev]
+        lsb = bw.cpu().numpy().view(np.uint32)[:(T + 15) // 16]
+        x = lsb.copy()
+        x = (x >> 16) | (x << 16)
+        x = ((x & 0xFF00FF00) >> 8) | ((x & 0x00FF00FF) << 8)
+        x = ((x & 0xF0F0F0F0) >> 4) | ((x & 0x0F0F0F0F) << 4)
+        x = ((x & 0xCCCCCCCC) >> 2) | ((x & 0x33333333) << 2)
+        metas.append(index_io.BwtFile(T=T, isa0=isa0, C=Cc.astype(np.uint32), code=x.astype(np.uint32)))
+    return OracleIndex(metas[0], metas[1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--genome", type=int, default=GENOME_T)
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--cpu-sample", type=int, default=20000, help="reads timed on the CPU restatement")
+    ap.add_argument("--parity-sample", type=int, default=4000, help="reads checked against the CPU restatement")
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--pool", type=int, default=0)
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from hsa_amd import _lib, synth
+    from hsa_amd._lib import DeviceBatch, GapOpt, Regime
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.cuda.current_device()
+    _lib.configure(a.waves, a.pool, 0)
+
+    T = a.genome
+    t0 = time.time()
+    gi, res = build_index(T, GENOME_SEED, device)
+    log(f"[bench] rank {rank}: index ready ({gi.nbytes() / 2**30:.2f} GiB of rank blocks) in {time.time() - t0:.1f} s")
+
+    # reads: rank r searches batches r, r+world, ... of one global stream (seed 5)
+    t0 = time.time()
+    genome = synth.PackedGenome(T, GENOME_SEED)
+    recs = synth.record_layout(T, RECORDS)
+    nb = a.warmup + a.steps
+    batches = []
+    for j in range(nb):
+        gidx = j * world + rank
+        reads, _ = synth.make_reads(genome, recs, a.batch, READ_LEN, 5 * 1_000_000 + gidx, max_mm=4)
+        batches.append(reads)
+    log(f"[bench] rank {rank}: {nb} x {a.batch} reads generated in {time.time() - t0:.1f} s")
+
+    # bwa_cal_sa_reg_gap prologue on the host (bwtaln.c:254-337): -n 4 -o 0, fixed length
+    opt = GapOpt.default()
+    opt.max_diff, opt.fnr, opt.max_gapo = 4, -1.0, 0
+    # aln_score(max_diff+1, max_gapo+1, max_gape+1) of local_opt (bwtaln.c:264-267, bwtgap.c:18)
+    n_stacks = (opt.max_diff + 1) * opt.s_mm + (opt.max_gapo + 1) * opt.s_gapo + (opt.max_gape + 1) * opt.s_gape
+    rg = Regime(s_mm=opt.s_mm, s_gapo=opt.s_gapo, s_gape=opt.s_gape, mode=0, indel_end_skip=opt.indel_end_skip,
+                max_del_occ=opt.max_del_occ, max_entries=opt.max_entries, max_gapo=0, max_gape=opt.max_gape,
+                max_seed_diff=opt.max_seed_diff, max_top2=opt.max_top2, n_stacks=n_stacks)
+    jobs = np.zeros(a.batch, _lib.JOB_DTYPE)
+    jobs["off"] = np.arange(a.batch, dtype=np.uint64) * READ_LEN
+    jobs["len"] = READ_LEN
+    jobs["max_diff"] = opt.max_diff
+    jobs["seed_len"] = opt.seed_len
+    d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).cuda()
+    d_codes = [torch.from_numpy(b.reshape(-1)).cuda() for b in batches]
+    hit_cap = a.batch * 8
+    outs = []
+    for j in range(nb):
+        outs.append(dict(n=torch.zeros(a.batch, dtype=torch.int32, device="cuda"),
+                         f=torch.zeros(a.batch, dtype=torch.int32, device="cuda"),
+                         o=torch.zeros(a.batch, dtype=torch.int64, device="cuda"),
+                         h=torch.zeros(hit_cap * 9, dtype=torch.int32, device="cuda"),
+                         c=torch.zeros(16, dtype=torch.int64, device="cuda")))
+
+    def launch(j):
+        o = outs[j]
+        b = DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[j].data_ptr(),
+                        d_n_aln=o["n"].data_ptr(), d_flags=o["f"].data_ptr(), d_hit_off=o["o"].data_ptr(),
+                        d_hits=o["h"].data_ptr(), hit_cap=hit_cap, d_counters=o["c"].data_ptr())
+        gi.search_device([rg], b)
+
+    lib_stream = torch.cuda.ExternalStream(gi.stream_handle())
+    for j in range(a.warmup):
+        launch(j)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        ev[s][0].record(lib_stream)
+        launch(a.warmup + s)
+        ev[s][1].record(lib_stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms = [e0.elapsed_time(e1) for e0, e1 in ev]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # counters and outputs of the timed launches
+    ctr = np.stack([outs[a.warmup + s]["c"].cpu().numpy() for s in range(a.steps)])
+    queries = int(ctr[:, 2].sum())
+    blocks = int(ctr[:, 3].sum())
+    pops = int(ctr[:, 4].sum())
+    flags = np.concatenate([outs[a.warmup + s]["f"].cpu().numpy() for s in range(a.steps)])
+    n_aln = np.concatenate([outs[a.warmup + s]["n"].cpu().numpy() for s in range(a.steps)])
+    overflow = int(((flags & 2) != 0).sum())
+    if overflow:
+        log(f"[bench] WARNING: {overflow} reads overflowed the per-lane capacity in the timed launches")
+    mapped = int((n_aln > 0).sum())
+    fallback = int(((flags & 1) != 0).sum())
+    reads_local = a.steps * a.batch
+
+    # final hit-list gather to rank 0 (RCCL over xGMI): counts, then the packed records
+    total_hits_local = int(ctr[:, 1].sum())
+    if world > 1:
+        cnt = torch.tensor([total_hits_local, mapped, fallback], dtype=torch.int64, device="cuda")
+        allc = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(allc, cnt)
+        last = outs[a.warmup + a.steps - 1]
+        nh_last = int(last["c"][1].item())
+        mx = torch.tensor([nh_last], dtype=torch.int64, device="cuda")
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        buf = torch.zeros(int(mx.item()) * 9, dtype=torch.int32, device="cuda")
+        buf[:nh_last * 9] = last["h"][:nh_last * 9]
+        gathered = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
+        dist.gather(buf, gathered, dst=0)
+        tot = torch.stack(allc).sum(0).tolist()
+        mapped_all, fallback_all = tot[1], tot[2]
+    else:
+        mapped_all, fallback_all = mapped, fallback
+
+    result = None
+    if rank == 0:
+        reads_all = reads_local * world
+        value = reads_all / elapsed
+        mean_kms = float(np.mean(kms))
+        q_per_launch = queries / a.steps
+        achieved = q_per_launch * BYTES_PER_QUERY / (mean_kms / 1e3) / 1e9
+        result = {
+            "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"{a.steps} x {a.batch} reads (= {reads_local // 1000}k per GPU) x 100bp, "
+                                   f"0-4 substitutions, 50% rc, vs synthetic hg19-sized 2BWT "
+                                   f"({T} bp, {RECORDS} records), -n 4 -o 0 (BASELINE configs[1])",
+                       "genome_bp": T, "reads_per_step": a.batch, "read_len": READ_LEN, "options": "-n 4 -o 0",
+                       "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "k_search", "kernel_ms_mean": round(mean_kms, 3),
+                         "rank_queries_per_read": round(queries / reads_local, 1),
+                         "blocks_per_query": round(blocks / max(queries, 1), 4),
+                         "bytes_per_query": BYTES_PER_QUERY},
+            "mapped_frac": round(mapped_all / reads_all, 4), "fallback_frac": round(fallback_all / reads_all, 4),
+            "pops_per_read": round(pops / reads_local, 1),
+        }
+
+    # parity on a sample and the CPU baseline (rank 0 at N=1 only)
+    if rank == 0 and world == 1 and (a.parity_sample or a.cpu_sample):
+        t0 = time.time()
+        ox = host_oracle_index(res, T)
+        log(f"[bench] CPU restatement index built in {time.time() - t0:.1f} s")
+        from oracle_ctypes import Opt, default_opt
+        od = default_opt()
+        od.update(max_diff=4, fnr=-1.0, max_gapo=0)
+        if a.parity_sample:
+            n = min(a.parity_sample, a.batch)
+            r0 = batches[a.warmup][:n]
+            o_n, o_f, o_h, _ = ox.cal_sa_reg_gap(np.full(n, READ_LEN, np.uint32), r0.reshape(-1), Opt.from_dict(od))
+            last = outs[a.warmup]
+            g_n = last["n"].cpu().numpy()[:n]
+            g_f = last["f"].cpu().numpy()[:n].astype(np.uint32)
+            g_o = last["o"].cpu().numpy()[:n]
+            g_h = last["h"].cpu().numpy().view(np.uint32).reshape(-1, 9)
+            oo = np.concatenate([[0], np.cumsum(o_n)])
+            bad = 0
+            for i in range(n):
+                if (g_f[i] & 1) != (o_f[i] & 1) or g_n[i] != o_n[i] or \
+                        not np.array_equal(g_h[g_o[i]:g_o[i] + g_n[i]], o_h[oo[i]:oo[i + 1]]):
+                    bad += 1
+            result["parity_sample"] = {"reads": n, "mismatching_reads": bad, "against": "oracle (C restatement)"}
+            log(f"[bench] parity sample: {n} reads, {bad} differ from the CPU restatement")
+        if a.cpu_sample:
+            n = min(a.cpu_sample, a.batch)
+            rs = batches[a.warmup + min(1, a.steps - 1)][:n]
+            t0 = time.perf_counter()
+            ox.cal_sa_reg_gap(np.full(n, READ_LEN, np.uint32), rs.reshape(-1), Opt.from_dict(od))
+            dt = time.perf_counter() - t0
+            result["cpu_baseline"] = {"value": round(n / dt, 1), "unit": "reads/s", "cores": 1, "kind": "port",
+                                      "sample": f"{n} reads of the same workload (bwa_cal_sa_reg_gap restatement, "
+                                                f"main path, 1 thread) in {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

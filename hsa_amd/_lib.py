@@ -23,7 +23,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_index_bytes", "hsa_index_device", "hsa_occ4_batch", "hsa_step_batch", "hsa_width_batch",
     "hsa_search_batch", "hsa_search_device", "hsa_configure", "hsa_free", "hsa_synth_genome_device",
     "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
-    "hsa_cal_sa_reg_gap_flat",
+    "hsa_cal_sa_reg_gap_flat", "hsa_index_stream",
 ]
 
 
@@ -106,6 +106,8 @@ def lib():
     L.hsa_index_free.argtypes = [vp]
     L.hsa_index_bytes.restype = C.c_size_t
     L.hsa_index_bytes.argtypes = [vp]
+    L.hsa_index_stream.restype = vp
+    L.hsa_index_stream.argtypes = [vp]
     L.hsa_occ4_batch.argtypes = [vp, C.c_int, C.c_size_t, u32, u32]
     L.hsa_step_batch.argtypes = [vp, C.c_size_t, u32, u32]
     L.hsa_width_batch.argtypes = [vp, C.c_size_t, u64, u32, u8, C.c_size_t, u32]
@@ -180,6 +182,13 @@ class GpuIndex:
             self.close()
         except Exception:
             pass
+
+    def stream_handle(self) -> int:
+        return int(lib().hsa_index_stream(self.h))
+
+    def search_device(self, regimes, batch: "DeviceBatch"):
+        rg = (Regime * len(regimes))(*regimes)
+        check(lib().hsa_search_device(self.h, rg, len(regimes), C.byref(batch), None))
 
     def nbytes(self) -> int:
         return int(lib().hsa_index_bytes(self.h))

@@ -253,6 +253,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
 
 extern "C" size_t hsa_index_bytes(const hsa_index_t *ix) { return (ix->nblk[0] + ix->nblk[1]) * 64; }
 extern "C" int hsa_index_device(const hsa_index_t *ix) { return ix->device; }
+extern "C" void *hsa_index_stream(const hsa_index_t *ix) { return (void *)ix->stream; }
 
 // ---------------------------------------------------------------- primitives
 __global__ void k_occ4(RankDir d, const uint32_t *pos, size_t n, uint32_t *out)

@@ -73,6 +73,8 @@ int  hsa_index_create_device(int device, uint32_t T, uint32_t isa0, const uint32
                              uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *d_rcode_lsb,
                              hsa_index_t **out);
 void hsa_index_free(hsa_index_t *ix);
+/* The HIP stream (hipStream_t) the library launches on for this index. */
+void *hsa_index_stream(const hsa_index_t *ix);
 size_t hsa_index_bytes(const hsa_index_t *ix);
 int  hsa_index_device(const hsa_index_t *ix);
 

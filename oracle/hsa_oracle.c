@@ -34,22 +34,37 @@ struct or_index {
     uint64_t queries;   /* rank queries issued (statistics only) */
 };
 
+static uint32_t rev_pairs32(uint32_t x)   /* reverse the order of the 16 2-bit fields */
+{
+    x = (x >> 16) | (x << 16);
+    x = ((x & 0xFF00FF00u) >> 8) | ((x & 0x00FF00FFu) << 8);
+    x = ((x & 0xF0F0F0F0u) >> 4) | ((x & 0x0F0F0F0Fu) << 4);
+    return ((x & 0xCCCCCCCCu) >> 2) | ((x & 0x33333333u) << 2);
+}
+
 static void bwt_init(or_bwt_t *b, uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code)
 {
-    /* .bwt words: char j of word at bits 31-2j..30-2j (BWT.c:156-181, BWTConstruct.c:1209) */
-    uint64_t nw = ((uint64_t)T + 31) / 32;
+    /* .bwt words: char j of a word at bits 31-2j..30-2j (BWT.c:156-181, BWTConstruct.c:1209) */
+    uint64_t nw = ((uint64_t)T + 31) / 32, ncw = ((uint64_t)T + 15) / 16;
     b->T = T; b->isa0 = isa0;
     memcpy(b->C, C, 5 * sizeof(uint32_t));
     b->w = (uint64_t *)calloc(nw + 1, sizeof(uint64_t));
     b->cnt = (uint32_t *)calloc((nw + 2) * 4, sizeof(uint32_t));
-    for (uint64_t p = 0; p < T; ++p) {
-        uint32_t c = (code[p >> 4] >> (30 - 2 * (p & 15))) & 3;
-        b->w[p >> 5] |= (uint64_t)c << (2 * (p & 31));
+    for (uint64_t q = 0; q < nw; ++q) {
+        uint64_t lo = rev_pairs32(code[2 * q]);
+        uint64_t hi = 2 * q + 1 < ncw ? rev_pairs32(code[2 * q + 1]) : 0;
+        b->w[q] = lo | hi << 32;
     }
+    if (T & 31) b->w[nw - 1] &= (1ull << (2 * (T & 31))) - 1;   /* BWTClearTrailingBwtCode */
     uint32_t acc[4] = {0, 0, 0, 0};
     for (uint64_t q = 0; q <= nw; ++q) {
         memcpy(b->cnt + q * 4, acc, sizeof acc);
-        for (uint64_t p = q * 32; p < q * 32 + 32 && p < T; ++p) acc[(b->w[q] >> (2 * (p & 31))) & 3]++;
+        if (q == nw) break;
+        uint64_t x = b->w[q], lo = x & 0x5555555555555555ull, hi = (x >> 1) & 0x5555555555555555ull;
+        uint32_t n3 = (uint32_t)__builtin_popcountll(lo & hi);
+        uint32_t n1 = (uint32_t)__builtin_popcountll(lo) - n3, n2 = (uint32_t)__builtin_popcountll(hi) - n3;
+        uint32_t valid = (q + 1) * 32 <= T ? 32u : (uint32_t)(T - q * 32);
+        acc[0] += valid - n1 - n2 - n3; acc[1] += n1; acc[2] += n2; acc[3] += n3;
     }
 }
 

@@ -65,3 +65,20 @@ def parse_opts(args, base):
         o["max_gape"] = opte
         o["mode"] &= ~0x01
     return o
+
+
+def main_path_digest(n_aln, flags, hits):
+    """Same definition as tools/make_golden.py hits_digest()."""
+    import hashlib
+    h = hashlib.sha256()
+    splice = (np.asarray(flags) & 1).astype(bool)
+    na = np.where(splice, -1, np.asarray(n_aln, np.int32)).astype(np.int32)
+    h.update(na.tobytes())
+    keep = np.repeat(~splice, np.maximum(np.asarray(n_aln, np.int64), 0))
+    h.update(np.ascontiguousarray(np.asarray(hits, np.uint32)[keep], np.uint32).tobytes())
+    return h.hexdigest()
+
+
+def ecoli_manifest():
+    with open(os.path.join(GOLD, "manifest_ecoli.json")) as f:
+        return json.load(f)

@@ -80,10 +80,15 @@ def save_case(name, index, seqs, args, batch, n_aln, flags, hits):
 
 
 def hits_digest(n_aln, flags, hits) -> str:
+    """Digest of the main-path result: splice-fallback flags, and n_aln + hit words
+    of every read that did NOT go to bwt_splice_match (splice hits are out of scope
+    for the GPU path; their reads are marked -1)."""
     h = hashlib.sha256()
-    h.update(np.ascontiguousarray(n_aln, np.int32).tobytes())
-    h.update(np.ascontiguousarray(flags, np.uint32).tobytes())
-    h.update(np.ascontiguousarray(hits, np.uint32).tobytes())
+    splice = (np.asarray(flags) & 1).astype(bool)
+    na = np.where(splice, -1, np.asarray(n_aln, np.int32)).astype(np.int32)
+    h.update(na.tobytes())
+    keep = np.repeat(~splice, np.maximum(np.asarray(n_aln, np.int64), 0))
+    h.update(np.ascontiguousarray(np.asarray(hits, np.uint32)[keep], np.uint32).tobytes())
     return h.hexdigest()
 
 
