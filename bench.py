@@ -25,6 +25,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
+import hsa_amd  # noqa: E402,F401  (loads libhsa_gpu.so before torch: hsa_amd/_lib.py)
+
 GENOME_T = 3_000_000_005
 GENOME_SEED = 1234
 RECORDS = 24

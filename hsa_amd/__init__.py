@@ -6,7 +6,14 @@ include/hsa_bwtaln.h).  This package holds its Python binding (`_lib`), the
 index file readers/writers (`index_io`) and the synthetic data generators
 (`synth`).  Nothing here computes alignments on the CPU.
 """
+import os as _os
+
 from . import index_io, synth  # noqa: F401
+
+# Load the HIP library before anything imports torch (see _lib._check_runtime).
+if _os.path.exists(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "libhsa_gpu.so")):
+    from . import _lib as _l
+    _l.lib()
 
 __all__ = ["index_io", "synth", "lib"]
 

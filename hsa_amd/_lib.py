@@ -85,13 +85,29 @@ class DeviceBatch(C.Structure):
 _lib = None
 
 
+def _check_runtime():
+    """libhsa_gpu.so is built against /opt/rocm's HIP runtime.  PyTorch-ROCm bundles
+    an older HIP/HSA runtime with the same sonames; whichever is loaded first serves
+    both.  With torch's loaded first the library sees no device, so the package must
+    be imported before torch (hsa_amd/__init__.py loads the library eagerly)."""
+    try:
+        maps = open("/proc/self/maps").read()
+    except OSError:
+        return
+    hip = {ln.split()[-1] for ln in maps.splitlines() if "libamdhip64" in ln}
+    if any("/torch/lib/" in h for h in hip):
+        raise HsaError("the HIP runtime bundled with torch was loaded before libhsa_gpu.so: "
+                       "import hsa_amd before importing torch")
+
+
 def lib():
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise HsaError(f"{LIB_PATH} is missing: build it with `make -C hsa_amd/csrc` (no CPU fallback exists)")
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    _check_runtime()
     u32 = np.ctypeslib.ndpointer(np.uint32, flags="C")
     u64 = np.ctypeslib.ndpointer(np.uint64, flags="C")
     i32 = np.ctypeslib.ndpointer(np.int32, flags="C")

@@ -12,3 +12,6 @@ if TESTS not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+
+# the product library must be loaded before torch (hsa_amd/_lib.py _check_runtime)
+import hsa_amd  # noqa: E402,F401
