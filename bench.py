@@ -131,7 +131,7 @@ def main():
     n_stacks = (opt.max_diff + 1) * opt.s_mm + (opt.max_gapo + 1) * opt.s_gapo + (opt.max_gape + 1) * opt.s_gape
     rg = Regime(s_mm=opt.s_mm, s_gapo=opt.s_gapo, s_gape=opt.s_gape, mode=0, indel_end_skip=opt.indel_end_skip,
                 max_del_occ=opt.max_del_occ, max_entries=opt.max_entries, max_gapo=0, max_gape=opt.max_gape,
-                max_seed_diff=opt.max_seed_diff, max_top2=opt.max_top2, n_stacks=n_stacks)
+                max_seed_diff=opt.max_seed_diff, max_top2=opt.max_top2, n_stacks=n_stacks, max_diff=opt.max_diff)
     jobs = np.zeros(a.batch, _lib.JOB_DTYPE)
     jobs["off"] = np.arange(a.batch, dtype=np.uint64) * READ_LEN
     jobs["len"] = READ_LEN
@@ -152,7 +152,8 @@ def main():
         o = outs[j]
         b = DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[j].data_ptr(),
                         d_n_aln=o["n"].data_ptr(), d_flags=o["f"].data_ptr(), d_hit_off=o["o"].data_ptr(),
-                        d_hits=o["h"].data_ptr(), hit_cap=hit_cap, d_counters=o["c"].data_ptr())
+                        d_hits=o["h"].data_ptr(), hit_cap=hit_cap, d_counters=o["c"].data_ptr(),
+                        max_len=READ_LEN, max_seed=opt.seed_len)
         gi.search_device([rg], b)
 
     lib_stream = torch.cuda.ExternalStream(gi.stream_handle())

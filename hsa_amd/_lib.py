@@ -60,7 +60,7 @@ class GapOpt(C.Structure):
 class Regime(C.Structure):
     _fields_ = [(k, C.c_int32) for k in ("s_mm", "s_gapo", "s_gape", "mode", "indel_end_skip", "max_del_occ",
                                          "max_entries", "max_gapo", "max_gape", "max_seed_diff", "max_top2",
-                                         "n_stacks")]
+                                         "n_stacks", "max_diff")]
 
 
 JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("max_diff", "<i4"), ("seed_len", "<i4"),
@@ -79,7 +79,8 @@ class Stats(C.Structure):
 class DeviceBatch(C.Structure):
     _fields_ = [("d_jobs", C.c_void_p), ("n_jobs", C.c_int), ("d_codes", C.c_void_p), ("d_n_aln", C.c_void_p),
                 ("d_flags", C.c_void_p), ("d_hit_off", C.c_void_p), ("d_hits", C.c_void_p),
-                ("hit_cap", C.c_uint64), ("d_counters", C.c_void_p)]
+                ("hit_cap", C.c_uint64), ("d_counters", C.c_void_p), ("max_len", C.c_int32),
+                ("max_seed", C.c_int32)]
 
 
 _lib = None

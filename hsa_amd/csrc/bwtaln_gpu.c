@@ -54,7 +54,7 @@ static int cal_maxdiff(int l, double err, double thres)
 
 static int aln_score(const gap_opt_t *o, int m, int g, int e) { return m * o->s_mm + g * o->s_gapo + e * o->s_gape; }
 
-static hsa_regime_t regime_of(const gap_opt_t *o, int n_stacks)
+static hsa_regime_t regime_of(const gap_opt_t *o, int n_stacks, int max_diff)
 {
     hsa_regime_t r;
     memset(&r, 0, sizeof r);
@@ -66,6 +66,7 @@ static hsa_regime_t regime_of(const gap_opt_t *o, int n_stacks)
     r.max_gapo = o->max_gapo; r.max_gape = o->max_gape;
     r.max_seed_diff = o->max_seed_diff; r.max_top2 = o->max_top2;
     r.n_stacks = n_stacks;
+    r.max_diff = max_diff;
     return r;
 }
 
@@ -169,7 +170,8 @@ long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint3
     if (opt->fnr > 0.0) local.max_diff = cal_maxdiff(max_len, BWA_AVG_ERR, opt->fnr);
     if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;
     const int n_stacks = aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
-    hsa_regime_t rg[2] = {regime_of(opt, n_stacks), regime_of(&local, n_stacks)};
+    /* every per-read max_diff of the call is <= local_opt.max_diff (bwtaln.c:264-267) */
+    hsa_regime_t rg[2] = {regime_of(opt, n_stacks, local.max_diff), regime_of(&local, n_stacks, local.max_diff)};
     const int equivalent = same_len && memcmp(&rg[0], &rg[1], sizeof rg[0]) == 0;
 
     int8_t *kind = (int8_t *)malloc((size_t)n + 1);

@@ -11,15 +11,26 @@
 // per lane (two Occ queries on one BWT, usually one 64-byte block), whatever the
 // lane is doing -- width extension, exact tail (bwt_match_exact) or expansion --
 // so all lanes issue their HBM loads together and the state machine in between
-// is register work.  Control that needs no rank (pruned pops, hits) loops
+// is register/LDS work.  Control that needs no rank (pruned pops, hits) loops
 // without touching the BWT.
 //
-// Stack (bwtgap.c:13-92): n_stacks score buckets, each a LIFO.  Here each
-// bucket is a singly linked list through a per-lane pool in HBM (16-byte entry +
-// 16-bit link), bucket heads live in LDS, a 128-bit mask in registers gives the
-// lowest non-empty bucket (== gap_stack_t.best).  The child pushed LAST by an
-// expansion is always the next pop (it is the top of the lowest bucket), so it
-// is kept in registers and never written ("virtual top").
+// Occupancy is what hides the HBM latency of the random rank loads, so the
+// per-lane state is packed to ~30 VGPRs (control words, one shared interval
+// register set for width/exact steps, stack entries decoded on demand) and the
+// kernel is bounded to 128 VGPRs = 4 waves per SIMD.
+//
+// Per-lane state in LDS (160 KiB per CU):
+//   * widths (bwt_width_t, bwtaln.h:36-39) as one byte per position:
+//     min(bid,127) | (w[p] == w[p+1]) << 7 -- everything bwt_match_gap's pruning
+//     reads (bwtgap.c:170, :256-263).  The full w values live in HBM and are only
+//     touched by gap_shadow (bwtgap.c:94-105) after an added hit.
+//   * the stack's bucket heads.  Buckets are the REACHABLE scores only (a score
+//     table per regime maps aln_score -> dense bucket, order preserved), so
+//     `-n 4 -o 0` needs 6 heads instead of the reference's 54 (bwtgap.c:18).
+// Stack entries (16 bytes + a 16-bit link) live in a per-lane pool in HBM; a
+// bit mask in registers gives the lowest non-empty bucket (== gap_stack_t.best).
+// The child pushed LAST by an expansion is always the next pop (it is the top of
+// the lowest bucket), so it stays in registers ("virtual top").
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -36,14 +47,16 @@
 #define ST_D 2
 #define NIL16 0xFFFFu
 #define BLOCK 256
+#define MAXB 128          // buckets per regime (and score table length)
 
-enum : int { PH_IDLE = 0, PH_WIDTH, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT };
+enum : uint32_t { PH_IDLE = 0, PH_WIDTH, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT };
 
 struct SearchArgs {
     RankDir fwd, rev;
     uint32_t T;
     uint32_t C[5];
     const hsa_regime_t *regimes;
+    const uint8_t *bmap;           // [2][MAXB]: aln_score -> dense bucket (0xFF: unreachable)
     const hsa_job_t *jobs;
     const int32_t *job_list;       // optional indirection (re-runs); null = identity
     int n_jobs;
@@ -53,20 +66,39 @@ struct SearchArgs {
     uint64_t *hit_off;
     uint32_t *hits;
     uint64_t hit_cap;
-    unsigned long long *ctr;       // [0] queue head [1] hit alloc [2] rank queries [3] blocks [4] pops
-    uint2 *width;                  // per lane wcap entries: back [0, maxl+1), seed [maxl+1, wcap)
+    unsigned long long *ctr;       // [0] queue head [1] hit alloc [2] rank queries [3] blocks [4] pops [5] errors
+    uint32_t *wg;                  // per lane wcap: full width_back w values (gap_shadow only)
     uint4 *pool;
     uint16_t *nxt;
     uint32_t *hbuf;
-    uint32_t wcap, seed_base, pcap, hcap, nb;
+    uint32_t wcap, pcap, hcap, nb;
+    uint32_t off_heads, off_wb, off_ws;   // LDS byte offsets
 };
 
 // entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
-__device__ __forceinline__ uint32_t meta_pack(int i, int st, int isd, int mm, int go, int ge)
+__device__ __forceinline__ uint32_t meta_pack(uint32_t i, uint32_t st, uint32_t isd, uint32_t mm, uint32_t go,
+                                              uint32_t ge)
 {
-    return (uint32_t)i | (uint32_t)st << 10 | (uint32_t)isd << 12 | (uint32_t)mm << 13 | (uint32_t)go << 20 |
-           (uint32_t)ge << 24;
+    return i | st << 10 | isd << 12 | mm << 13 | go << 20 | ge << 24;
 }
+#define M_I(m) ((int)((m) & 1023u))
+#define M_ST(m) ((int)(((m) >> 10) & 3u))
+#define M_ISD(m) ((int)(((m) >> 12) & 1u))
+#define M_MM(m) ((int)(((m) >> 13) & 127u))
+#define M_GO(m) ((int)(((m) >> 20) & 15u))
+#define M_GE(m) ((int)((m) >> 24))
+
+// control word: ph:3 | strand:1 | has_seed:1 | reg:1 | has_vt:1 | wseed:1 | ovf:2 | len:10 | seed_len:10
+#define C_PH(c) ((c) & 7u)
+#define C_STRAND(c) (((c) >> 3) & 1u)
+#define C_SEED(c) (((c) >> 4) & 1u)
+#define C_REG(c) (((c) >> 5) & 1u)
+#define C_VT(c) (((c) >> 6) & 1u)
+#define C_WSEED(c) (((c) >> 7) & 1u)
+#define C_OVF(c) (((c) >> 8) & 3u)
+#define C_LEN(c) ((int)(((c) >> 10) & 1023u))
+#define C_SLEN(c) ((int)(((c) >> 20) & 1023u))
+#define SET_PH(c, p) ((c) = ((c) & ~7u) | (p))
 
 __device__ __forceinline__ int int_log2(uint32_t v)   // bwtgap.c:107-116
 {
@@ -79,253 +111,312 @@ __device__ __forceinline__ int int_log2(uint32_t v)   // bwtgap.c:107-116
     return c;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_search(SearchArgs a)
-{
-    extern __shared__ uint16_t s_heads[];   // [nb][BLOCK]
-    const uint32_t tid = threadIdx.x;
-    const size_t gid = (size_t)blockIdx.x * BLOCK + tid;
-    const int lane = (int)(tid & 63);
-    uint2 *const wb = a.width + gid * a.wcap;
-    uint2 *const ws = wb + a.seed_base;
-    uint4 *const pool = a.pool + gid * a.pcap;
-    uint16_t *const nxt = a.nxt + gid * a.pcap;
-    uint32_t *const hb = a.hbuf + gid * (size_t)a.hcap * 9;
-#define HEAD(b) s_heads[(size_t)(b) * BLOCK + tid]
+template <int MW> struct BMask;
+template <> struct BMask<1> {
+    uint64_t m0 = 0;
+    __device__ __forceinline__ void clear() { m0 = 0; }
+    __device__ __forceinline__ bool any() const { return m0 != 0; }
+    __device__ __forceinline__ int lowest() const { return m0 ? __ffsll((unsigned long long)m0) - 1 : (1 << 30); }
+    __device__ __forceinline__ bool test(int b) const { return (m0 >> b) & 1ull; }
+    __device__ __forceinline__ void set(int b) { m0 |= 1ull << b; }
+    __device__ __forceinline__ void reset(int b) { m0 &= ~(1ull << b); }
+};
+template <> struct BMask<2> {
+    uint64_t m0 = 0, m1 = 0;
+    __device__ __forceinline__ void clear() { m0 = m1 = 0; }
+    __device__ __forceinline__ bool any() const { return (m0 | m1) != 0; }
+    __device__ __forceinline__ int lowest() const
+    {
+        if (m0) return __ffsll((unsigned long long)m0) - 1;
+        if (m1) return 64 + __ffsll((unsigned long long)m1) - 1;
+        return 1 << 30;
+    }
+    __device__ __forceinline__ bool test(int b) const { return b < 64 ? ((m0 >> b) & 1ull) : ((m1 >> (b - 64)) & 1ull); }
+    __device__ __forceinline__ void set(int b) { if (b < 64) m0 |= 1ull << b; else m1 |= 1ull << (b - 64); }
+    __device__ __forceinline__ void reset(int b) { if (b < 64) m0 &= ~(1ull << b); else m1 &= ~(1ull << (b - 64)); }
+};
 
-    // ---- per-read state
-    int ph = PH_IDLE;
+template <int MW>
+__global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
+{
+    extern __shared__ __align__(16) uint8_t s_lds[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gid = blockIdx.x * BLOCK + tid;
+    const int lane = (int)(tid & 63);
+    for (uint32_t t = tid; t < 2 * MAXB; t += BLOCK) s_lds[t] = a.bmap[t];
+    static_assert(2 * sizeof(hsa_regime_t) <= 128, "regime LDS slot");
+    hsa_regime_t *const s_reg = reinterpret_cast<hsa_regime_t *>(s_lds + 2 * MAXB);
+    if (tid < 2 * sizeof(hsa_regime_t) / 4)
+        reinterpret_cast<uint32_t *>(s_reg)[tid] = reinterpret_cast<const uint32_t *>(a.regimes)[tid];
+    __syncthreads();
+    uint16_t *const s_heads = reinterpret_cast<uint16_t *>(s_lds + a.off_heads);
+    uint8_t *const s_wb = s_lds + a.off_wb;
+    uint8_t *const s_ws = s_lds + a.off_ws;
+#define WG(p) a.wg[(size_t)gid * a.wcap + (uint32_t)(p)]
+#define POOL(s) a.pool[(size_t)gid * a.pcap + (uint32_t)(s)]
+#define NXT(s) a.nxt[(size_t)gid * a.pcap + (uint32_t)(s)]
+#define HB(i) a.hbuf[(size_t)gid * a.hcap * 9 + (uint32_t)(i)]
+#define HEAD(b) s_heads[(uint32_t)(b) * BLOCK + tid]
+#define WB(p) s_wb[(uint32_t)(p) * BLOCK + tid]
+#define WS(p) s_ws[(uint32_t)(p) * BLOCK + tid]
+#define RG(f) (s_reg[C_REG(ctl)].f)
+
+    // ---- persistent per-lane state (~30 registers)
+    uint32_t ctl = PH_IDLE;        // control word (C_* accessors)
     int job = -1;
-    uint64_t off = 0;
-    int len = 0, strand = 1, has_seed = 0, seed_len = 0, opt_max_diff = 0;
-    hsa_regime_t R;
-    // width
-    int wpos = 0, wlen = 0, wstart = 0, wseed = 0, wbid = 0;
-    uint32_t wk = 0, wl = 0;
-    // search
-    int best_score = 0, best_diff = 0, max_diff = 0, best_cnt = 0, n_aln = 0, n_entries = 0;
+    uint32_t off = 0;              // read offset in codes
+    uint32_t pen = 0;              // s_mm | s_gapo << 10 | s_gape << 20
+    uint32_t rmode = 0;            // mode | max_gapo << 8 | max_gape << 16
+    uint32_t pos = 0;              // wpos:11 | wbid:11 (width) -- or -- xj (exact)
+    uint32_t ik = 0, il = 0;       // width / exact-tail interval
+    uint32_t aux = 0;              // width: w of the previous position; exact: rev_l
+    int opt_max_diff = 0, max_diff = 0, best_score = 0, best_cnt = 0, n_aln = 0, n_entries = 0;
     uint32_t pool_top = 0;
-    uint64_t mask0 = 0, mask1 = 0;
-    int has_vt = 0;
+    BMask<MW> mask;
     uint4 vt = make_uint4(0, 0, 0, 0);
-    int pend = 0, pend_score = 0;
-    uint4 pendv = make_uint4(0, 0, 0, 0);
-    // current entry
-    uint32_t ek = 0, el = 0, erk = 0, erl = 0;
-    int ei = 0, est = 0, eisd = 0, emm = 0, ego = 0, ege = 0, em = 0, em_seed = 0;
-    // exact tail
-    uint32_t xk = 0, xl = 0, xrk = 0, xrl = 0;
-    int xj = 0;
-    // statistics
-    uint64_t st_q = 0, st_b = 0, st_p = 0;
-    int overflow = 0;
+    uint4 e = make_uint4(0, 0, 0, 0);    // current entry (k, l, rev_k, meta)
+    uint32_t st_q = 0, st_b = 0, st_p = 0;
+
+#define S_MM ((int)(pen & 1023u))
+#define S_GO ((int)((pen >> 10) & 1023u))
+#define S_GE ((int)(pen >> 20))
+#define R_MODE ((int)(rmode & 255u))
+#define R_MAXGO ((int)((rmode >> 8) & 255u))
+#define R_MAXGE ((int)(rmode >> 16))
+#define SCORE(mm, go, ge) ((mm) * S_MM + (go) * S_GO + (ge) * S_GE)
+#define WPOS ((int)(pos & 2047u))
+#define WBID ((int)(pos >> 11))
 
     auto getc = [&](int p) -> uint32_t {
-        uint32_t c = a.codes[off + (strand ? (uint64_t)(len - 1 - p) : (uint64_t)p)];
-        return strand ? (c < 4 ? 3u - c : c) : c;
+        const int len = C_LEN(ctl);
+        if (C_STRAND(ctl)) {
+            const uint32_t c = a.codes[off + (uint32_t)(len - 1 - p)];
+            return c < 4 ? 3u - c : c;
+        }
+        return a.codes[off + (uint32_t)p];
     };
-    auto score_of = [&](int mm, int go, int ge) -> int { return mm * R.s_mm + go * R.s_gapo + ge * R.s_gape; };
-
     auto start_width = [&]() {
-        wseed = has_seed;
-        wstart = has_seed ? len - seed_len : 0;
-        wlen = has_seed ? seed_len : len;
-        wpos = 0; wk = 0; wl = a.T; wbid = 0;
-        ph = PH_WIDTH;
+        ctl = (ctl & ~(1u << 7)) | (C_SEED(ctl) << 7);   // wseed = has_seed
+        pos = 0; ik = 0; il = a.T;
+        SET_PH(ctl, PH_WIDTH);
+    };
+    auto wlen = [&]() -> int { return C_WSEED(ctl) ? C_SLEN(ctl) : C_LEN(ctl); };
+    auto wstart = [&]() -> int { return C_WSEED(ctl) ? C_LEN(ctl) - C_SLEN(ctl) : 0; };
+    // store position WPOS of the width being computed (bwtaln.c:95-96)
+    auto put_width = [&](uint32_t w) {
+        const int p = WPOS;
+        const uint32_t bq = WBID < 127 ? (uint32_t)WBID : 127u;
+        if (C_WSEED(ctl)) {
+            if (p > 0 && aux == w) WS(p - 1) |= 0x80;
+            WS(p) = (uint8_t)bq;
+        } else {
+            if (p > 0 && aux == w) WB(p - 1) |= 0x80;
+            WB(p) = (uint8_t)bq;
+            WG(p) = w;
+        }
+        aux = w;
+        pos += 1;
     };
     auto flush = [&](uint4 v, int b) {
-        if (pool_top >= a.pcap || (uint32_t)b >= a.nb) { overflow = 1; return; }
+        if (pool_top >= a.pcap || (uint32_t)b >= a.nb) { ctl |= 1u << 8; return; }
         const uint32_t slot = pool_top++;
-        const bool nonempty = b < 64 ? ((mask0 >> b) & 1ull) : ((mask1 >> (b - 64)) & 1ull);
-        pool[slot] = v;
-        nxt[slot] = nonempty ? HEAD(b) : (uint16_t)NIL16;
+        POOL(slot) = v;
+        NXT(slot) = mask.test(b) ? HEAD(b) : (uint16_t)NIL16;
         HEAD(b) = (uint16_t)slot;
-        if (b < 64) mask0 |= 1ull << b; else mask1 |= 1ull << (b - 64);
-    };
-    auto push = [&](int i, uint32_t k, uint32_t l, uint32_t rk, int mm, int go, int ge, int st, int isd) {
-        if (pend) flush(pendv, pend_score);
-        pendv = make_uint4(k, l, rk, meta_pack(i, st, isd, mm, go, ge));
-        pend_score = score_of(mm, go, ge);
-        pend = 1;
-        ++n_entries;
+        mask.set(b);
     };
     auto start_search = [&]() {
-        best_score = score_of(opt_max_diff + 1, R.max_gapo + 1, R.max_gape + 1);
-        best_diff = opt_max_diff + 1;
+        best_score = SCORE(opt_max_diff + 1, R_MAXGO + 1, R_MAXGE + 1);
         max_diff = opt_max_diff;
         best_cnt = 0; n_aln = 0;
-        mask0 = mask1 = 0; pool_top = 0; pend = 0;
-        // root entry (bwtgap.c:142) as the virtual top
-        vt = make_uint4(0, a.T, 0, meta_pack(len, ST_M, 0, 0, 0, 0));
-        has_vt = 1;
+        mask.clear(); pool_top = 0;
+        vt = make_uint4(0, a.T, 0, meta_pack((uint32_t)C_LEN(ctl), ST_M, 0, 0, 0, 0));   // root (bwtgap.c:142)
+        ctl |= 1u << 6;
         n_entries = 1;
-        ph = PH_POP;
+        SET_PH(ctl, PH_POP);
     };
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
         a.n_aln[job] = na;
         a.flags[job] = fl;
         a.hit_off[job] = ho;
-        ph = PH_IDLE;
+        SET_PH(ctl, PH_IDLE);
     };
     auto end_strand = [&]() {
         if (n_aln > 0) {
             const unsigned long long o = atomicAdd(&a.ctr[1], (unsigned long long)n_aln);
             if (o + (uint64_t)n_aln > a.hit_cap) { finish_job(HSA_F_OVERFLOW, 0, 0); return; }
             uint32_t *dst = a.hits + o * 9;
+            const uint32_t s30 = C_STRAND(ctl) << 30;
             for (int h = 0; h < n_aln; ++h) {
-                const uint32_t *s = hb + h * 9;
-                dst[h * 9 + 0] = s[0];
-                dst[h * 9 + 1] = s[1];
-                dst[h * 9 + 2] = s[2];
-                dst[h * 9 + 3] = s[3];
-                dst[h * 9 + 4] = s[4];
-                dst[h * 9 + 5] = (uint32_t)strand << 30;
+                dst[h * 9 + 0] = HB(h * 9 + 0);
+                dst[h * 9 + 1] = HB(h * 9 + 1);
+                dst[h * 9 + 2] = HB(h * 9 + 2);
+                dst[h * 9 + 3] = HB(h * 9 + 3);
+                dst[h * 9 + 4] = HB(h * 9 + 4);
+                dst[h * 9 + 5] = s30;
                 dst[h * 9 + 6] = 0;
-                dst[h * 9 + 7] = h == 0 ? (uint32_t)(len - 1) : 0u;   // bwtaln.c:371-372
-                dst[h * 9 + 8] = s[8];
+                dst[h * 9 + 7] = h == 0 ? (uint32_t)(C_LEN(ctl) - 1) : 0u;   // bwtaln.c:371-372
+                dst[h * 9 + 8] = HB(h * 9 + 8);
             }
             finish_job(0, n_aln, o);
-        } else if (strand == 1) {
-            strand = 0;
+        } else if (C_STRAND(ctl)) {
+            ctl &= ~(1u << 3);          // strand 0
             start_width();
         } else {
             finish_job(HSA_F_FALLBACK, 0, 0);
         }
     };
-    // hit handling (bwtgap.c:188-243); returns false when the search must stop
+    // hit handling (bwtgap.c:188-243) for entry e with final interval (k,l,rk,rl);
+    // returns false when the search must stop
     auto on_hit = [&](uint32_t k, uint32_t l, uint32_t rk, uint32_t rl) -> bool {
-        const int score = score_of(emm, ego, ege);
+        const uint32_t m = e.w;
+        const int score = SCORE(M_MM(m), M_GO(m), M_GE(m));
         if (n_aln == 0) {
             best_score = score;
-            best_diff = emm + ego + ((R.mode & MODE_GAPE) ? ege : 0);
-            if (!(R.mode & MODE_NONSTOP)) max_diff = (best_diff + 1 > opt_max_diff) ? opt_max_diff : best_diff + 1;
+            const int best_diff = M_MM(m) + M_GO(m) + ((R_MODE & MODE_GAPE) ? M_GE(m) : 0);
+            if (!(R_MODE & MODE_NONSTOP)) max_diff = (best_diff + 1 > opt_max_diff) ? opt_max_diff : best_diff + 1;
         }
         if (score == best_score) best_cnt = (int)((uint32_t)best_cnt + (l - k + 1u));
-        else if (best_cnt > R.max_top2) return false;
+        else if (best_cnt > RG(max_top2)) return false;
         bool add = true;
-        if (ego) {
+        if (M_GO(m)) {
             for (int j = 0; j < n_aln; ++j)
-                if (hb[j * 9 + 1] == k && hb[j * 9 + 2] == l) { add = false; break; }
+                if (HB(j * 9 + 1) == k && HB(j * 9 + 2) == l) { add = false; break; }
         }
         if (add) {
-            if ((uint32_t)n_aln >= a.hcap) { overflow = 1; return false; }
-            // gap_shadow (bwtgap.c:94-105) on width_back[0, last_diff_pos)
+            if ((uint32_t)n_aln >= a.hcap) { ctl |= 1u << 8; return false; }
+            // gap_shadow (bwtgap.c:94-105) on width_back[0, last_diff_pos), then the
+            // pruning bytes of those positions (eq bit of p needs w[p+1])
             const uint32_t x = l - k + 1u;
-            const int ldp = eisd ? ei : 0;
-            uint32_t jj = 0;
-            for (int p = 0; p < ldp; ++p) {
-                uint2 w = wb[p];
-                if (w.x > x) { w.x -= x; wb[p] = w; }
-                else if (w.x == x) { w.y = 1; w.x = a.T - (++jj); wb[p] = w; }
+            const int ldp = M_ISD(m) ? M_I(m) : 0;
+            if (ldp > 0) {
+                uint32_t jj = 0;
+                for (int p = 0; p < ldp; ++p) {
+                    uint32_t w = WG(p);
+                    if (w > x) { w -= x; WG(p) = w; }
+                    else if (w == x) { WB(p) = (uint8_t)((WB(p) & 0x80u) | 1u); WG(p) = a.T - (++jj); }
+                }
+                uint32_t wnext = WG(ldp);
+                for (int p = ldp - 1; p >= 0; --p) {
+                    const uint32_t w = WG(p);
+                    WB(p) = (uint8_t)((WB(p) & 0x7fu) | (w == wnext ? 0x80u : 0u));
+                    wnext = w;
+                }
             }
-            uint32_t *h = hb + n_aln * 9;
-            h[0] = (uint32_t)emm | (uint32_t)ego << 16 | (uint32_t)ege << 24;
-            h[1] = k; h[2] = l; h[3] = rk; h[4] = rl;
-            h[8] = (uint32_t)score;
+            HB(n_aln * 9 + 0) = (uint32_t)M_MM(m) | (uint32_t)M_GO(m) << 16 | (uint32_t)M_GE(m) << 24;
+            HB(n_aln * 9 + 1) = k; HB(n_aln * 9 + 2) = l; HB(n_aln * 9 + 3) = rk; HB(n_aln * 9 + 4) = rl;
+            HB(n_aln * 9 + 8) = (uint32_t)score;
             ++n_aln;
         }
         return true;
     };
-
-    // request for this iteration's rank step
-    int req = 0, rdir = 0;
-    uint32_t rp1 = 0, rp2 = 0;
+    // m (available differences) of entry e (bwtgap.c:160-163)
+    auto m_of = [&](uint32_t m) -> int {
+        int mm = max_diff - (M_MM(m) + M_GO(m));
+        if (R_MODE & MODE_GAPE) mm -= M_GE(m);
+        return mm;
+    };
 
     for (;;) {
         // ---------------- (A) read acquisition, wave aggregated
         {
-            const bool need = (ph == PH_IDLE);
-            const uint64_t m = __ballot(need);
-            if (m) {
-                const int leader = __ffsll((unsigned long long)m) - 1;
+            const bool need = C_PH(ctl) == PH_IDLE;
+            const uint64_t mb = __ballot(need);
+            if (mb) {
+                const int leader = __ffsll((unsigned long long)mb) - 1;
                 unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(&a.ctr[0], (unsigned long long)__popcll(m));
+                if (lane == leader) base = atomicAdd(&a.ctr[0], (unsigned long long)__popcll(mb));
                 base = __shfl(base, leader);
                 if (need) {
-                    const unsigned long long j = base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+                    const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
                     if (j < (unsigned long long)a.n_jobs) {
                         job = a.job_list ? a.job_list[j] : (int)j;
                         const hsa_job_t J = a.jobs[job];
-                        off = J.off; len = (int)J.len; opt_max_diff = J.max_diff;
-                        seed_len = J.seed_len;
-                        R = a.regimes[J.regime];
-                        has_seed = len > seed_len;
-                        strand = 1;
-                        overflow = 0;
+                        off = (uint32_t)J.off;
+                        opt_max_diff = J.max_diff;
+                        const uint32_t len = J.len;
+                        const uint32_t has_seed = (int)len > J.seed_len;
+                        ctl = 8u | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 | len << 10 |
+                              (has_seed ? (uint32_t)J.seed_len : 0u) << 20;     // strand 1 (rc first, bwtaln.c:343)
+                        const hsa_regime_t *R = s_reg + (J.regime & 1);
+                        pen = (uint32_t)R->s_mm | (uint32_t)R->s_gapo << 10 | (uint32_t)R->s_gape << 20;
+                        rmode = (uint32_t)R->mode | (uint32_t)R->max_gapo << 8 | (uint32_t)R->max_gape << 16;
+                        if (opt_max_diff > R->max_diff) ctl |= 2u << 8;
                         start_width();
                     } else {
-                        ph = PH_EXIT;
+                        SET_PH(ctl, PH_EXIT);
                     }
                 }
             }
         }
-        if (__all(ph == PH_EXIT)) break;
+        if (__all(C_PH(ctl) == PH_EXIT)) break;
 
         // ---------------- (B) control until a rank step is needed
-        req = 0;
-        while (ph != PH_EXIT && ph != PH_IDLE && !req) {
-            if (overflow) { finish_job(HSA_F_OVERFLOW, 0, 0); break; }
+        int req = 0, rdir = 0;
+        uint32_t rp1 = 0, rp2 = 0;
+        while (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && !req) {
+            if (C_OVF(ctl)) {
+                if (C_OVF(ctl) > 1) atomicAdd(&a.ctr[5], 1ull);
+                finish_job(HSA_F_OVERFLOW, 0, 0);
+                break;
+            }
+            const uint32_t ph = C_PH(ctl);
             if (ph == PH_WIDTH) {
                 // bwt_cal_width type 1 (bwtaln.c:84-97)
-                while (wpos < wlen) {
-                    const uint32_t c = getc(wstart + wpos);
+                const int wl = wlen(), ws0 = wstart();
+                while (WPOS < wl) {
+                    const uint32_t c = getc(ws0 + WPOS);
                     if (c < 4) break;
-                    wk = 0; wl = a.T; ++wbid;                               // N: restart
-                    (wseed ? ws : wb)[wpos] = make_uint2(wl - wk + 1u, (uint32_t)wbid);
-                    ++wpos;
+                    ik = 0; il = a.T; pos += 1u << 11;                       // N: restart, ++bid
+                    put_width(il - ik + 1u);
                 }
-                if (wpos < wlen) { req = 1; rdir = 1; rp1 = wk; rp2 = wl + 1u; break; }
-                (wseed ? ws : wb)[wlen] = make_uint2(0u, (uint32_t)(++wbid));
-                if (wseed) { wseed = 0; wstart = 0; wlen = len; wpos = 0; wk = 0; wl = a.T; wbid = 0; }
+                if (WPOS < wl) { req = 1; rdir = 1; rp1 = ik; rp2 = il + 1u; break; }
+                pos += 1u << 11;
+                put_width(0u);                                              // width[len] = {0, ++bid}
+                if (C_WSEED(ctl)) { ctl &= ~(1u << 7); pos = 0; ik = 0; il = a.T; }
                 else start_search();
                 continue;
             }
             if (ph == PH_EXACT) {
-                const uint32_t c = getc(xj);
-                if (c > 3) { ph = PH_POP; continue; }                     // 2BWT-Interface.c:377
-                req = 1; rdir = 0; rp1 = xk; rp2 = xl + 1u;
+                const uint32_t c = getc((int)pos);
+                if (c > 3) { SET_PH(ctl, PH_POP); continue; }              // 2BWT-Interface.c:377
+                req = 1; rdir = 0; rp1 = ik; rp2 = il + 1u;
                 break;
             }
             // PH_POP: bwtgap.c:144-186
-            if (n_entries == 0 || n_entries > R.max_entries) { end_strand(); continue; }
-            uint4 e;
-            if (has_vt) {
-                e = vt; has_vt = 0;
+            if (n_entries == 0 || n_entries > RG(max_entries)) { end_strand(); continue; }
+            if (C_VT(ctl)) {
+                e = vt; ctl &= ~(1u << 6);
             } else {
-                int b;
-                if (mask0) b = __ffsll((unsigned long long)mask0) - 1;
-                else b = 64 + __ffsll((unsigned long long)mask1) - 1;
+                const int b = mask.lowest();
                 const uint32_t slot = HEAD(b);
-                e = pool[slot];
-                const uint16_t nx = nxt[slot];
-                if (nx == NIL16) { if (b < 64) mask0 &= ~(1ull << b); else mask1 &= ~(1ull << (b - 64)); }
+                e = POOL(slot);
+                const uint16_t nx = NXT(slot);
+                if (nx == NIL16) mask.reset(b);
                 else HEAD(b) = nx;
             }
             --n_entries;
             ++st_p;
-            ek = e.x; el = e.y; erk = e.z; erl = erk + (el - ek);
-            ei = (int)(e.w & 1023u); est = (int)((e.w >> 10) & 3u); eisd = (int)((e.w >> 12) & 1u);
-            emm = (int)((e.w >> 13) & 127u); ego = (int)((e.w >> 20) & 15u); ege = (int)(e.w >> 24);
-            if (!(R.mode & MODE_NONSTOP) && score_of(emm, ego, ege) > best_score + R.s_mm) { end_strand(); continue; }
-            em = max_diff - (emm + ego);
-            if (R.mode & MODE_GAPE) em -= ege;
+            const uint32_t m = e.w;
+            if (!(R_MODE & MODE_NONSTOP) && SCORE(M_MM(m), M_GO(m), M_GE(m)) > best_score + S_MM) {
+                end_strand();
+                continue;
+            }
+            const int em = m_of(m);
             if (em < 0) continue;
-            if (has_seed) {
-                em_seed = R.max_seed_diff - (emm + ego);
-                if (R.mode & MODE_GAPE) em_seed -= ege;
-            }
-            if (ei > 0 && em < (int)wb[ei - 1].y) continue;
+            const int ei = M_I(m);
+            if (ei > 0 && em < (int)(WB(ei - 1) & 0x7fu)) continue;
             if (ei == 0) {
-                if (!on_hit(ek, el, erk, erl) && !overflow) end_strand();
+                if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) end_strand();
                 continue;
             }
-            if (em == 0 && (est == ST_M || (R.mode & MODE_GAPE) || ege == R.max_gape)) {
-                xk = ek; xl = el; xrk = erk; xrl = erl; xj = ei - 1;
-                ph = PH_EXACT;
+            if (em == 0 && (M_ST(m) == ST_M || (R_MODE & MODE_GAPE) || M_GE(m) == R_MAXGE)) {
+                ik = e.x; il = e.y; aux = e.z + (e.y - e.x); pos = (uint32_t)(ei - 1);   // bwt_match_exact
+                SET_PH(ctl, PH_EXACT);
                 continue;
             }
-            --ei;
-            req = 1; rdir = 0; rp1 = ek; rp2 = el + 1u;
-            ph = PH_EXPAND;
+            req = 1; rdir = 0; rp1 = e.x; rp2 = e.y + 1u;
+            SET_PH(ctl, PH_EXPAND);
         }
 
         // ---------------- (C) the rank step
@@ -336,68 +427,96 @@ __global__ void __launch_bounds__(BLOCK) k_search(SearchArgs a)
         }
 
         // ---------------- (D) apply
+        const uint32_t ph = C_PH(ctl);
         if (req && ph == PH_WIDTH) {
-            const uint32_t c = getc(wstart + wpos);
-            wk = a.C[c] + oa[c] + 1u;
-            wl = a.C[c] + ob[c];
-            if (wk > wl) { wk = 0; wl = a.T; ++wbid; }
-            (wseed ? ws : wb)[wpos] = make_uint2(wl - wk + 1u, (uint32_t)wbid);
-            ++wpos;
+            const uint32_t c = getc(wstart() + WPOS);
+            ik = a.C[c] + oa[c] + 1u;
+            il = a.C[c] + ob[c];
+            if (ik > il) { ik = 0; il = a.T; pos += 1u << 11; }
+            put_width(il - ik + 1u);
         } else if (req && ph == PH_EXACT) {
             // BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170), one character
-            const uint32_t c = getc(xj);
+            const uint32_t c = getc((int)pos);
             uint32_t oc = 0;
             for (uint32_t d = c + 1; d < 4; ++d) oc += ob[d] - oa[d];
-            const uint32_t nk = a.C[c] + oa[c] + 1u, nl = a.C[c] + ob[c];
-            const uint32_t nrl = xrl - oc;
-            xk = nk; xl = nl; xrl = nrl; xrk = nrl - (nl - nk);
-            if (xk > xl) {
-                ph = PH_POP;                                             // no match: continue (bwtgap.c:185)
-            } else if (--xj < 0) {
+            ik = a.C[c] + oa[c] + 1u;
+            il = a.C[c] + ob[c];
+            aux -= oc;                                                   // rev_l
+            if (ik > il) {
+                SET_PH(ctl, PH_POP);                                     // no match: continue (bwtgap.c:185)
+            } else if (pos-- == 0) {
                 // write-back guard of bwt_match_exact (2BWT-Interface.c:383-386)
-                const uint32_t hk = ek ? xk : ek, hl = el ? xl : el, hrk = erk ? xrk : erk, hrl = erl ? xrl : erl;
-                ph = PH_POP;
-                if (!on_hit(hk, hl, hrk, hrl) && !overflow) end_strand();
+                const uint32_t rk = aux - (il - ik), erl = e.z + (e.y - e.x);
+                const uint32_t hk = e.x ? ik : 0u, hl = e.y ? il : 0u, hrk = e.z ? rk : 0u, hrl = erl ? aux : 0u;
+                SET_PH(ctl, PH_POP);
+                if (!on_hit(hk, hl, hrk, hrl) && !C_OVF(ctl)) end_strand();
             }
         } else if (req && ph == PH_EXPAND) {
             // children of the bidirectional step (2BWT-Interface.c:235-272)
-            uint32_t sk[4], sl[4], srk[4], oc[4];
-            oc[3] = 0;
-            for (int c = 2; c >= 0; --c) oc[c] = oc[c + 1] + ob[c + 1] - oa[c + 1];
-            for (int c = 0; c < 4; ++c) {
-                sk[c] = a.C[c] + oa[c] + 1u;
-                sl[c] = a.C[c] + ob[c];
-                const uint32_t rl = erl - oc[c];
-                srk[c] = rl - (sl[c] - sk[c]);
+            const uint32_t m = e.w;
+            const uint32_t ek = e.x, el = e.y, erk = e.z, erl = erk + (el - ek);
+            const int i = M_I(m) - 1;                                    // --i (bwtgap.c:245)
+            const int est = M_ST(m), emm = M_MM(m), ego = M_GO(m), ege = M_GE(m);
+            const int em = m_of(m);
+            const int len = C_LEN(ctl);
+            uint32_t sk[4], sl[4], srk[4];
+            {
+                uint32_t oc = 0;
+                for (int c = 3; c >= 0; --c) {
+                    sk[c] = a.C[c] + oa[c] + 1u;
+                    sl[c] = a.C[c] + ob[c];
+                    srk[c] = (erl - oc) - (sl[c] - sk[c]);
+                    oc += ob[c] - oa[c];
+                }
             }
-            const int i = ei;
             const uint32_t occ = el - ek + 1u;
             int allow_diff = 1, allow_M = 1;
             if (i > 0) {
-                const uint2 w1 = wb[i - 1], w0 = wb[i];
-                if ((int)w1.y > em - 1) allow_diff = 0;
-                else if ((int)w1.y == em - 1 && (int)w0.y == em - 1 && w1.x == w0.x) allow_M = 0;
-                const int ii = i - (len - seed_len);
-                if (has_seed && ii > 0) {
-                    const uint2 s1 = ws[ii - 1], s0 = ws[ii];
-                    if ((int)s1.y > em_seed - 1) allow_diff = 0;
-                    else if ((int)s1.y == em_seed - 1 && (int)s0.y == em_seed - 1 && s1.x == s0.x) allow_M = 0;
+                // width[i-1].bid, width[i].bid and w[i-1] == w[i] (bwtgap.c:256-258)
+                const uint32_t w1 = WB(i - 1), w0 = WB(i);
+                const int b1 = (int)(w1 & 0x7fu), b0 = (int)(w0 & 0x7fu);
+                if (b1 > em - 1) allow_diff = 0;
+                else if (b1 == em - 1 && b0 == em - 1 && (w1 & 0x80u)) allow_M = 0;
+                const int ii = i - (len - C_SLEN(ctl));
+                if (C_SEED(ctl) && ii > 0) {
+                    int ems = RG(max_seed_diff) - (emm + ego);
+                    if (R_MODE & MODE_GAPE) ems -= ege;
+                    const uint32_t s1 = WS(ii - 1), s0 = WS(ii);
+                    const int c1 = (int)(s1 & 0x7fu), c0 = (int)(s0 & 0x7fu);
+                    if (c1 > ems - 1) allow_diff = 0;
+                    else if (c1 == ems - 1 && c0 == ems - 1 && (s1 & 0x80u)) allow_M = 0;
                 }
             }
-            const int tmp = (R.mode & MODE_LOGGAP) ? int_log2((uint32_t)(ege + ego)) / 2 + 1 : ego + ege;
-            if (allow_diff && i >= R.indel_end_skip + tmp && len - i >= R.indel_end_skip + tmp) {
-                if (est == ST_M) {
-                    if (ego < R.max_gapo) {
-                        push(i, ek, el, erk, emm, ego + 1, ege, ST_I, 1);
-                        for (int j = 0; j < 4; ++j)
-                            if (sk[j] <= sl[j]) push(i + 1, sk[j], sl[j], srk[j], emm, ego + 1, ege, ST_D, 1);
-                    }
-                } else if (est == ST_I) {
-                    if (ege < R.max_gape) push(i, ek, el, erk, emm, ego, ege + 1, ST_I, 1);
-                } else if (est == ST_D) {
-                    if (ege < R.max_gape && (ege + ego < max_diff || occ < (uint32_t)R.max_del_occ)) {
-                        for (int j = 0; j < 4; ++j)
-                            if (sk[j] <= sl[j]) push(i + 1, sk[j], sl[j], srk[j], emm, ego, ege + 1, ST_D, 1);
+            // pushes (bwtgap.c:267-325): all but the last go to the pool at once;
+            // the last stays pending and becomes the virtual top if it is the next pop
+            int pend = 0, pend_b = 0;
+            uint4 pendv = make_uint4(0, 0, 0, 0);
+            auto push = [&](int pi, uint32_t k, uint32_t l, uint32_t rk, int mm, int go, int ge, int st, int isd) {
+                if (pend) flush(pendv, pend_b);
+                pendv = make_uint4(k, l, rk, meta_pack((uint32_t)pi, (uint32_t)st, (uint32_t)isd, (uint32_t)mm,
+                                                       (uint32_t)go, (uint32_t)ge));
+                const int sc = SCORE(mm, go, ge);
+                pend_b = (uint32_t)sc < MAXB ? (int)s_lds[C_REG(ctl) * MAXB + sc] : 0xFF;
+                pend = 1;
+                ++n_entries;
+            };
+            const int tmp = (R_MODE & MODE_LOGGAP) ? int_log2((uint32_t)(ege + ego)) / 2 + 1 : ego + ege;
+            if (allow_diff && (R_MAXGO > 0 || ego > 0)) {
+                const int ies = RG(indel_end_skip);
+                if (i >= ies + tmp && len - i >= ies + tmp) {
+                    if (est == ST_M) {
+                        if (ego < R_MAXGO) {
+                            push(i, ek, el, erk, emm, ego + 1, ege, ST_I, 1);
+                            for (int j = 0; j < 4; ++j)
+                                if (sk[j] <= sl[j]) push(i + 1, sk[j], sl[j], srk[j], emm, ego + 1, ege, ST_D, 1);
+                        }
+                    } else if (est == ST_I) {
+                        if (ege < R_MAXGE) push(i, ek, el, erk, emm, ego, ege + 1, ST_I, 1);
+                    } else if (est == ST_D) {
+                        if (ege < R_MAXGE && (ege + ego < max_diff || occ < (uint32_t)RG(max_del_occ))) {
+                            for (int j = 0; j < 4; ++j)
+                                if (sk[j] <= sl[j]) push(i + 1, sk[j], sl[j], srk[j], emm, ego, ege + 1, ST_D, 1);
+                        }
                     }
                 }
             }
@@ -412,16 +531,11 @@ __global__ void __launch_bounds__(BLOCK) k_search(SearchArgs a)
                 const int c = (int)sc;
                 if (sk[c] <= sl[c]) push(i, sk[c], sl[c], srk[c], emm, ego, ege, ST_M, 0);
             }
-            // the last child: next pop if no memory bucket is lower (virtual top)
             if (pend) {
-                int low = 1 << 30;
-                if (mask0) low = __ffsll((unsigned long long)mask0) - 1;
-                else if (mask1) low = 64 + __ffsll((unsigned long long)mask1) - 1;
-                if (pend_score <= low) { vt = pendv; has_vt = 1; }
-                else flush(pendv, pend_score);
-                pend = 0;
+                if (pend_b <= mask.lowest()) { vt = pendv; ctl |= 1u << 6; }
+                else flush(pendv, pend_b);
             }
-            ph = PH_POP;
+            SET_PH(ctl, PH_POP);
         }
     }
 
@@ -430,6 +544,22 @@ __global__ void __launch_bounds__(BLOCK) k_search(SearchArgs a)
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);
 #undef HEAD
+#undef WB
+#undef WS
+#undef WG
+#undef POOL
+#undef NXT
+#undef HB
+#undef RG
+#undef S_MM
+#undef S_GO
+#undef S_GE
+#undef R_MODE
+#undef R_MAXGO
+#undef R_MAXGE
+#undef SCORE
+#undef WPOS
+#undef WBID
 }
 
 // ---------------------------------------------------------------- host side
@@ -438,24 +568,50 @@ static int check_regimes(const hsa_regime_t *rg, int n)
     for (int r = 0; r < n; ++r) {
         const hsa_regime_t &R = rg[r];
         if (R.s_mm < 0 || R.s_gapo < 0 || R.s_gape < 0) { hsa_set_error("negative penalty"); return HSA_E_ARG; }
-        if (R.n_stacks <= 0 || R.n_stacks > 128) { hsa_set_error("n_stacks %d outside 1..128", R.n_stacks); return HSA_E_ARG; }
+        if (R.n_stacks <= 0 || R.n_stacks > MAXB) { hsa_set_error("n_stacks %d outside 1..%d", R.n_stacks, MAXB); return HSA_E_ARG; }
         if (R.max_gapo > 14 || R.max_gape > 254) { hsa_set_error("max_gapo/max_gape out of range"); return HSA_E_ARG; }
+        if (R.max_diff < -1 || R.max_diff > 125) { hsa_set_error("max_diff out of range"); return HSA_E_ARG; }
     }
     return 0;
 }
 
+// Dense bucket numbering of the scores a search of this regime can push
+// (bwtgap.c:46-75): n_mm <= max_diff+1, n_gapo <= min(max_gapo, max_diff), n_gape > 0
+// only after a gap open.  Returns the bucket count.
+static int bucket_map(const hsa_regime_t &R, uint8_t map[MAXB])
+{
+    bool used[MAXB] = {false};
+    const int md = R.max_diff < 0 ? 0 : R.max_diff;
+    const int go_max = R.max_gapo < md ? R.max_gapo : md;
+    for (int mm = 0; mm <= md + 1; ++mm)
+        for (int go = 0; go <= go_max; ++go)
+            for (int ge = 0; ge <= (go > 0 ? R.max_gape : 0); ++ge) {
+                const int s = mm * R.s_mm + go * R.s_gapo + ge * R.s_gape;
+                if (s >= 0 && s < MAXB && s < R.n_stacks) used[s] = true;
+            }
+    int k = 0;
+    for (int s = 0; s < MAXB; ++s) map[s] = used[s] ? (uint8_t)k++ : (uint8_t)0xFF;
+    return k;
+}
+
 struct LaunchPlan {
     size_t lanes, blocks;
-    uint32_t wcap, seed_base, pcap, hcap, nb;
+    uint32_t wcap, pcap, hcap, nb;
+    uint32_t off_heads, off_wb, off_ws;
     size_t lds;
 };
 
 static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int nb, bool big, LaunchPlan &P)
 {
     P.nb = (uint32_t)nb;
-    P.lds = (size_t)nb * BLOCK * sizeof(uint16_t);
+    P.off_heads = 2 * MAXB + 128;   // score tables, then the two regimes
+    P.off_wb = P.off_heads + (uint32_t)nb * BLOCK * 2;
+    P.off_ws = P.off_wb + (uint32_t)(max_len + 1) * BLOCK;
+    P.lds = ((size_t)P.off_ws + (size_t)(max_seed + 1) * BLOCK + 15) / 16 * 16;
+    if (P.lds > 160 * 1024) { hsa_set_error("reads too long for the LDS budget (%zu bytes)", P.lds); return HSA_E_ARG; }
     int per_cu = 0;
-    HSA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_search, BLOCK, P.lds));
+    if (nb <= 64) HSA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_search<1>, BLOCK, P.lds));
+    else HSA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_search<2>, BLOCK, P.lds));
     const int want = g_waves_per_cu / (BLOCK / 64);
     if (per_cu > want) per_cu = want > 0 ? want : 1;
     if (per_cu < 1) { hsa_set_error("search kernel does not fit (LDS %zu)", P.lds); return HSA_E_ARG; }
@@ -469,8 +625,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     if (blocks < 1) blocks = 1;
     P.blocks = blocks;
     P.lanes = blocks * BLOCK;
-    P.seed_base = (uint32_t)max_len + 1;
-    P.wcap = P.seed_base + (uint32_t)max_seed + 1;
+    P.wcap = (uint32_t)max_len + 1;
     P.pcap = big ? 65535u : (uint32_t)g_pool_entries;
     P.hcap = big ? 16384u : (uint32_t)g_hit_cap;
     return 0;
@@ -478,24 +633,26 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
 
 // Launch one search pass over jobs (or job_list subset) with device pointers.
 static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
-                       const hsa_job_t *d_jobs, const int32_t *d_list, int n, const uint8_t *d_codes,
-                       int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho, uint32_t *d_hits, uint64_t hit_cap,
-                       unsigned long long *d_ctr, hipStream_t st)
+                       const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n,
+                       const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho, uint32_t *d_hits,
+                       uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st)
 {
-    int rc = hsa_scratch_reserve(S, P.lanes, P.wcap, P.pcap, P.hcap);
+    // width scratch is reserved in uint2 units; wg uses it as u32 (2 per unit)
+    int rc = hsa_scratch_reserve(S, P.lanes, (P.wcap + 1) / 2, P.pcap, P.hcap);
     if (rc) return rc;
     SearchArgs A;
     A.fwd = RankDir{ix->blk[0], ix->isa0};
     A.rev = RankDir{ix->blk[1], ix->risa0};
     A.T = ix->T;
     memcpy(A.C, ix->C, sizeof A.C);
-    A.regimes = d_regimes; A.jobs = d_jobs; A.job_list = d_list; A.n_jobs = n; A.codes = d_codes;
+    A.regimes = d_regimes; A.bmap = d_bmap; A.jobs = d_jobs; A.job_list = d_list; A.n_jobs = n; A.codes = d_codes;
     A.n_aln = d_n; A.flags = d_fl; A.hit_off = d_ho; A.hits = d_hits; A.hit_cap = hit_cap; A.ctr = d_ctr;
-    A.width = S.width; A.pool = S.pool; A.nxt = S.nxt; A.hbuf = S.hbuf;
-    A.wcap = (uint32_t)S.wcap; A.seed_base = P.seed_base; A.pcap = (uint32_t)S.pcap; A.hcap = (uint32_t)S.hcap;
-    A.nb = P.nb;
+    A.wg = reinterpret_cast<uint32_t *>(S.width); A.pool = S.pool; A.nxt = S.nxt; A.hbuf = S.hbuf;
+    A.wcap = (uint32_t)S.wcap * 2; A.pcap = (uint32_t)S.pcap; A.hcap = (uint32_t)S.hcap;
+    A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
     HSA_HIP(hipMemsetAsync(d_ctr, 0, 8 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_search, dim3((unsigned)P.blocks), dim3(BLOCK), P.lds, st, A);
+    if (P.nb <= 64) hipLaunchKernelGGL(k_search<1>, dim3((unsigned)P.blocks), dim3(BLOCK), P.lds, st, A);
+    else hipLaunchKernelGGL(k_search<2>, dim3((unsigned)P.blocks), dim3(BLOCK), P.lds, st, A);
     HSA_HIP(hipGetLastError());
     return 0;
 }
@@ -512,6 +669,21 @@ static int jobs_limits(const hsa_job_t *jobs, int n, int &max_len, int &max_seed
     return 0;
 }
 
+// regimes + bucket maps into the staging area: [regimes (256 B)][bmap 2*MAXB]
+static int stage_regimes(const hsa_regime_t *regimes, int n_regimes, char *dst, int &nb, hipStream_t st)
+{
+    static thread_local uint8_t host[256 + 2 * MAXB];
+    memset(host, 0xFF, sizeof host);
+    memcpy(host, regimes, sizeof(hsa_regime_t) * n_regimes);
+    nb = 1;
+    for (int r = 0; r < n_regimes; ++r) {
+        int k = bucket_map(regimes[r], host + 256 + r * MAXB);
+        nb = k > nb ? k : nb;
+    }
+    HSA_HIP(hipMemcpyAsync(dst, host, sizeof host, hipMemcpyHostToDevice, st));
+    return 0;
+}
+
 extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs,
                                  int n_jobs, const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
                                  uint64_t *hit_off, uint32_t **hits_out, hsa_stats_t *stats)
@@ -522,19 +694,21 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
     if (rc) return rc;
     int max_len, max_seed;
     if ((rc = jobs_limits(jobs, n_jobs, max_len, max_seed))) return rc;
-    int nb = 0;
-    for (int r = 0; r < n_regimes; ++r) nb = regimes[r].n_stacks > nb ? regimes[r].n_stacks : nb;
+    if (codes_len >= 0xFFFFFFFFull) { hsa_set_error("read codes of one call must be < 4 GiB"); return HSA_E_ARG; }
     HSA_HIP(hipSetDevice(ix->device));
     hipStream_t st = ix->stream;
     if (stats) memset(stats, 0, sizeof *stats);
     if (n_jobs == 0) { *hits_out = (uint32_t *)calloc(9, 4); return 0; }
 
-    // device staging: regimes | jobs | list | codes
-    const size_t o_reg = 0, o_jobs = 256, o_list = o_jobs + ((size_t)n_jobs * sizeof(hsa_job_t) + 255) / 256 * 256;
+    // device staging: regimes+bmap | jobs | list | codes
+    const size_t o_reg = 0, o_jobs = 1024, o_list = o_jobs + ((size_t)n_jobs * sizeof(hsa_job_t) + 255) / 256 * 256;
     const size_t o_codes = o_list + ((size_t)n_jobs * 4 + 255) / 256 * 256;
     if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, o_codes + codes_len + 256))) return rc;
     char *din = (char *)ix->d_in;
-    HSA_HIP(hipMemcpyAsync(din + o_reg, regimes, sizeof(hsa_regime_t) * n_regimes, hipMemcpyHostToDevice, st));
+    int nb = 0;
+    if ((rc = stage_regimes(regimes, n_regimes, din + o_reg, nb, st))) return rc;
+    const hsa_regime_t *d_reg = (const hsa_regime_t *)(din + o_reg);
+    const uint8_t *d_bmap = (const uint8_t *)(din + o_reg + 256);
     HSA_HIP(hipMemcpyAsync(din + o_jobs, jobs, sizeof(hsa_job_t) * n_jobs, hipMemcpyHostToDevice, st));
     HSA_HIP(hipMemcpyAsync(din + o_codes, codes, codes_len, hipMemcpyHostToDevice, st));
     // outputs: n_aln | flags | hit_off | hits
@@ -553,8 +727,8 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
     LaunchPlan P;
     if ((rc = plan_launch(ix, n_jobs, max_len, max_seed, nb, false, P))) return rc;
     HSA_HIP(hipEventRecord(ix->ev0, st));
-    if ((rc = launch_pass(ix, P, ix->main, (const hsa_regime_t *)(din + o_reg), (const hsa_job_t *)(din + o_jobs),
-                          nullptr, n_jobs, (const uint8_t *)(din + o_codes), d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, st)))
+    if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs), nullptr, n_jobs,
+                          (const uint8_t *)(din + o_codes), d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, st)))
         return rc;
     HSA_HIP(hipEventRecord(ix->ev1, st));
     unsigned long long ctr[8];
@@ -563,6 +737,7 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
     HSA_HIP(hipMemcpyAsync(flags, d_fl, (size_t)n_jobs * 4, hipMemcpyDeviceToHost, st));
     HSA_HIP(hipMemcpyAsync(hit_off, d_ho, (size_t)n_jobs * 8, hipMemcpyDeviceToHost, st));
     HSA_HIP(hipStreamSynchronize(st));
+    if (ctr[5]) { hsa_set_error("%llu reads exceed the regime's max_diff bound", ctr[5]); return HSA_E_ARG; }
     float ms = 0;
     HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
     uint64_t total = ctr[1] < hit_cap ? ctr[1] : hit_cap;
@@ -590,7 +765,7 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
         HSA_HIP(hipMemcpyAsync(din + o_list, list, sizeof(int32_t) * n_over, hipMemcpyHostToDevice, st));
         char *c2 = (char *)d2;
         HSA_HIP(hipEventRecord(ix->ev0, st));
-        if ((rc = launch_pass(ix, B, ix->big, (const hsa_regime_t *)(din + o_reg), (const hsa_job_t *)(din + o_jobs),
+        if ((rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs),
                               (const int32_t *)(din + o_list), n_over, (const uint8_t *)(din + o_codes), (int32_t *)c2,
                               (uint32_t *)(c2 + o2_fl), (uint64_t *)(c2 + o2_ho), (uint32_t *)(c2 + o2_hits), cap2,
                               d_ctr, st))) {
@@ -630,18 +805,22 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
 extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes,
                                  const hsa_device_batch_t *b, void *stream)
 {
-    // regimes: host array; copied into the index's staging area
+    // regimes: host array; staged into the index's staging area
+    if (n_regimes < 1 || n_regimes > 2) { hsa_set_error("1 or 2 regimes"); return HSA_E_ARG; }
     int rc = check_regimes(regimes, n_regimes);
     if (rc) return rc;
+    if (b->max_len < 1 || b->max_len > 1023 || b->max_seed < 0 || b->max_seed > 1023) {
+        hsa_set_error("max_len/max_seed out of range");
+        return HSA_E_ARG;
+    }
     HSA_HIP(hipSetDevice(ix->device));
     hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
     if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1024))) return rc;
-    HSA_HIP(hipMemcpyAsync(ix->d_in, regimes, sizeof(hsa_regime_t) * n_regimes, hipMemcpyHostToDevice, st));
     int nb = 0;
-    for (int r = 0; r < n_regimes; ++r) nb = regimes[r].n_stacks > nb ? regimes[r].n_stacks : nb;
+    if ((rc = stage_regimes(regimes, n_regimes, (char *)ix->d_in, nb, st))) return rc;
     LaunchPlan P;
-    if ((rc = plan_launch(ix, b->n_jobs, 1023, 1023, nb, false, P))) return rc;
-    return launch_pass(ix, P, ix->main, (const hsa_regime_t *)ix->d_in, b->d_jobs, nullptr, b->n_jobs, b->d_codes,
-                       b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap,
+    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, false, P))) return rc;
+    return launch_pass(ix, P, ix->main, (const hsa_regime_t *)ix->d_in, (const uint8_t *)ix->d_in + 256, b->d_jobs,
+                       nullptr, b->n_jobs, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap,
                        (unsigned long long *)b->d_counters, st);
 }

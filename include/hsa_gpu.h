@@ -43,6 +43,7 @@ typedef struct {
     int32_t max_gapo, max_gape;
     int32_t max_seed_diff, max_top2;
     int32_t n_stacks;             /* aln_score(max_diff+1, max_gapo+1, max_gape+1) of the batch's local_opt */
+    int32_t max_diff;             /* upper bound of the per-read max_diff of this regime's reads */
 } hsa_regime_t;
 
 /* One read to search.  `off` indexes the codes buffer given to hsa_search_batch. */
@@ -113,6 +114,7 @@ typedef struct {
     int32_t *d_n_aln; uint32_t *d_flags; uint64_t *d_hit_off;
     uint32_t *d_hits; uint64_t hit_cap;
     uint64_t *d_counters;         /* >= 8 u64 of device scratch, zeroed by the call */
+    int32_t max_len, max_seed;    /* longest read, longest seed among the jobs */
 } hsa_device_batch_t;
 int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes,
                       const hsa_device_batch_t *b, void *stream);
