@@ -39,6 +39,8 @@ struct hsa_index {
     void *d_in = nullptr; size_t d_in_cap = 0;
     void *d_out = nullptr; size_t d_out_cap = 0;
     uint64_t *d_ctr = nullptr;
+    unsigned char staged[512];          // last regime block copied to d_in (skip identical re-copies)
+    int staged_valid = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
 
