@@ -84,6 +84,28 @@ def host_oracle_index(res, T):
     return OracleIndex(metas[0], metas[1])
 
 
+def diag_dump(path):
+    """Diagnostic builds only (libhsa_gpu_diag.so): per-workgroup clock stamps of
+    the last launch -> in-kernel clock and workgroup-duration spread."""
+    from hsa_amd import _lib
+    L = _lib.lib()
+    nb = 8192
+    buf = np.zeros(nb * 4, np.uint64)
+    _lib.check(L.hsa_diag_read(buf.ctypes.data_as(C.c_void_p), nb))
+    d = buf.reshape(nb, 4).astype(np.int64)
+    d = d[d[:, 3] > 0]
+    t0 = d[:, 1].min()
+    dur_ms = (d[:, 3] - d[:, 1]) / 100e3          # s_memrealtime: 100 MHz
+    clk = (d[:, 2] - d[:, 0]) / np.maximum(d[:, 3] - d[:, 1], 1) * 100.0
+    out = {"blocks": int(len(d)), "clock_mhz_median": float(np.median(clk)),
+           "start_spread_ms": float((d[:, 1].max() - t0) / 100e3),
+           "dur_ms_pct": [float(np.percentile(dur_ms, q)) for q in (0, 10, 50, 90, 99, 100)],
+           "end_ms_pct": [float(np.percentile((d[:, 3] - t0) / 100e3, q)) for q in (0, 10, 50, 90, 99, 100)]}
+    log(f"[bench] diag: {json.dumps(out)}")
+    with open(path, "w") as f:
+        json.dump(out, f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -180,6 +202,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kms = [e0.elapsed_time(e1) for e0, e1 in ev]
+    if os.environ.get("HSA_DIAG_OUT"):
+        diag_dump(os.environ["HSA_DIAG_OUT"])
     log(f"[bench] rank {rank}: per-step device ms {[round(x, 2) for x in kms]}, wall {elapsed * 1e3:.1f} ms")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")

@@ -11,7 +11,8 @@ import os as _os
 from . import index_io, synth  # noqa: F401
 
 # Load the HIP library before anything imports torch (see _lib._check_runtime).
-if _os.path.exists(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "libhsa_gpu.so")):
+if _os.path.exists(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)),
+                                 _os.environ.get("HSA_GPU_LIB", "libhsa_gpu.so"))):
     from . import _lib as _l
     _l.lib()
 

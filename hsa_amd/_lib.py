@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhsa_gpu.so")
+# HSA_GPU_LIB selects another in-tree build of the same library (A/B experiments).
+LIB_PATH = os.path.join(HERE, os.environ.get("HSA_GPU_LIB", "libhsa_gpu.so"))
 
 HSA_F_FALLBACK = 1
 HSA_F_OVERFLOW = 2

@@ -100,6 +100,13 @@ __device__ __forceinline__ uint32_t meta_pack(uint32_t i, uint32_t st, uint32_t 
 #define C_SLEN(c) ((int)(((c) >> 20) & 1023u))
 #define SET_PH(c, p) ((c) = ((c) & ~7u) | (p))
 
+// v[c] for a runtime c in 0..3 as selects: a dynamically indexed register array
+// would be lowered through the private segment (scratch) of the dispatch.
+__device__ __forceinline__ uint32_t pick4(const uint32_t v[4], uint32_t c)
+{
+    return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3];
+}
+
 __device__ __forceinline__ int int_log2(uint32_t v)   // bwtgap.c:107-116
 {
     int c = 0;
@@ -136,9 +143,22 @@ template <> struct BMask<2> {
     __device__ __forceinline__ void reset(int b) { if (b < 64) m0 &= ~(1ull << b); else m1 &= ~(1ull << (b - 64)); }
 };
 
+#ifdef HSA_DIAG
+// Diagnostic build only (-DHSA_DIAG, never the product library): per-workgroup
+// start/end s_memtime and s_memrealtime of the last launch, for the in-kernel
+// clock and the workgroup-duration spread.
+__device__ unsigned long long g_diag[8192 * 4];
+#endif
+
 template <int MW>
 __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 {
+#ifdef HSA_DIAG
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {
+        g_diag[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime();
+        g_diag[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     extern __shared__ __align__(16) uint8_t s_lds[];
     const uint32_t tid = threadIdx.x;
     const uint32_t gid = blockIdx.x * BLOCK + tid;
@@ -152,10 +172,14 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
     uint16_t *const s_heads = reinterpret_cast<uint16_t *>(s_lds + a.off_heads);
     uint8_t *const s_wb = s_lds + a.off_wb;
     uint8_t *const s_ws = s_lds + a.off_ws;
-#define WG(p) a.wg[(size_t)gid * a.wcap + (uint32_t)(p)]
-#define POOL(s) a.pool[(size_t)gid * a.pcap + (uint32_t)(s)]
-#define NXT(s) a.nxt[(size_t)gid * a.pcap + (uint32_t)(s)]
-#define HB(i) a.hbuf[(size_t)gid * a.hcap * 9 + (uint32_t)(i)]
+    // per-lane HBM scratch, wave-interleaved: element e of lane l of wave w at
+    // (w * cap + e) * 64 + l, so one wave's accesses stay inside one small region
+    // (few pages) and lanes at equal e coalesce
+    const size_t wv = gid >> 6;
+#define WG(p) a.wg[(wv * a.wcap + (uint32_t)(p)) * 64 + lane]
+#define POOL(s) a.pool[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
+#define NXT(s) a.nxt[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
+#define HB(i) a.hbuf[(wv * a.hcap * 9 + (uint32_t)(i)) * 64 + lane]
 #define HEAD(b) s_heads[(uint32_t)(b) * BLOCK + tid]
 #define WB(p) s_wb[(uint32_t)(p) * BLOCK + tid]
 #define WS(p) s_ws[(uint32_t)(p) * BLOCK + tid]
@@ -430,17 +454,20 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         const uint32_t ph = C_PH(ctl);
         if (req && ph == PH_WIDTH) {
             const uint32_t c = getc(wstart() + WPOS);
-            ik = a.C[c] + oa[c] + 1u;
-            il = a.C[c] + ob[c];
+            const uint32_t cc = pick4(a.C, c);
+            ik = cc + pick4(oa, c) + 1u;
+            il = cc + pick4(ob, c);
             if (ik > il) { ik = 0; il = a.T; pos += 1u << 11; }
             put_width(il - ik + 1u);
         } else if (req && ph == PH_EXACT) {
             // BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170), one character
             const uint32_t c = getc((int)pos);
             uint32_t oc = 0;
-            for (uint32_t d = c + 1; d < 4; ++d) oc += ob[d] - oa[d];
-            ik = a.C[c] + oa[c] + 1u;
-            il = a.C[c] + ob[c];
+#pragma unroll
+            for (uint32_t d = 1; d < 4; ++d) oc += d > c ? ob[d] - oa[d] : 0u;
+            const uint32_t cc = pick4(a.C, c);
+            ik = cc + pick4(oa, c) + 1u;
+            il = cc + pick4(ob, c);
             aux -= oc;                                                   // rev_l
             if (ik > il) {
                 SET_PH(ctl, PH_POP);                                     // no match: continue (bwtgap.c:185)
@@ -462,6 +489,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             uint32_t sk[4], sl[4], srk[4];
             {
                 uint32_t oc = 0;
+#pragma unroll
                 for (int c = 3; c >= 0; --c) {
                     sk[c] = a.C[c] + oa[c] + 1u;
                     sl[c] = a.C[c] + ob[c];
@@ -507,6 +535,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                     if (est == ST_M) {
                         if (ego < R_MAXGO) {
                             push(i, ek, el, erk, emm, ego + 1, ege, ST_I, 1);
+#pragma unroll
                             for (int j = 0; j < 4; ++j)
                                 if (sk[j] <= sl[j]) push(i + 1, sk[j], sl[j], srk[j], emm, ego + 1, ege, ST_D, 1);
                         }
@@ -514,6 +543,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                         if (ege < R_MAXGE) push(i, ek, el, erk, emm, ego, ege + 1, ST_I, 1);
                     } else if (est == ST_D) {
                         if (ege < R_MAXGE && (ege + ego < max_diff || occ < (uint32_t)RG(max_del_occ))) {
+#pragma unroll
                             for (int j = 0; j < 4; ++j)
                                 if (sk[j] <= sl[j]) push(i + 1, sk[j], sl[j], srk[j], emm, ego, ege + 1, ST_D, 1);
                         }
@@ -522,14 +552,16 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             }
             const uint32_t sc = getc(i);
             if (allow_diff && allow_M) {
+#pragma unroll
                 for (int j = 1; j <= 4; ++j) {
-                    const int c = (int)((sc + (uint32_t)j) & 3u);
+                    const uint32_t c = (sc + (uint32_t)j) & 3u;
                     const int is_mm = (j != 4 || sc > 3);
-                    if (sk[c] <= sl[c]) push(i, sk[c], sl[c], srk[c], emm + is_mm, ego, ege, ST_M, is_mm);
+                    const uint32_t ck = pick4(sk, c), cl = pick4(sl, c);
+                    if (ck <= cl) push(i, ck, cl, pick4(srk, c), emm + is_mm, ego, ege, ST_M, is_mm);
                 }
             } else if (sc < 4) {
-                const int c = (int)sc;
-                if (sk[c] <= sl[c]) push(i, sk[c], sl[c], srk[c], emm, ego, ege, ST_M, 0);
+                const uint32_t ck = pick4(sk, sc), cl = pick4(sl, sc);
+                if (ck <= cl) push(i, ck, cl, pick4(srk, sc), emm, ego, ege, ST_M, 0);
             }
             if (pend) {
                 if (pend_b <= mask.lowest()) { vt = pendv; ctl |= 1u << 6; }
@@ -539,6 +571,13 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         }
     }
 
+#ifdef HSA_DIAG
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {
+        g_diag[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memtime();
+        g_diag[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     // statistics
     atomicAdd(&a.ctr[2], (unsigned long long)st_q);
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
@@ -563,6 +602,13 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 }
 
 // ---------------------------------------------------------------- host side
+#ifdef HSA_DIAG
+extern "C" int hsa_diag_read(unsigned long long *out, int n_blocks)
+{
+    HSA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 4 * (size_t)n_blocks));
+    return 0;
+}
+#endif
 static int check_regimes(const hsa_regime_t *rg, int n)
 {
     for (int r = 0; r < n; ++r) {
@@ -609,9 +655,13 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     P.off_ws = P.off_wb + (uint32_t)(max_len + 1) * BLOCK;
     P.lds = ((size_t)P.off_ws + (size_t)(max_seed + 1) * BLOCK + 15) / 16 * 16;
     if (P.lds > 160 * 1024) { hsa_set_error("reads too long for the LDS budget (%zu bytes)", P.lds); return HSA_E_ARG; }
-    int per_cu = 0;
-    if (nb <= 64) HSA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_search<1>, BLOCK, P.lds));
-    else HSA_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_search<2>, BLOCK, P.lds));
+    // Resident workgroups per CU, from gfx950's own limits: 160 KiB of LDS per CU,
+    // and __launch_bounds__(BLOCK, 4) caps VGPRs so 4 workgroups of 4 waves fit.
+    // (hipOccupancyMaxActiveBlocksPerMultiprocessor is not used: depending on which
+    // HIP runtime the process loaded first it assumed 64 KiB of LDS and halved the
+    // grid -- measured 512 instead of 1024 workgroups, 1.5x slower.)
+    int per_cu = (int)((160u * 1024u) / P.lds);
+    if (per_cu > 4) per_cu = 4;
     const int want = g_waves_per_cu / (BLOCK / 64);
     if (per_cu > want) per_cu = want > 0 ? want : 1;
     if (per_cu < 1) { hsa_set_error("search kernel does not fit (LDS %zu)", P.lds); return HSA_E_ARG; }
@@ -625,6 +675,14 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     if (blocks < 1) blocks = 1;
     P.blocks = blocks;
     P.lanes = blocks * BLOCK;
+    static int verbose = -1;
+    if (verbose < 0) verbose = getenv("HSA_VERBOSE") != nullptr;
+    if (verbose) {
+        int occ = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_search<1>, BLOCK, P.lds);
+        fprintf(stderr, "[hsa] launch: %d CUs x %d workgroups (runtime occupancy query says %d), LDS %zu B, "
+                "%zu workgroups, %d buckets\n", ix->n_cu, per_cu, occ, P.lds, blocks, nb);
+    }
     P.wcap = (uint32_t)max_len + 1;
     P.pcap = big ? 65535u : (uint32_t)g_pool_entries;
     P.hcap = big ? 16384u : (uint32_t)g_hit_cap;
