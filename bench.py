@@ -84,6 +84,21 @@ def host_oracle_index(res, T):
     return OracleIndex(metas[0], metas[1])
 
 
+TRAFFIC_SRC = "profiles/r01_pmc_summary.json"
+
+
+def traffic_per_launch():
+    """HBM read+write bytes per k_search launch from the committed PMC pass
+    (FETCH_SIZE calibrated on random 64-B gathers + WRITE_SIZE; tools/profile_run.sh,
+    tools/pmc_summary.py) -- counters cannot be read in the timed run itself."""
+    try:
+        with open(os.path.join(ROOT, TRAFFIC_SRC)) as f:
+            d = json.load(f)
+        return round(d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def diag_dump(path):
     """Diagnostic builds only (libhsa_gpu_diag.so): per-workgroup clock stamps of
     the last launch -> in-kernel clock and workgroup-duration spread."""
@@ -184,6 +199,11 @@ def main():
                         max_len=READ_LEN, max_seed=opt.seed_len)
         gi.search_device([rg], b)
 
+    # the measured ceiling for this access pattern: random whole 64-B blocks over a
+    # table as large as the rank index (before the timed region, same process)
+    rand_gbs = _lib.probe_gather64(gi.nbytes(), device)
+    log(f"[bench] rank {rank}: random 64-B gather probe over {gi.nbytes() / 2**30:.2f} GiB: {rand_gbs:.0f} GB/s")
+
     lib_stream = torch.cuda.ExternalStream(gi.stream_handle())
     for j in range(a.warmup):
         launch(j)
@@ -262,11 +282,15 @@ def main():
                        "genome_bp": T, "reads_per_step": a.batch, "read_len": READ_LEN, "options": "-n 4 -o 0",
                        "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_per_launch(),
                          "kernel": "k_search", "kernel_ms_mean": round(mean_kms, 3),
+                         "algorithmic_bytes_per_launch": q_per_launch * BYTES_PER_QUERY,
                          "rank_queries_per_read": round(queries / reads_local, 1),
                          "blocks_per_query": round(blocks / max(queries, 1), 4),
-                         "bytes_per_query": BYTES_PER_QUERY},
+                         "bytes_per_query": BYTES_PER_QUERY,
+                         "peak_random64_measured": round(rand_gbs, 1),
+                         "frac_of_random64": round(achieved / rand_gbs, 4),
+                         "traffic_source": TRAFFIC_SRC},
             "mapped_frac": round(mapped_all / reads_all, 4), "fallback_frac": round(fallback_all / reads_all, 4),
             "pops_per_read": round(pops / reads_local, 1),
         }

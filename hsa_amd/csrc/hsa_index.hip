@@ -415,3 +415,66 @@ extern "C" int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, ui
     HSA_HIP(hipDeviceSynchronize());
     return 0;
 }
+
+// ---------------------------------------------------------------- roofline probe
+// Random 64-byte block gather over a table as large as the rank index (the access
+// pattern of every rank query): each lane loads one whole uniformly random 64-B
+// block per iteration, 16 waves per CU.  Gives the measured ceiling the search
+// kernel's achieved bandwidth is compared with (tools/membench.hip is
+// the stand-alone version with more modes).
+__global__ void __launch_bounds__(256) k_gather64(const uint4 *__restrict__ buf, uint64_t nblk, int iters,
+                                                 uint32_t *out)
+{
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t acc = 0;
+    uint64_t s = splitmix64(gid + 1);
+    for (int it = 0; it < iters; ++it) {
+        s = splitmix64(s);
+        const uint4 *p = buf + (s % nblk) * 4;
+        const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+        acc += a.x ^ b.y ^ c.z ^ d.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;   // keeps the loads live; never true in practice
+}
+
+__global__ void k_fill_words(uint32_t *buf, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        buf[i] = (uint32_t)splitmix64(i);
+}
+
+extern "C" int hsa_probe_gather64(int device, uint64_t table_bytes, double *gbps)
+{
+    HSA_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HSA_HIP(hipGetDeviceProperties(&prop, device));
+    table_bytes &= ~(uint64_t)63;
+    if (table_bytes < (1u << 20)) { hsa_set_error("probe table too small"); return HSA_E_ARG; }
+    uint4 *buf = nullptr;
+    uint32_t *out = nullptr;
+    if (hipMalloc(&buf, table_bytes) != hipSuccess) { hsa_set_error("probe: hipMalloc failed"); return HSA_E_MEM; }
+    if (hipMalloc(&out, 64) != hipSuccess) { (void)hipFree(buf); hsa_set_error("probe: hipMalloc failed"); return HSA_E_MEM; }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = 0;
+    float ms = 0;
+    const uint64_t nblk = table_bytes / 64;
+    const unsigned blocks = (unsigned)prop.multiProcessorCount * 4;   // 16 waves per CU
+    const int iters = 1000;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { rc = HSA_E_HIP; goto done; }
+    k_fill_words<<<4096, 256>>>((uint32_t *)buf, table_bytes / 4);
+    k_gather64<<<blocks, 256>>>(buf, nblk, iters / 4, out);           // warm-up
+    (void)hipEventRecord(e0, 0);
+    k_gather64<<<blocks, 256>>>(buf, nblk, iters, out);
+    (void)hipEventRecord(e1, 0);
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+        hsa_set_error("probe: kernel failed");
+        rc = HSA_E_HIP;
+        goto done;
+    }
+    *gbps = (double)blocks * 256 * iters * 64 / (ms * 1e-3) / 1e9;
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(buf); (void)hipFree(out);
+    return rc;
+}

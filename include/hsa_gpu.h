@@ -126,6 +126,12 @@ void hsa_free(void *p);
 /* Synthetic workload helpers (bench data generation on the device). */
 int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, uint32_t *d_code_lsb);
 
+/* Roofline probe: measured bandwidth (GB/s) of uniformly random whole 64-byte
+ * block loads over a table of `table_bytes` -- the access pattern of a rank query --
+ * with all CUs at 16 waves each.  The denominator the search kernel's achieved
+ * bandwidth is compared with next to the 8 TB/s spec peak. */
+int hsa_probe_gather64(int device, uint64_t table_bytes, double *gbps);
+
 /* Suffix-array based BWT construction on the device for a text given as LSB-first
  * 2-bit codes (16 per u32).  Produces the $-less BWT codes (LSB-first) and
  * inverseSa0 = rank of suffix 0 among T+1 suffixes incl. '$' (BWT.h:61-83).

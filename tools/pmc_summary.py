@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_run.sh output directory into one JSON (committed
+under profiles/) -- the per-launch HBM traffic of k_search that bench.py reports
+as roofline.traffic, and the SQ/TCC ratios.
+
+FETCH_SIZE is in KiB.  Calibration (MI355X_MICROARCH.md, HBM section: access
+widths other than 16 B/lane streaming are uncalibrated): membench's k_indep
+issues a known number of random 64-byte block loads per dispatch; the ratio
+FETCH_SIZE*1024 / known bytes on that pattern is applied to k_search.
+
+usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>_pmc_summary.json
+"""
+import collections
+import csv
+import json
+import os
+import statistics
+import sys
+
+
+def counters(d, kernel):
+    rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    dur = {}
+    for r in rows:
+        if kernel not in r["Kernel_Name"]:
+            continue
+        agg[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+        dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    return agg, dur
+
+
+def med(agg, name):
+    return statistics.median(v[name] for v in agg.values())
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    out = {"source": src}
+    # calibration on membench k_indep<1>: 1024 workgroups x 256 lanes x 2000 iterations x 64 B
+    mb, _ = counters(os.path.join(src, "pmc_membench"), "k_indep<1>")
+    known = 256 * 16 // 4 * 256 * 2000 * 64
+    cal = med(mb, "FETCH_SIZE") * 1024 / known
+    out["fetch_calibration_random64"] = round(cal, 4)
+    f, dur = counters(os.path.join(src, "pmc_fetch"), "k_search")
+    w, _ = counters(os.path.join(src, "pmc_write"), "k_search")
+    out["fetch_bytes_per_launch"] = med(f, "FETCH_SIZE") * 1024 / cal
+    out["write_bytes_per_launch"] = med(w, "WRITE_SIZE") * 1024
+    out["launch_ms_median_pmc_pass"] = statistics.median(dur.values())
+    sq, _ = counters(os.path.join(src, "pmc_sq"), "k_search")
+    wc = med(sq, "SQ_WAVE_CYCLES")
+    out["sq"] = {"wait_any_frac": med(sq, "SQ_WAIT_ANY") / wc,
+                 "active_inst_any_frac": med(sq, "SQ_ACTIVE_INST_ANY") / wc,
+                 "active_valu_frac": med(sq, "SQ_ACTIVE_INST_VALU") / wc,
+                 "vmem_rd_wave_insts": med(sq, "SQ_INSTS_VMEM_RD"),
+                 "waves": med(sq, "SQ_WAVES"),
+                 "grbm_gui_active_per_xcd": med(sq, "GRBM_GUI_ACTIVE") / 8}
+    tcc, _ = counters(os.path.join(src, "pmc_tcc"), "k_search")
+    h, m = med(tcc, "TCC_HIT_sum"), med(tcc, "TCC_MISS_sum")
+    out["tcc"] = {"hit_rate": h / (h + m), "ea_rdreq": med(tcc, "TCC_EA0_RDREQ_sum")}
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,17 +1,25 @@
 #!/bin/bash
-# Profiling recipe run on the GPU box (see DESIGN.md "Measurement").
-# usage: tools/profile_run.sh <tag>
+# Profiling recipe run on the GPU box (DESIGN.md "Measurement"):
+#   kernel trace + stats, then one PMC pass per counter group (separate runs, no
+#   tracing domains besides --kernel-trace), and a FETCH_SIZE calibration pass on
+#   membench's random 64-byte gather (known byte count).
+# usage: tools/profile_run.sh <tag>      outputs under gpurun_out/prof_<tag>/
 set -o pipefail
 TAG=${1:-r01}
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 5 --warmup 1 --cpu-sample 0 --parity-sample 0"
+BENCH="$R/bench.py --steps 5 --warmup 1 --cpu-sample 0 --parity-sample 0 $BENCH_ARGS"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $BENCH > $OUT/trace.json 2> $OUT/trace.err || exit 11
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex k_search --output-format csv -d $OUT/pmc_fetch -o run -- python3 $BENCH > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err || exit 12
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --kernel-include-regex k_search --output-format csv -d $OUT/pmc_write -o run -- python3 $BENCH > $OUT/pmc_write.json 2> $OUT/pmc_write.err || exit 13
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --kernel-include-regex k_search --output-format csv -d $OUT/pmc_sq -o run -- python3 $BENCH > $OUT/pmc_sq.json 2> $OUT/pmc_sq.err || exit 14
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex k_search --output-format csv -d $OUT/pmc_tcc -o run -- python3 $BENCH > $OUT/pmc_tcc.json 2> $OUT/pmc_tcc.err || exit 15
+pmc() {  # name, counters...
+  local n=$1; shift
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc "$@" --kernel-include-regex k_search --output-format csv -d $OUT/pmc_$n -o run -- python3 $BENCH > $OUT/pmc_$n.json 2> $OUT/pmc_$n.err || exit 12
+}
+pmc fetch FETCH_SIZE
+pmc write WRITE_SIZE
+pmc sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
+pmc tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex k_indep --output-format csv -d $OUT/pmc_membench -o run -- $R/tools/membench 2147483648 16 > $OUT/pmc_membench.log 2>&1 || exit 13
 echo done
