@@ -15,7 +15,7 @@ REFOBJS   = bwtaln bwtgap BWT BWTConstruct utils dictionary DNACount HSP inipars
             bamlite 2BWT-Interface bwaseqio r250 cs2nt bwtse kstring stdaln bwt_array
 OBJS      = $(addprefix $(OUT)/obj/,$(addsuffix .o,$(REFOBJS)))
 
-all: $(OUT)/HSA $(OUT)/ref_probe
+all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/HSA_gpu
 
 $(OUT)/obj/%.o: $(REF)/%.c
 	@mkdir -p $(OUT)/obj
@@ -32,6 +32,22 @@ $(OUT)/HSA: $(OUT)/obj/main.o $(OUT)/libhsaref.a
 $(OUT)/ref_probe: ref_probe.c $(OUT)/libhsaref.a
 	$(CC) $(REFFLAGS) -I$(REF) ref_probe.c $(OUT)/libhsaref.a \
 	    -Wl,--wrap=bwt_splice_match -lm -lz -o $@
+
+# HSA_gpu: the reference's own HSA binary with OUR bwa_cal_sa_reg_gap linked in
+# (INTEGRATION.md).  The reference definition is weakened in a copy of bwtaln.o
+# (verified there), our strong definition comes from bwtaln_gpu.o, and
+# the search core from libhsa_gpu.so.  Only built when the product library exists;
+# the drop-in test (tests/test_gpu_dropin.py) compares its SAM with the reference's.
+GPULIB    = $(CURDIR)/../hsa_amd/libhsa_gpu.so
+GPUOBJ    = $(CURDIR)/../hsa_amd/csrc/bwtaln_gpu.o
+WEAKOBJS  = $(filter-out $(OUT)/obj/bwtaln.o,$(OBJS)) $(OUT)/obj/bwtaln_weak.o
+
+$(OUT)/obj/bwtaln_weak.o: $(OUT)/obj/bwtaln.o
+	objcopy --weaken-symbol=bwa_cal_sa_reg_gap $< $@
+
+$(OUT)/HSA_gpu: $(OUT)/obj/main.o $(WEAKOBJS) $(GPUOBJ) $(GPULIB)
+	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(WEAKOBJS) $(GPUOBJ) -L$(dir $(GPULIB)) -lhsa_gpu \
+	    -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
 
 clean:
 	rm -rf $(OUT)

@@ -1,0 +1,62 @@
+"""Drop-in test: the reference's own `HSA aln` binary with OUR
+bwa_cal_sa_reg_gap linked in place of its definition (oracle/ref.mk target HSA_gpu:
+reference objects, bwtaln.o with the symbol weakened, hsa_amd/csrc/bwtaln_gpu.o,
+libhsa_gpu.so) must print byte-identical SAM to the unmodified reference binary on
+the same FASTQ.  The reference's SAM was recorded in this container by
+tools/make_golden.py --dropin (tests/golden/dropin_ref_*.sam.gz).
+
+This covers the whole boundary at once: FASTQ batches through bwa_aln_core, the
+option-block side effects (Q2/Q3), strand order and start/end (Q4), the filters
+(Q13), the calloc'd hit arrays SAM generation consumes, and the host splice
+fallback (bwt_splice_match) fed with the option state our side reports.
+
+HSA_gpu lives under oracle/_ref (built here from /root/reference, git-ignored, travels
+to the GPU box with the tree); the test skips when it has not been built.
+"""
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+HSA_GPU = os.path.join(ROOT, "oracle", "_ref", "HSA_gpu")
+MAN = json.load(open(os.path.join(GOLD, "manifest_dropin.json")))
+
+needs_bin = pytest.mark.skipif(not os.path.exists(HSA_GPU), reason="oracle/_ref/HSA_gpu not built (make -C oracle)")
+
+
+def run_hsa_gpu(args):
+    idx = os.path.join(GOLD, "index", "tiny.fa")
+    fq = os.path.join(GOLD, MAN["reads"])
+    return subprocess.run([HSA_GPU, "aln", *args, idx, fq], capture_output=True, timeout=120)
+
+
+@needs_bin
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["default", "n4o0"])
+def test_dropin_sam_identical(name):
+    r = run_hsa_gpu(MAN[name]["args"])
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    sam = r.stdout
+    if hashlib.sha256(sam).hexdigest() != MAN[name]["sam_sha256"]:
+        ref = gzip.open(os.path.join(GOLD, f"dropin_ref_{name}.sam.gz")).read().splitlines()
+        got = sam.splitlines()
+        diff = [(i, a, b) for i, (a, b) in enumerate(zip(ref, got)) if a != b][:5]
+        pytest.fail(f"SAM differs: {len(got)} vs {len(ref)} lines; first differences {diff}")
+
+
+@needs_bin
+def test_dropin_fails_loudly_without_gpu():
+    """No CPU fallback: without a visible GPU the drop-in exits 1 with a message
+    (the reference's error convention), it never silently computes on the host."""
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    idx = os.path.join(GOLD, "index", "tiny.fa")
+    fq = os.path.join(GOLD, MAN["reads"])
+    r = subprocess.run([HSA_GPU, "aln", idx, fq], capture_output=True, timeout=120, env=env)
+    assert r.returncode == 1
+    assert b"[bwa_cal_sa_reg_gap]" in r.stderr
+    assert r.stdout == b""

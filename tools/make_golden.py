@@ -7,6 +7,7 @@ Every fixture is data: synthetic inputs plus the reference's outputs on them.
 
     python tools/make_golden.py            # tiny fixtures (committed)
     python tools/make_golden.py --ecoli    # E.coli-sized digests (committed)
+    python tools/make_golden.py --dropin   # FASTQ + reference SAM for the drop-in test
 """
 from __future__ import annotations
 
@@ -270,9 +271,59 @@ def ecoli_cases(work):
         json.dump(man, f, indent=1, sort_keys=True)
 
 
+DROPIN_ARGS = {"default": [], "n4o0": ["-n", "4", "-o", "0"]}
+
+
+def write_fastq_mixed(path, seqs):
+    import gzip
+    with gzip.GzipFile(path, "wb", compresslevel=9, mtime=0) as f:
+        for i, s in enumerate(seqs):
+            f.write(b"@r%d\n" % i)
+            f.write(bytes(b"ACGTN"[min(int(c), 4)] for c in s) + b"\n+\n")
+            f.write(b"I" * len(s) + b"\n")
+
+
+def dropin_cases(work):
+    """Reads + the reference HSA binary's SAM output on the tiny index: the
+    fixture of the drop-in test (our bwa_cal_sa_reg_gap linked into the reference's
+    own HSA, oracle/ref.mk HSA_gpu), which must reproduce it byte for byte."""
+    T, seed = 200003, 7
+    g = synth.genome_codes(T, seed)
+    rec = synth.record_layout(T, 3)
+    seqs = []
+    r, _ = synth.make_reads(g, rec, 500, 100, 31, max_mm=4)
+    seqs += list(r)
+    r, _ = synth.make_reads(g, rec, 400, 100, 32, indel=True, max_mm_indel=2)
+    seqs += list(r)
+    # spliced: 45-60 bp exon + the rest 200-2000 bp downstream (GT..AG not enforced)
+    a, _ = synth.make_reads(g, rec, 150, 60, 33)
+    for i in range(150):
+        st = int(synth._u(34, 1, i)[0] % np.uint64(T - 3000))
+        cut = 45 + i % 16
+        intron = 200 + (i * 37) % 1800
+        seqs.append(np.concatenate([g[st:st + cut], g[st + cut + intron:st + 100 + intron]]).astype(np.uint8))
+    seqs += edge_reads(g, rec, 35)
+    fq = os.path.join(GOLD, "dropin_reads.fq.gz")
+    write_fastq_mixed(fq, seqs)
+    idx = os.path.join(GOLD, "index", "tiny.fa")
+    man = {"reads": os.path.basename(fq), "n": len(seqs), "index": "tiny"}
+    import gzip
+    for name, args in DROPIN_ARGS.items():
+        r = subprocess.run([os.path.join(REF, "HSA"), "aln", *args, idx, fq], check=True, capture_output=True)
+        sam = r.stdout
+        out = os.path.join(GOLD, f"dropin_ref_{name}.sam.gz")
+        with gzip.GzipFile(out, "wb", compresslevel=9, mtime=0) as f:
+            f.write(sam)
+        man[name] = {"args": args, "sam_sha256": hashlib.sha256(sam).hexdigest(), "sam_lines": sam.count(b"\n")}
+        print(name, man[name])
+    with open(os.path.join(GOLD, "manifest_dropin.json"), "w") as f:
+        json.dump(man, f, indent=1, sort_keys=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ecoli", action="store_true")
+    ap.add_argument("--dropin", action="store_true")
     a = ap.parse_args()
     if not os.path.exists(os.path.join(REF, "ref_probe")):
         sys.exit("build oracle/_ref first: make -C oracle -f ref.mk")
@@ -280,6 +331,8 @@ def main():
     with tempfile.TemporaryDirectory() as work:
         if a.ecoli:
             ecoli_cases(work)
+        elif a.dropin:
+            dropin_cases(work)
         else:
             tiny_cases(work)
 
