@@ -246,22 +246,25 @@ def main():
     fallback = int(((flags & 1) != 0).sum())
     reads_local = a.steps * a.batch
 
-    # final hit-list gather to rank 0 (RCCL over xGMI): counts, then the packed records
+    # final hit-list gather to rank 0 (RCCL over xGMI): each rank's last searched
+    # read set, as whole batches (hsa_amd/shard.py), then the counters
     total_hits_local = int(ctr[:, 1].sum())
     if world > 1:
-        cnt = torch.tensor([total_hits_local, mapped, fallback], dtype=torch.int64, device="cuda")
-        allc = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(allc, cnt)
-        last = outs[(a.warmup + a.steps - 1) % nd]
+        from hsa_amd import shard
+        last_j = (a.warmup + a.steps - 1) % nd
+        last = outs[last_j]
         nh_last = int(last["c"][1].item())
-        mx = torch.tensor([nh_last], dtype=torch.int64, device="cuda")
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        buf = torch.zeros(int(mx.item()) * 9, dtype=torch.int32, device="cuda")
-        buf[:nh_last * 9] = last["h"][:nh_last * 9]
-        gathered = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
-        dist.gather(buf, gathered, dst=0)
-        tot = torch.stack(allc).sum(0).tolist()
-        mapped_all, fallback_all = tot[1], tot[2]
+        gidx = (a.warmup + a.steps - 1) * world + rank          # global batch index of that launch
+        res = {gidx: (last["n"].cpu().numpy(), last["f"].cpu().numpy().view(np.uint32), last["o"].cpu().numpy(),
+                      last["h"][:nh_last * 9].cpu().numpy().view(np.uint32).reshape(-1, 9))}
+        t0 = time.perf_counter()
+        g = shard.gather_to_root(res, dist, torch.device("cuda", local))
+        if rank == 0:
+            log(f"[bench] gathered {len(g[0])} reads / {len(g[2])} hits from {world} ranks in "
+                f"{(time.perf_counter() - t0) * 1e3:.1f} ms")
+        cnt = torch.tensor([total_hits_local, mapped, fallback], dtype=torch.int64, device="cuda")
+        dist.all_reduce(cnt)
+        mapped_all, fallback_all = int(cnt[1].item()), int(cnt[2].item())
     else:
         mapped_all, fallback_all = mapped, fallback
 
