@@ -116,6 +116,12 @@ def diag_dump(path):
            "start_spread_ms": float((d[:, 1].max() - t0) / 100e3),
            "dur_ms_pct": [float(np.percentile(dur_ms, q)) for q in (0, 10, 50, 90, 99, 100)],
            "end_ms_pct": [float(np.percentile((d[:, 3] - t0) / 100e3, q)) for q in (0, 10, 50, 90, 99, 100)]}
+    ev = (C.c_ulonglong * 16)()
+    _lib.check(L.hsa_diag_counters(ev, 0))
+    names = ["width_steps", "exact_steps", "expand_steps", "vt_pops", "pool_pops", "outer_iters_per_wave",
+             "lanes_stepping", "control_iters_per_wave", "pool_flushes", "cyc_acquire", "cyc_control",
+             "cyc_rank_wait", "cyc_apply", "gap_shadows", "gap_shadow_ldp_sum", "strand_starts"]
+    out["events_total"] = {n: int(ev[i]) for i, n in enumerate(names)}
     log(f"[bench] diag: {json.dumps(out)}")
     with open(path, "w") as f:
         json.dump(out, f)
@@ -212,6 +218,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if os.environ.get("HSA_DIAG_OUT"):
+        _lib.check(_lib.lib().hsa_diag_counters((C.c_ulonglong * 16)(), 1))
     t0 = time.perf_counter()
     for s in range(a.steps):
         ev[s][0].record(lib_stream)
@@ -222,6 +230,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kms = [e0.elapsed_time(e1) for e0, e1 in ev]
+    # per-kernel split of one more (untimed) step: k_widths, then k_search
+    launch(a.warmup + a.steps)
+    split_ms = gi.last_pass_ms()
+    torch.cuda.synchronize()
+    log(f"[bench] rank {rank}: kernel split of one step: k_widths {split_ms[0]:.2f} ms, k_search {split_ms[1]:.2f} ms")
     if os.environ.get("HSA_DIAG_OUT"):
         diag_dump(os.environ["HSA_DIAG_OUT"])
     log(f"[bench] rank {rank}: per-step device ms {[round(x, 2) for x in kms]}, wall {elapsed * 1e3:.1f} ms")

@@ -24,7 +24,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_index_bytes", "hsa_index_device", "hsa_occ4_batch", "hsa_step_batch", "hsa_width_batch",
     "hsa_search_batch", "hsa_search_device", "hsa_configure", "hsa_free", "hsa_synth_genome_device",
     "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
-    "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather64",
+    "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather64", "hsa_last_pass_ms",
 ]
 
 
@@ -215,6 +215,12 @@ class GpuIndex:
     def search_device(self, regimes, batch: "DeviceBatch"):
         rg = (Regime * len(regimes))(*regimes)
         check(lib().hsa_search_device(self.h, rg, len(regimes), C.byref(batch), None))
+
+    def last_pass_ms(self):
+        """(k_widths ms, k_search ms) of the last device pass on this index."""
+        w, q = C.c_float(), C.c_float()
+        check(lib().hsa_last_pass_ms(self.h, C.byref(w), C.byref(q)))
+        return w.value, q.value
 
     def nbytes(self) -> int:
         return int(lib().hsa_index_bytes(self.h))

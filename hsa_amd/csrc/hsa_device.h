@@ -74,3 +74,44 @@ __device__ __forceinline__ void hsa_occ4(const RankDir d, uint32_t p, uint32_t o
     const uint32_t bb = p / HSA_BLK_CHARS;
     hsa_occ_in_block(d.blk + (size_t)bb * 4, p - bb * HSA_BLK_CHARS, o);
 }
+
+// Occ of ONE character c over one block at in-block offset r (0..191): the width
+// (bwt_cal_width, BWTSARangeForeward) and exact-tail steps need a single count.
+// A code equal to c becomes 11 after XOR with the complement pattern of c, so one
+// popcount per code word instead of three.
+__device__ __forceinline__ uint32_t hsa_occ1_in_block(const uint4 *__restrict__ q, uint32_t r, uint32_t c)
+{
+    const bool up = r >= 96u;
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(q);
+    const uint4 h = q[0];
+    const uint4 w4 = *reinterpret_cast<const uint4 *>(base + (up ? 12 : 4));
+    const uint2 w2 = *reinterpret_cast<const uint2 *>(base + (up ? 10 : 8));
+    const uint32_t w[6] = {up ? w2.x : w4.x, up ? w2.y : w4.y, up ? w4.x : w4.z,
+                           up ? w4.y : w4.w, up ? w4.z : w2.x, up ? w4.w : w2.y};
+    const uint32_t n = up ? r - 96u : r;
+    const uint32_t qq = n >> 4;
+    const uint32_t part = (n & 15u) ? ((1u << (2u * (n & 15u))) - 1u) : 0u;
+    const uint32_t flip = up ? 0u : 0xffffffffu;
+    const uint32_t pat = ~(c * 0x55555555u);            // XOR turns code c into 0b11
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) {
+        const uint32_t pm = k < qq ? 0xffffffffu : (k == qq ? part : 0u);
+        const uint32_t x = w[k] ^ pat;
+        cnt += __popc(x & (x >> 1) & (pm ^ flip) & 0x55555555u);
+    }
+    const uint32_t hc = c == 0 ? h.x : c == 1 ? h.y : c == 2 ? h.z : h.w;
+    return up ? hc + cnt : hc - cnt;
+}
+
+// Occ(p1, c) and Occ(p2, c) on one BWT; returns the distinct 64-byte blocks (1 or 2).
+__device__ __forceinline__ uint32_t hsa_occ1_pair(const RankDir d, uint32_t p1, uint32_t p2, uint32_t c,
+                                                  uint32_t &a, uint32_t &b)
+{
+    p1 -= (p1 > d.isa0);
+    p2 -= (p2 > d.isa0);
+    const uint32_t b1 = p1 / HSA_BLK_CHARS, b2 = p2 / HSA_BLK_CHARS;
+    a = hsa_occ1_in_block(d.blk + (size_t)b1 * 4, p1 - b1 * HSA_BLK_CHARS, c);
+    b = hsa_occ1_in_block(d.blk + (size_t)b2 * 4, p2 - b2 * HSA_BLK_CHARS, c);
+    return 1u + (b2 != b1);
+}

@@ -68,27 +68,25 @@ int hsa_grow(void **p, size_t *cap, size_t need)
 
 void hsa_scratch_free(SearchScratch &s)
 {
-    (void)hipFree(s.width); (void)hipFree(s.pool); (void)hipFree(s.nxt); (void)hipFree(s.hbuf);
+    (void)hipFree(s.pool); (void)hipFree(s.nxt); (void)hipFree(s.hbuf);
     s = SearchScratch();
 }
 
-int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t wcap, size_t pcap, size_t hcap)
+int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap)
 {
-    if (lanes <= s.lanes && wcap <= s.wcap && pcap <= s.pcap && hcap <= s.hcap && s.width) return 0;
+    if (lanes <= s.lanes && pcap <= s.pcap && hcap <= s.hcap && s.pool) return 0;
     lanes = lanes > s.lanes ? lanes : s.lanes;
-    wcap = wcap > s.wcap ? wcap : s.wcap;
     pcap = pcap > s.pcap ? pcap : s.pcap;
     hcap = hcap > s.hcap ? hcap : s.hcap;
     hsa_scratch_free(s);
-    if (hipMalloc(&s.width, lanes * wcap * sizeof(uint2)) != hipSuccess ||
-        hipMalloc(&s.pool, lanes * pcap * sizeof(uint4)) != hipSuccess ||
+    if (hipMalloc(&s.pool, lanes * pcap * sizeof(uint4)) != hipSuccess ||
         hipMalloc(&s.nxt, lanes * pcap * sizeof(uint16_t)) != hipSuccess ||
         hipMalloc(&s.hbuf, lanes * hcap * 9 * sizeof(uint32_t)) != hipSuccess) {
         hsa_set_error("scratch allocation failed (lanes %zu, pool %zu, hits %zu)", lanes, pcap, hcap);
         hsa_scratch_free(s);
         return HSA_E_MEM;
     }
-    s.lanes = lanes; s.wcap = wcap; s.pcap = pcap; s.hcap = hcap;
+    s.lanes = lanes; s.pcap = pcap; s.hcap = hcap;
     return 0;
 }
 
@@ -196,6 +194,7 @@ static int index_init(int device, hsa_index **out)
     HSA_HIP(hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking));
     HSA_HIP(hipEventCreate(&ix->ev0));
     HSA_HIP(hipEventCreate(&ix->ev1));
+    HSA_HIP(hipEventCreate(&ix->evm));
     HSA_HIP(hipMalloc(&ix->d_ctr, 16 * sizeof(uint64_t)));
     *out = ix;
     return 0;
@@ -249,9 +248,10 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     (void)hipSetDevice(ix->device);
     (void)hipFree(ix->blk[0]); (void)hipFree(ix->blk[1]);
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big);
-    (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr);
+    (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
+    if (ix->evm) (void)hipEventDestroy(ix->evm);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
     delete ix;
 }

@@ -19,8 +19,7 @@ void hsa_set_error(const char *fmt, ...);
 
 // Per-launch scratch of the search kernel: grows, never shrinks.
 struct SearchScratch {
-    size_t lanes = 0, wcap = 0, pcap = 0, hcap = 0;
-    uint2 *width = nullptr;      // lanes * wcap
+    size_t lanes = 0, pcap = 0, hcap = 0;
     uint4 *pool = nullptr;       // lanes * pcap
     uint16_t *nxt = nullptr;     // lanes * pcap
     uint32_t *hbuf = nullptr;    // lanes * hcap * 9
@@ -38,14 +37,17 @@ struct hsa_index {
     // staging for the host-pointer batch API
     void *d_in = nullptr; size_t d_in_cap = 0;
     void *d_out = nullptr; size_t d_out_cap = 0;
+    // per-(read, strand) width rows written by k_widths, read by k_search
+    void *d_wrows = nullptr; size_t d_wrows_cap = 0;
     uint64_t *d_ctr = nullptr;
     unsigned char staged[512];          // last regime block copied to d_in (skip identical re-copies)
     int staged_valid = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t evm = nullptr;           // between k_widths and k_search of the last pass (timing split)
 };
 
 int hsa_grow(void **p, size_t *cap, size_t need);
-int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t wcap, size_t pcap, size_t hcap);
+int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap);
 void hsa_scratch_free(SearchScratch &s);
 
 // Knobs (hsa_configure).

@@ -1,36 +1,35 @@
-// hsa_search.hip -- the bwa_cal_sa_reg_gap per-read loop as one persistent kernel.
+// hsa_search.hip -- the bwa_cal_sa_reg_gap per-read loop as two persistent kernels.
+//
+// k_widths: bwt_cal_width (bwtaln.c:73-98) for every (read, strand) of the batch --
+//   the seed width and the whole-read width of the rc and the fwd strand, one work
+//   item per lane, pulled from a global queue.  All lanes run the same short step
+//   (one single-character rank pair on the reverse BWT), so the waves stay
+//   converged.  Output: per (read, strand) a row of pruning bytes
+//   min(bid,127) | (w[p] == w[p+1]) << 7 for the read and for the seed, and the
+//   full w values (only gap_shadow reads them).
+// k_search: per read, rc strand then fwd strand (bwtaln.c:343-359): copy the
+//   strand's pruning bytes into LDS and run bwt_match_gap (bwtgap.c:118-331); the
+//   first strand with hits wins; no hit on either -> HSA_F_FALLBACK (splice).
 //
 // One lane owns one read at a time (reads are pulled from a global queue with a
 // wave-aggregated atomic, so a lane that finishes a cheap read immediately takes
-// the next one: work-stealing at read granularity).  Per read the lane runs the
-// reference's sequence exactly (bwtaln.c:343-373):
-//   for strand = rc, fwd:  bwt_cal_width(seed) ; bwt_cal_width(read) ; bwt_match_gap
-//   first strand with hits wins; no hit on either -> HSA_F_FALLBACK (splice).
+// the next one: work-stealing at read granularity).  Every loop iteration of
+// k_search performs at most ONE bidirectional rank step per lane (two Occ queries
+// on the forward BWT, usually one 64-byte block), whatever the lane is doing --
+// exact tail (bwt_match_exact) or expansion -- so all lanes issue their HBM loads
+// together and the state machine in between is register/LDS work.  Control that
+// needs no rank (pruned pops, hits) loops without touching the BWT.
 //
-// Every loop iteration of the kernel performs at most ONE bidirectional rank step
-// per lane (two Occ queries on one BWT, usually one 64-byte block), whatever the
-// lane is doing -- width extension, exact tail (bwt_match_exact) or expansion --
-// so all lanes issue their HBM loads together and the state machine in between
-// is register/LDS work.  Control that needs no rank (pruned pops, hits) loops
-// without touching the BWT.
-//
-// Occupancy is what hides the HBM latency of the random rank loads, so the
-// per-lane state is packed to ~30 VGPRs (control words, one shared interval
-// register set for width/exact steps, stack entries decoded on demand) and the
-// kernel is bounded to 128 VGPRs = 4 waves per SIMD.
-//
-// Per-lane state in LDS (160 KiB per CU):
-//   * widths (bwt_width_t, bwtaln.h:36-39) as one byte per position:
-//     min(bid,127) | (w[p] == w[p+1]) << 7 -- everything bwt_match_gap's pruning
-//     reads (bwtgap.c:170, :256-263).  The full w values live in HBM and are only
-//     touched by gap_shadow (bwtgap.c:94-105) after an added hit.
-//   * the stack's bucket heads.  Buckets are the REACHABLE scores only (a score
-//     table per regime maps aln_score -> dense bucket, order preserved), so
-//     `-n 4 -o 0` needs 6 heads instead of the reference's 54 (bwtgap.c:18).
-// Stack entries (16 bytes + a 16-bit link) live in a per-lane pool in HBM; a
-// bit mask in registers gives the lowest non-empty bucket (== gap_stack_t.best).
-// The child pushed LAST by an expansion is always the next pop (it is the top of
-// the lowest bucket), so it stays in registers ("virtual top").
+// Per-lane state in LDS (160 KiB per CU): the pruning bytes of the current strand
+// (everything bwt_match_gap's pruning reads: bwtgap.c:170, :256-263) and the
+// stack's bucket heads.  Buckets are the REACHABLE scores only (a score table per
+// regime maps aln_score -> dense bucket, order preserved), so `-n 4 -o 0` needs 6
+// heads instead of the reference's 54 (bwtgap.c:18).  Stack entries (16 bytes + a
+// 16-bit link) live in a per-lane pool in HBM; a bit mask in registers gives the
+// lowest non-empty bucket (== gap_stack_t.best).  The child pushed LAST by an
+// expansion is always the next pop when its bucket is the lowest, so it stays in
+// registers ("virtual top").  A regime set without gap opens (max_gapo == 0: every
+// entry stays in state M) runs a specialisation without the indel code.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -49,7 +48,7 @@
 #define BLOCK 256
 #define MAXB 128          // buckets per regime (and score table length)
 
-enum : uint32_t { PH_IDLE = 0, PH_WIDTH, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT };
+enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT };
 
 struct SearchArgs {
     RankDir fwd, rev;
@@ -67,11 +66,14 @@ struct SearchArgs {
     uint32_t *hits;
     uint64_t hit_cap;
     unsigned long long *ctr;       // [0] queue head [1] hit alloc [2] rank queries [3] blocks [4] pops [5] errors
-    uint32_t *wg;                  // per lane wcap: full width_back w values (gap_shadow only)
+                                   // [6] width item queue head
+    const uint8_t *wb, *ws;        // width rows of k_widths (row = list position * 2 + strand),
+    uint32_t *wg;                  //   64 rows interleaved; wg: full w values (gap_shadow only)
+    uint32_t rb, rs, rg;           //   row capacities: bytes, bytes, words
     uint4 *pool;
     uint16_t *nxt;
     uint32_t *hbuf;
-    uint32_t wcap, pcap, hcap, nb;
+    uint32_t pcap, hcap, nb;
     uint32_t off_heads, off_wb, off_ws;   // LDS byte offsets
 };
 
@@ -88,13 +90,12 @@ __device__ __forceinline__ uint32_t meta_pack(uint32_t i, uint32_t st, uint32_t 
 #define M_GO(m) ((int)(((m) >> 20) & 15u))
 #define M_GE(m) ((int)((m) >> 24))
 
-// control word: ph:3 | strand:1 | has_seed:1 | reg:1 | has_vt:1 | wseed:1 | ovf:2 | len:10 | seed_len:10
+// control word: ph:3 | strand:1 | has_seed:1 | reg:1 | has_vt:1 | -:1 | ovf:2 | len:10 | seed_len:10
 #define C_PH(c) ((c) & 7u)
 #define C_STRAND(c) (((c) >> 3) & 1u)
 #define C_SEED(c) (((c) >> 4) & 1u)
 #define C_REG(c) (((c) >> 5) & 1u)
 #define C_VT(c) (((c) >> 6) & 1u)
-#define C_WSEED(c) (((c) >> 7) & 1u)
 #define C_OVF(c) (((c) >> 8) & 3u)
 #define C_LEN(c) ((int)(((c) >> 10) & 1023u))
 #define C_SLEN(c) ((int)(((c) >> 20) & 1023u))
@@ -143,16 +144,131 @@ template <> struct BMask<2> {
     __device__ __forceinline__ void reset(int b) { if (b < 64) m0 &= ~(1ull << b); else m1 &= ~(1ull << (b - 64)); }
 };
 
+// Pruning element of one read position, as k_widths writes it and k_search keeps it
+// in LDS: min(bid, BIDM) | (w[p] == w[p+1]) << BIDB | (code & 3) << CSH |
+// (code > 3) << (CSH + 2), code being the strand sequence's base at p.  A bid is
+// only ever compared with m, m - 1 or m_seed - 1 (bwtgap.c:170, :256-263), all
+// <= max(max_diff, max_seed_diff), so capping it at BIDM is exact while that bound
+// is < BIDM: 8-bit elements (4-bit bid) for bounds <= 14, else 16-bit (8-bit bid).
+// The base code keeps exactly what bwt_match_gap derives from it: c > 3 (N) and
+// (c + j) & 3 (bwtgap.c:305-306).
+template <typename WT> struct WFmt {
+    static constexpr uint32_t BIDB = sizeof(WT) == 1 ? 4u : 8u;
+    static constexpr uint32_t BIDM = (1u << BIDB) - 1u;
+    static constexpr uint32_t EQ = 1u << BIDB;
+    static constexpr uint32_t CSH = BIDB + 1u;
+    static constexpr uint32_t EB = 8u * sizeof(WT);           // bits per element
+    static constexpr uint32_t EPW = 4u / sizeof(WT);          // elements per u32
+    __device__ static uint32_t code_bits(uint32_t c) { return (c & 3u) << CSH | (c > 3 ? 4u : 0u) << CSH; }
+    __device__ static uint32_t code(uint32_t v) { return (v >> CSH) & 7u; }   // 0..3, or 4..7 for N
+};
+
+// ---------------------------------------------------------------- k_widths
+// bwt_cal_width type 1 (bwtaln.c:84-97) of every (read, strand): the whole read
+// (width_back) and its last seed_len bases (width_seed, bwtaln.c:344-348).  The
+// strand-1 sequence is the reverse complement (seq_reverse(.., 1), bwtaln.c:337).
+// Forward extension on the reverse BWT with the forward C table
+// (BWTSARangeForeward, 2BWT-Interface.c:121-131).
+//
+// One lane per (read, strand) row, rows in order, so a wave's 64 rows are stored
+// interleaved -- element e of row R at (R / 64 * cap + e) * 64 + R % 64 -- and every
+// store of a step is one coalesced 256-byte wave store.  The two chains of a row
+// (read and seed) are independent, so each iteration advances both: two rank pairs
+// in flight per lane.  All reads of a batch have similar lengths, so the lanes stay
+// converged without a work queue.
+struct WChain {
+    uint32_t k, l, bid, prevw, acc;
+};
+
+template <typename WT>
+__device__ __forceinline__ void width_step(const SearchArgs &a, WChain &ch, uint32_t t, uint32_t n, uint32_t c,
+                                           uint32_t cbits, uint32_t *__restrict__ brow, uint32_t *__restrict__ wrow,
+                                           uint32_t &st_q, uint32_t &st_b)
+{
+    using F = WFmt<WT>;
+    uint32_t w;
+    if (t < n) {
+        if (c < 4) {
+            uint32_t ok, ol;
+            st_b += hsa_occ1_pair(a.rev, ch.k, ch.l + 1u, c, ok, ol);
+            st_q += 2;
+            const uint32_t cc = pick4(a.C, c);
+            ch.k = cc + ok + 1u;
+            ch.l = cc + ol;
+        }
+        if (ch.k > ch.l || c > 3) { ch.k = 0; ch.l = a.T; ++ch.bid; }
+        w = ch.l - ch.k + 1u;
+    } else {
+        w = 0; ++ch.bid;                                         // width[len] = {0, ++bid}
+    }
+    // element t-1 is final now (its eq bit needs w[t]); elements go out a word at a time
+    if (t > 0) {
+        if (ch.prevw == w) ch.acc |= F::EQ << (((t - 1) % F::EPW) * F::EB);
+        if ((t - 1) % F::EPW == F::EPW - 1) { brow[((t - 1) / F::EPW) * 64] = ch.acc; ch.acc = 0; }
+    }
+    ch.acc |= ((ch.bid < F::BIDM ? ch.bid : F::BIDM) | cbits) << ((t % F::EPW) * F::EB);
+    if (wrow) wrow[t * 64] = w;
+    ch.prevw = w;
+    if (t == n) brow[(t / F::EPW) * 64] = ch.acc;
+}
+
+template <typename WT>
+__global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
+{
+    using F = WFmt<WT>;
+    const uint32_t R = blockIdx.x * BLOCK + threadIdx.x;     // row = list position * 2 + strand
+    if (R >= 2u * (uint32_t)a.n_jobs) return;
+    const uint32_t q = R >> 1, strand = R & 1u;
+    const hsa_job_t J = a.jobs[a.job_list ? a.job_list[q] : (int)q];
+    const uint32_t len = J.len, off = (uint32_t)J.off;
+    const bool has_seed = (int)len > J.seed_len;
+    const uint32_t slen = has_seed ? (uint32_t)J.seed_len : 0u;
+    const size_t rb = R >> 6, rl = R & 63u;
+    uint32_t *const brow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.wb)) + rb * (a.rb / 4) * 64 + rl;
+    uint32_t *const srow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.ws)) + rb * (a.rs / 4) * 64 + rl;
+    uint32_t *const wrow = a.wg + rb * a.rg * 64 + rl;
+    WChain f{0, a.T, 0, 0, 0}, sd{0, a.T, 0, 0, 0};
+    uint32_t st_q = 0, st_b = 0;
+    const uint32_t s0 = len - slen;
+    auto base = [&](uint32_t sp) -> uint32_t {
+        const uint32_t c = a.codes[off + (strand ? len - 1u - sp : sp)];
+        return strand && c < 4 ? 3u - c : c;
+    };
+    for (uint32_t t = 0; t <= len; ++t) {
+        const uint32_t cf = t < len ? base(t) : 4u;
+        // the read's elements also carry the strand sequence's base (k_search's getc)
+        width_step<WT>(a, f, t, len, cf, t < len ? F::code_bits(cf) : 0u, brow, wrow, st_q, st_b);
+        if (has_seed && t <= slen) {
+            const uint32_t cs = t < slen ? base(s0 + t) : 4u;
+            width_step<WT>(a, sd, t, slen, cs, 0u, srow, nullptr, st_q, st_b);
+        }
+    }
+    atomicAdd(&a.ctr[2], (unsigned long long)st_q);
+    atomicAdd(&a.ctr[3], (unsigned long long)st_b);
+    atomicAdd(&a.ctr[7], (unsigned long long)st_q);
+}
+
 #ifdef HSA_DIAG
 // Diagnostic build only (-DHSA_DIAG, never the product library): per-workgroup
 // start/end s_memtime and s_memrealtime of the last launch, for the in-kernel
 // clock and the workgroup-duration spread.
 __device__ unsigned long long g_diag[8192 * 4];
+// event counters: 0 width steps, 1 exact steps, 2 expand steps, 3 virtual-top pops,
+// 4 pool pops, 5 outer iterations (per wave), 6 lanes stepping summed over outer
+// iterations, 7 control-loop iterations (per wave), 8 entries flushed to the pool,
+// 9..12 shader cycles per wave in acquisition / control / rank-load wait / apply,
+// 13 gap_shadow calls with last_diff_pos > 0, 14 their summed last_diff_pos,
+// 15 strand starts
+__device__ unsigned long long g_dctr[16];
+#define DC(i) (++dc[i])
+#else
+#define DC(i) ((void)0)
 #endif
 
-template <int MW>
+template <int MW, bool GAPS, typename WT>
 __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 {
+    using F = WFmt<WT>;
 #ifdef HSA_DIAG
     if (threadIdx.x == 0 && blockIdx.x < 8192) {
         g_diag[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime();
@@ -170,13 +286,13 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         reinterpret_cast<uint32_t *>(s_reg)[tid] = reinterpret_cast<const uint32_t *>(a.regimes)[tid];
     __syncthreads();
     uint16_t *const s_heads = reinterpret_cast<uint16_t *>(s_lds + a.off_heads);
-    uint8_t *const s_wb = s_lds + a.off_wb;
-    uint8_t *const s_ws = s_lds + a.off_ws;
+    WT *const s_wb = reinterpret_cast<WT *>(s_lds + a.off_wb);
+    WT *const s_ws = reinterpret_cast<WT *>(s_lds + a.off_ws);
     // per-lane HBM scratch, wave-interleaved: element e of lane l of wave w at
     // (w * cap + e) * 64 + l, so one wave's accesses stay inside one small region
     // (few pages) and lanes at equal e coalesce
     const size_t wv = gid >> 6;
-#define WG(p) a.wg[(wv * a.wcap + (uint32_t)(p)) * 64 + lane]
+#define WG(p) wgrow[(uint32_t)(p) * 64]
 #define POOL(s) a.pool[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
 #define NXT(s) a.nxt[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
 #define HB(i) a.hbuf[(wv * a.hcap * 9 + (uint32_t)(i)) * 64 + lane]
@@ -188,18 +304,25 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
     // ---- persistent per-lane state (~30 registers)
     uint32_t ctl = PH_IDLE;        // control word (C_* accessors)
     int job = -1;
-    uint32_t off = 0;              // read offset in codes
+    uint32_t qpos = 0;             // position of the read in the job list (width row = qpos * 2 + strand)
     uint32_t pen = 0;              // s_mm | s_gapo << 10 | s_gape << 20
     uint32_t rmode = 0;            // mode | max_gapo << 8 | max_gape << 16
-    uint32_t pos = 0;              // wpos:11 | wbid:11 (width) -- or -- xj (exact)
-    uint32_t ik = 0, il = 0;       // width / exact-tail interval
-    uint32_t aux = 0;              // width: w of the previous position; exact: rev_l
+    uint32_t pos = 0;              // exact tail: next position
+    uint32_t ik = 0, il = 0;       // exact-tail interval
+    uint32_t aux = 0;              // exact tail: rev_l
+    uint32_t *wgrow = nullptr;     // full widths of the current strand (HBM)
     int opt_max_diff = 0, max_diff = 0, best_score = 0, best_cnt = 0, n_aln = 0, n_entries = 0;
     uint32_t pool_top = 0;
     BMask<MW> mask;
     uint4 vt = make_uint4(0, 0, 0, 0);
     uint4 e = make_uint4(0, 0, 0, 0);    // current entry (k, l, rev_k, meta)
     uint32_t st_q = 0, st_b = 0, st_p = 0;
+#ifdef HSA_DIAG
+    uint32_t dc[16] = {0};
+    uint64_t tsec[4] = {0, 0, 0, 0};
+    uint64_t tt = 0;
+#define TMARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); tsec[k] += t_ - tt; tt = t_; } while (0)
+#endif
 
 #define S_MM ((int)(pen & 1023u))
 #define S_GO ((int)((pen >> 10) & 1023u))
@@ -208,41 +331,12 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 #define R_MAXGO ((int)((rmode >> 8) & 255u))
 #define R_MAXGE ((int)(rmode >> 16))
 #define SCORE(mm, go, ge) ((mm) * S_MM + (go) * S_GO + (ge) * S_GE)
-#define WPOS ((int)(pos & 2047u))
-#define WBID ((int)(pos >> 11))
 
-    auto getc = [&](int p) -> uint32_t {
-        const int len = C_LEN(ctl);
-        if (C_STRAND(ctl)) {
-            const uint32_t c = a.codes[off + (uint32_t)(len - 1 - p)];
-            return c < 4 ? 3u - c : c;
-        }
-        return a.codes[off + (uint32_t)p];
-    };
-    auto start_width = [&]() {
-        ctl = (ctl & ~(1u << 7)) | (C_SEED(ctl) << 7);   // wseed = has_seed
-        pos = 0; ik = 0; il = a.T;
-        SET_PH(ctl, PH_WIDTH);
-    };
-    auto wlen = [&]() -> int { return C_WSEED(ctl) ? C_SLEN(ctl) : C_LEN(ctl); };
-    auto wstart = [&]() -> int { return C_WSEED(ctl) ? C_LEN(ctl) - C_SLEN(ctl) : 0; };
-    // store position WPOS of the width being computed (bwtaln.c:95-96)
-    auto put_width = [&](uint32_t w) {
-        const int p = WPOS;
-        const uint32_t bq = WBID < 127 ? (uint32_t)WBID : 127u;
-        if (C_WSEED(ctl)) {
-            if (p > 0 && aux == w) WS(p - 1) |= 0x80;
-            WS(p) = (uint8_t)bq;
-        } else {
-            if (p > 0 && aux == w) WB(p - 1) |= 0x80;
-            WB(p) = (uint8_t)bq;
-            WG(p) = w;
-        }
-        aux = w;
-        pos += 1;
-    };
+    // base of the current strand's sequence at p (from the LDS element, see WFmt)
+    auto getc = [&](int p) -> uint32_t { return F::code(WB(p)); };
     auto flush = [&](uint4 v, int b) {
         if (pool_top >= a.pcap || (uint32_t)b >= a.nb) { ctl |= 1u << 8; return; }
+        DC(8);
         const uint32_t slot = pool_top++;
         POOL(slot) = v;
         NXT(slot) = mask.test(b) ? HEAD(b) : (uint16_t)NIL16;
@@ -258,6 +352,33 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         ctl |= 1u << 6;
         n_entries = 1;
         SET_PH(ctl, PH_POP);
+    };
+    // copy the strand's pruning bytes (k_widths) into the lane's LDS columns, then
+    // start bwt_match_gap (bwtgap.c:141-142)
+    auto start_strand = [&]() {
+        const uint32_t r = qpos * 2u + C_STRAND(ctl);
+        const size_t rb = r >> 6, rl = r & 63u;
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.wb) + rb * (a.rb / 4) * 64 + rl;
+        const int len = C_LEN(ctl);
+        for (int q = 0; q <= len; q += F::EPW) {
+            const uint32_t v = src[(q / F::EPW) * 64];
+#pragma unroll
+            for (int b = 0; b < (int)F::EPW; ++b)
+                if (q + b <= len) WB(q + b) = (WT)(v >> (F::EB * b));
+        }
+        if (C_SEED(ctl)) {
+            const uint32_t *ss = reinterpret_cast<const uint32_t *>(a.ws) + rb * (a.rs / 4) * 64 + rl;
+            const int sl = C_SLEN(ctl);
+            for (int q = 0; q <= sl; q += F::EPW) {
+                const uint32_t v = ss[(q / F::EPW) * 64];
+#pragma unroll
+                for (int b = 0; b < (int)F::EPW; ++b)
+                    if (q + b <= sl) WS(q + b) = (WT)(v >> (F::EB * b));
+            }
+        }
+        wgrow = a.wg + rb * a.rg * 64 + rl;
+        DC(15);
+        start_search();
     };
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
         a.n_aln[job] = na;
@@ -285,7 +406,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             finish_job(0, n_aln, o);
         } else if (C_STRAND(ctl)) {
             ctl &= ~(1u << 3);          // strand 0
-            start_width();
+            start_strand();
         } else {
             finish_job(HSA_F_FALLBACK, 0, 0);
         }
@@ -314,16 +435,19 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             const uint32_t x = l - k + 1u;
             const int ldp = M_ISD(m) ? M_I(m) : 0;
             if (ldp > 0) {
+#ifdef HSA_DIAG
+                DC(13); dc[14] += (uint32_t)ldp;
+#endif
                 uint32_t jj = 0;
                 for (int p = 0; p < ldp; ++p) {
                     uint32_t w = WG(p);
                     if (w > x) { w -= x; WG(p) = w; }
-                    else if (w == x) { WB(p) = (uint8_t)((WB(p) & 0x80u) | 1u); WG(p) = a.T - (++jj); }
+                    else if (w == x) { WB(p) = (WT)((WB(p) & ~F::BIDM) | 1u); WG(p) = a.T - (++jj); }
                 }
                 uint32_t wnext = WG(ldp);
                 for (int p = ldp - 1; p >= 0; --p) {
                     const uint32_t w = WG(p);
-                    WB(p) = (uint8_t)((WB(p) & 0x7fu) | (w == wnext ? 0x80u : 0u));
+                    WB(p) = (WT)((WB(p) & ~F::EQ) | (w == wnext ? F::EQ : 0u));
                     wnext = w;
                 }
             }
@@ -341,6 +465,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         return mm;
     };
 
+#ifdef HSA_DIAG
+    tt = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {
         // ---------------- (A) read acquisition, wave aggregated
         {
@@ -354,9 +481,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                 if (need) {
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
                     if (j < (unsigned long long)a.n_jobs) {
+                        qpos = (uint32_t)j;
                         job = a.job_list ? a.job_list[j] : (int)j;
                         const hsa_job_t J = a.jobs[job];
-                        off = (uint32_t)J.off;
                         opt_max_diff = J.max_diff;
                         const uint32_t len = J.len;
                         const uint32_t has_seed = (int)len > J.seed_len;
@@ -366,7 +493,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                         pen = (uint32_t)R->s_mm | (uint32_t)R->s_gapo << 10 | (uint32_t)R->s_gape << 20;
                         rmode = (uint32_t)R->mode | (uint32_t)R->max_gapo << 8 | (uint32_t)R->max_gape << 16;
                         if (opt_max_diff > R->max_diff) ctl |= 2u << 8;
-                        start_width();
+                        start_strand();
                     } else {
                         SET_PH(ctl, PH_EXIT);
                     }
@@ -375,43 +502,38 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         }
         if (__all(C_PH(ctl) == PH_EXIT)) break;
 
+#ifdef HSA_DIAG
+        TMARK(0);
+#endif
         // ---------------- (B) control until a rank step is needed
-        int req = 0, rdir = 0;
+        int req = 0;
         uint32_t rp1 = 0, rp2 = 0;
+#ifdef HSA_DIAG
+        if (lane == 0) DC(5);
+#endif
         while (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && !req) {
+#ifdef HSA_DIAG
+            { const uint64_t em = __ballot(1); if (lane == __ffsll((unsigned long long)em) - 1) DC(7); }
+#endif
             if (C_OVF(ctl)) {
                 if (C_OVF(ctl) > 1) atomicAdd(&a.ctr[5], 1ull);
                 finish_job(HSA_F_OVERFLOW, 0, 0);
                 break;
             }
             const uint32_t ph = C_PH(ctl);
-            if (ph == PH_WIDTH) {
-                // bwt_cal_width type 1 (bwtaln.c:84-97)
-                const int wl = wlen(), ws0 = wstart();
-                while (WPOS < wl) {
-                    const uint32_t c = getc(ws0 + WPOS);
-                    if (c < 4) break;
-                    ik = 0; il = a.T; pos += 1u << 11;                       // N: restart, ++bid
-                    put_width(il - ik + 1u);
-                }
-                if (WPOS < wl) { req = 1; rdir = 1; rp1 = ik; rp2 = il + 1u; break; }
-                pos += 1u << 11;
-                put_width(0u);                                              // width[len] = {0, ++bid}
-                if (C_WSEED(ctl)) { ctl &= ~(1u << 7); pos = 0; ik = 0; il = a.T; }
-                else start_search();
-                continue;
-            }
             if (ph == PH_EXACT) {
                 const uint32_t c = getc((int)pos);
                 if (c > 3) { SET_PH(ctl, PH_POP); continue; }              // 2BWT-Interface.c:377
-                req = 1; rdir = 0; rp1 = ik; rp2 = il + 1u;
+                req = 1; rp1 = ik; rp2 = il + 1u;
                 break;
             }
             // PH_POP: bwtgap.c:144-186
             if (n_entries == 0 || n_entries > RG(max_entries)) { end_strand(); continue; }
             if (C_VT(ctl)) {
+                DC(3);
                 e = vt; ctl &= ~(1u << 6);
             } else {
+                DC(4);
                 const int b = mask.lowest();
                 const uint32_t slot = HEAD(b);
                 e = POOL(slot);
@@ -429,7 +551,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             const int em = m_of(m);
             if (em < 0) continue;
             const int ei = M_I(m);
-            if (ei > 0 && em < (int)(WB(ei - 1) & 0x7fu)) continue;
+            if (ei > 0 && em < (int)(WB(ei - 1) & F::BIDM)) continue;
             if (ei == 0) {
                 if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) end_strand();
                 continue;
@@ -439,27 +561,35 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                 SET_PH(ctl, PH_EXACT);
                 continue;
             }
-            req = 1; rdir = 0; rp1 = e.x; rp2 = e.y + 1u;
+            req = 1; rp1 = e.x; rp2 = e.y + 1u;
             SET_PH(ctl, PH_EXPAND);
         }
 
+#ifdef HSA_DIAG
+        TMARK(1);
+#endif
         // ---------------- (C) the rank step
         uint32_t oa[4], ob[4];
+#ifdef HSA_DIAG
+        {
+            const uint64_t rb = __ballot(req);
+            if (lane == 0) dc[6] += (uint32_t)__popcll(rb);
+            const uint32_t ph0 = C_PH(ctl);
+            if (req) DC(ph0 == PH_EXACT ? 1 : 2);
+        }
+#endif
         if (req) {
-            st_b += hsa_occ_pair(rdir ? a.rev : a.fwd, rp1, rp2, oa, ob);
+            st_b += hsa_occ_pair(a.fwd, rp1, rp2, oa, ob);
             st_q += 2;
         }
 
+#ifdef HSA_DIAG
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        TMARK(2);
+#endif
         // ---------------- (D) apply
         const uint32_t ph = C_PH(ctl);
-        if (req && ph == PH_WIDTH) {
-            const uint32_t c = getc(wstart() + WPOS);
-            const uint32_t cc = pick4(a.C, c);
-            ik = cc + pick4(oa, c) + 1u;
-            il = cc + pick4(ob, c);
-            if (ik > il) { ik = 0; il = a.T; pos += 1u << 11; }
-            put_width(il - ik + 1u);
-        } else if (req && ph == PH_EXACT) {
+        if (req && ph == PH_EXACT) {
             // BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170), one character
             const uint32_t c = getc((int)pos);
             uint32_t oc = 0;
@@ -502,17 +632,17 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             if (i > 0) {
                 // width[i-1].bid, width[i].bid and w[i-1] == w[i] (bwtgap.c:256-258)
                 const uint32_t w1 = WB(i - 1), w0 = WB(i);
-                const int b1 = (int)(w1 & 0x7fu), b0 = (int)(w0 & 0x7fu);
+                const int b1 = (int)(w1 & F::BIDM), b0 = (int)(w0 & F::BIDM);
                 if (b1 > em - 1) allow_diff = 0;
-                else if (b1 == em - 1 && b0 == em - 1 && (w1 & 0x80u)) allow_M = 0;
+                else if (b1 == em - 1 && b0 == em - 1 && (w1 & F::EQ)) allow_M = 0;
                 const int ii = i - (len - C_SLEN(ctl));
                 if (C_SEED(ctl) && ii > 0) {
                     int ems = RG(max_seed_diff) - (emm + ego);
                     if (R_MODE & MODE_GAPE) ems -= ege;
                     const uint32_t s1 = WS(ii - 1), s0 = WS(ii);
-                    const int c1 = (int)(s1 & 0x7fu), c0 = (int)(s0 & 0x7fu);
+                    const int c1 = (int)(s1 & F::BIDM), c0 = (int)(s0 & F::BIDM);
                     if (c1 > ems - 1) allow_diff = 0;
-                    else if (c1 == ems - 1 && c0 == ems - 1 && (s1 & 0x80u)) allow_M = 0;
+                    else if (c1 == ems - 1 && c0 == ems - 1 && (s1 & F::EQ)) allow_M = 0;
                 }
             }
             // pushes (bwtgap.c:267-325): all but the last go to the pool at once;
@@ -529,7 +659,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                 ++n_entries;
             };
             const int tmp = (R_MODE & MODE_LOGGAP) ? int_log2((uint32_t)(ege + ego)) / 2 + 1 : ego + ege;
-            if (allow_diff && (R_MAXGO > 0 || ego > 0)) {
+            if (GAPS && allow_diff && (R_MAXGO > 0 || ego > 0)) {
                 const int ies = RG(indel_end_skip);
                 if (i >= ies + tmp && len - i >= ies + tmp) {
                     if (est == ST_M) {
@@ -569,6 +699,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             }
             SET_PH(ctl, PH_POP);
         }
+#ifdef HSA_DIAG
+        TMARK(3);
+#endif
     }
 
 #ifdef HSA_DIAG
@@ -579,6 +712,12 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
     }
 #endif
     // statistics
+#ifdef HSA_DIAG
+    for (int i = 0; i < 16; ++i)
+        if (i < 9 || i > 12) atomicAdd(&g_dctr[i], (unsigned long long)dc[i]);
+    if (lane == 0)
+        for (int i = 0; i < 4; ++i) atomicAdd(&g_dctr[9 + i], (unsigned long long)tsec[i]);
+#endif
     atomicAdd(&a.ctr[2], (unsigned long long)st_q);
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);
@@ -597,8 +736,6 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 #undef R_MAXGO
 #undef R_MAXGE
 #undef SCORE
-#undef WPOS
-#undef WBID
 }
 
 // ---------------------------------------------------------------- host side
@@ -606,6 +743,15 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 extern "C" int hsa_diag_read(unsigned long long *out, int n_blocks)
 {
     HSA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 4 * (size_t)n_blocks));
+    return 0;
+}
+extern "C" int hsa_diag_counters(unsigned long long *out, int reset)
+{
+    HSA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dctr), sizeof(unsigned long long) * 16));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        HSA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dctr), z, sizeof z));
+    }
     return 0;
 }
 #endif
@@ -642,18 +788,23 @@ static int bucket_map(const hsa_regime_t &R, uint8_t map[MAXB])
 
 struct LaunchPlan {
     size_t lanes, blocks;
-    uint32_t wcap, pcap, hcap, nb;
+    uint32_t pcap, hcap, nb;
+    bool gaps, wide;                 // gap opens possible; 16-bit pruning elements (WFmt)
     uint32_t off_heads, off_wb, off_ws;
     size_t lds;
 };
 
-static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int nb, bool big, LaunchPlan &P)
+static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int nb, bool gaps, bool wide, bool big,
+                       LaunchPlan &P)
 {
     P.nb = (uint32_t)nb;
+    P.gaps = gaps;
+    P.wide = wide;
+    const uint32_t esz = wide ? 2u : 1u;
     P.off_heads = 2 * MAXB + 128;   // score tables, then the two regimes
     P.off_wb = P.off_heads + (uint32_t)nb * BLOCK * 2;
-    P.off_ws = P.off_wb + (uint32_t)(max_len + 1) * BLOCK;
-    P.lds = ((size_t)P.off_ws + (size_t)(max_seed + 1) * BLOCK + 15) / 16 * 16;
+    P.off_ws = P.off_wb + (uint32_t)(max_len + 1) * BLOCK * esz;
+    P.lds = ((size_t)P.off_ws + (size_t)(max_seed + 1) * BLOCK * esz + 15) / 16 * 16;
     if (P.lds > 160 * 1024) { hsa_set_error("reads too long for the LDS budget (%zu bytes)", P.lds); return HSA_E_ARG; }
     // Resident workgroups per CU, from gfx950's own limits: 160 KiB of LDS per CU,
     // and __launch_bounds__(BLOCK, 4) caps VGPRs so 4 workgroups of 4 waves fit.
@@ -679,25 +830,43 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     if (verbose < 0) verbose = getenv("HSA_VERBOSE") != nullptr;
     if (verbose) {
         int occ = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_search<1>, BLOCK, P.lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_search<1, true, uint8_t>, BLOCK, P.lds);
         fprintf(stderr, "[hsa] launch: %d CUs x %d workgroups (runtime occupancy query says %d), LDS %zu B, "
                 "%zu workgroups, %d buckets\n", ix->n_cu, per_cu, occ, P.lds, blocks, nb);
     }
-    P.wcap = (uint32_t)max_len + 1;
     P.pcap = big ? 65535u : (uint32_t)g_pool_entries;
     P.hcap = big ? 16384u : (uint32_t)g_hit_cap;
     return 0;
 }
 
-// Launch one search pass over jobs (or job_list subset) with device pointers.
-static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
-                       const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n,
-                       const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho, uint32_t *d_hits,
-                       uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st)
+template <typename WT>
+static void launch_search(const LaunchPlan &P, const SearchArgs &A, hipStream_t st)
 {
-    // width scratch is reserved in uint2 units; wg uses it as u32 (2 per unit)
-    int rc = hsa_scratch_reserve(S, P.lanes, (P.wcap + 1) / 2, P.pcap, P.hcap);
+    const dim3 g((unsigned)P.blocks), b(BLOCK);
+    if (P.nb <= 64) {
+        if (P.gaps) hipLaunchKernelGGL((k_search<1, true, WT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<1, false, WT>), g, b, P.lds, st, A);
+    } else {
+        if (P.gaps) hipLaunchKernelGGL((k_search<2, true, WT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<2, false, WT>), g, b, P.lds, st, A);
+    }
+}
+
+// One search pass over jobs (or a job_list subset) with device pointers: k_widths
+// fills the width rows of every (read, strand), then k_search runs the reads.
+static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
+                       const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
+                       int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
+                       uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st)
+{
+    int rc = hsa_scratch_reserve(S, P.lanes, P.pcap, P.hcap);
     if (rc) return rc;
+    const uint32_t esz = P.wide ? 2u : 1u;
+    const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;
+    const uint32_t rg = (uint32_t)max_len + 1u;
+    const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
+    if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * (rb + rs + 4 * (size_t)rg) + 256))) return rc;
+    uint8_t *wr = (uint8_t *)ix->d_wrows;
     SearchArgs A;
     A.fwd = RankDir{ix->blk[0], ix->isa0};
     A.rev = RankDir{ix->blk[1], ix->risa0};
@@ -705,14 +874,37 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     memcpy(A.C, ix->C, sizeof A.C);
     A.regimes = d_regimes; A.bmap = d_bmap; A.jobs = d_jobs; A.job_list = d_list; A.n_jobs = n; A.codes = d_codes;
     A.n_aln = d_n; A.flags = d_fl; A.hit_off = d_ho; A.hits = d_hits; A.hit_cap = hit_cap; A.ctr = d_ctr;
-    A.wg = reinterpret_cast<uint32_t *>(S.width); A.pool = S.pool; A.nxt = S.nxt; A.hbuf = S.hbuf;
-    A.wcap = (uint32_t)S.wcap * 2; A.pcap = (uint32_t)S.pcap; A.hcap = (uint32_t)S.hcap;
+    A.wb = wr; A.ws = wr + rows * rb; A.wg = reinterpret_cast<uint32_t *>(wr + rows * (rb + rs));
+    A.rb = rb; A.rs = rs; A.rg = rg;
+    A.pool = S.pool; A.nxt = S.nxt; A.hbuf = S.hbuf;
+    A.pcap = (uint32_t)S.pcap; A.hcap = (uint32_t)S.hcap;
     A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
     HSA_HIP(hipMemsetAsync(d_ctr, 0, 8 * sizeof(unsigned long long), st));
-    if (P.nb <= 64) hipLaunchKernelGGL(k_search<1>, dim3((unsigned)P.blocks), dim3(BLOCK), P.lds, st, A);
-    else hipLaunchKernelGGL(k_search<2>, dim3((unsigned)P.blocks), dim3(BLOCK), P.lds, st, A);
+    size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
+    if (wblocks < 1) wblocks = 1;
+    if (P.wide) hipLaunchKernelGGL(k_widths<uint16_t>, dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
+    else hipLaunchKernelGGL(k_widths<uint8_t>, dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
+    HSA_HIP(hipGetLastError());
+    if (ix->evm) HSA_HIP(hipEventRecord(ix->evm, st));
+    if (P.wide) launch_search<uint16_t>(P, A, st);
+    else launch_search<uint8_t>(P, A, st);
     HSA_HIP(hipGetLastError());
     return 0;
+}
+
+static bool any_gaps(const hsa_regime_t *rg, int n)
+{
+    for (int r = 0; r < n; ++r)
+        if (rg[r].max_gapo > 0) return true;
+    return false;
+}
+
+// 16-bit pruning elements when a bid may be compared with a bound above 14 (WFmt).
+static bool need_wide(const hsa_regime_t *rg, int n)
+{
+    for (int r = 0; r < n; ++r)
+        if (rg[r].max_diff > 14 || rg[r].max_seed_diff > 14) return true;
+    return false;
 }
 
 static int jobs_limits(const hsa_job_t *jobs, int n, int &max_len, int &max_seed)
@@ -791,10 +983,12 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
     unsigned long long *d_ctr = (unsigned long long *)ix->d_ctr;
 
     LaunchPlan P;
-    if ((rc = plan_launch(ix, n_jobs, max_len, max_seed, nb, false, P))) return rc;
+    const bool gaps = any_gaps(regimes, n_regimes);
+    const bool wide = need_wide(regimes, n_regimes);
+    if ((rc = plan_launch(ix, n_jobs, max_len, max_seed, nb, gaps, wide, false, P))) return rc;
     HSA_HIP(hipEventRecord(ix->ev0, st));
     if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs), nullptr, n_jobs,
-                          (const uint8_t *)(din + o_codes), d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, st)))
+                          max_len, max_seed, (const uint8_t *)(din + o_codes), d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, st)))
         return rc;
     HSA_HIP(hipEventRecord(ix->ev1, st));
     unsigned long long ctr[8];
@@ -822,7 +1016,7 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
         if (n_over == 0) { free(list); break; }
         if (stats) stats->overflow_reruns += n_over;
         LaunchPlan B;
-        if ((rc = plan_launch(ix, n_over, max_len, max_seed, nb, true, B))) { free(list); free(h); return rc; }
+        if ((rc = plan_launch(ix, n_over, max_len, max_seed, nb, gaps, wide, true, B))) { free(list); free(h); return rc; }
         uint64_t cap2 = (uint64_t)n_over * 256 * (round + 1) + 65536;
         void *d2 = nullptr;
         size_t o2_fl = ((size_t)n_jobs * 4 + 255) / 256 * 256;
@@ -832,7 +1026,8 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
         char *c2 = (char *)d2;
         HSA_HIP(hipEventRecord(ix->ev0, st));
         if ((rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs),
-                              (const int32_t *)(din + o_list), n_over, (const uint8_t *)(din + o_codes), (int32_t *)c2,
+                              (const int32_t *)(din + o_list), n_over, max_len, max_seed,
+                              (const uint8_t *)(din + o_codes), (int32_t *)c2,
                               (uint32_t *)(c2 + o2_fl), (uint64_t *)(c2 + o2_ho), (uint32_t *)(c2 + o2_hits), cap2,
                               d_ctr, st))) {
             free(list); free(h); (void)hipFree(d2); return rc;
@@ -886,8 +1081,22 @@ extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, i
     int nb = 0;
     if ((rc = stage_regimes(ix, regimes, n_regimes, (char *)ix->d_in, nb, st, before != ix->d_in))) return rc;
     LaunchPlan P;
-    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, false, P))) return rc;
-    return launch_pass(ix, P, ix->main, (const hsa_regime_t *)ix->d_in, (const uint8_t *)ix->d_in + 256, b->d_jobs,
-                       nullptr, b->n_jobs, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap,
-                       (unsigned long long *)b->d_counters, st);
+    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, any_gaps(regimes, n_regimes),
+                          need_wide(regimes, n_regimes), false, P)))
+        return rc;
+    HSA_HIP(hipEventRecord(ix->ev0, st));
+    if ((rc = launch_pass(ix, P, ix->main, (const hsa_regime_t *)ix->d_in, (const uint8_t *)ix->d_in + 256, b->d_jobs,
+                          nullptr, b->n_jobs, b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags,
+                          b->d_hit_off, b->d_hits, b->hit_cap, (unsigned long long *)b->d_counters, st)))
+        return rc;
+    HSA_HIP(hipEventRecord(ix->ev1, st));
+    return 0;
+}
+
+extern "C" int hsa_last_pass_ms(hsa_index_t *ix, float *widths_ms, float *search_ms)
+{
+    HSA_HIP(hipEventSynchronize(ix->ev1));
+    HSA_HIP(hipEventElapsedTime(widths_ms, ix->ev0, ix->evm));
+    HSA_HIP(hipEventElapsedTime(search_ms, ix->evm, ix->ev1));
+    return 0;
 }

@@ -14,7 +14,8 @@
  *   hsa_width_batch    -- bwt_cal_width type 1 (bwtaln.c:73-98).
  *   hsa_search_batch   -- the per-read loop of bwa_cal_sa_reg_gap (bwtaln.c:303-373):
  *                         rc strand then forward strand, bwt_cal_width x2 and
- *                         bwt_match_gap (bwtgap.c:118-331) per strand.
+ *                         bwt_match_gap (bwtgap.c:118-331) per strand (two kernels:
+ *                         the widths of every read and strand, then the searches).
  *
  * Errors: every call returns 0 on success or a negative HSA_E* code and leaves a
  * message readable with hsa_last_error().  The library never falls back to a CPU
@@ -113,11 +114,15 @@ typedef struct {
     const uint8_t *d_codes;
     int32_t *d_n_aln; uint32_t *d_flags; uint64_t *d_hit_off;
     uint32_t *d_hits; uint64_t hit_cap;
-    uint64_t *d_counters;         /* >= 8 u64 of device scratch, zeroed by the call */
+    uint64_t *d_counters;         /* >= 8 u64 of device scratch, zeroed by the call: [1] hits, [2] rank
+                                     queries, [3] 64-B blocks fetched, [4] pops, [7] width rank queries */
     int32_t max_len, max_seed;    /* longest read, longest seed among the jobs */
 } hsa_device_batch_t;
 int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes,
                       const hsa_device_batch_t *b, void *stream);
+/* Device time of the two kernels of the last pass on this index (k_widths, then
+ * k_search); waits for that pass to finish. */
+int hsa_last_pass_ms(hsa_index_t *ix, float *widths_ms, float *search_ms);
 /* Kernel geometry/capacity knobs (0 = default). */
 int hsa_configure(int waves_per_cu, int pool_entries, int hit_cap);
 
