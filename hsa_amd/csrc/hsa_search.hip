@@ -47,6 +47,9 @@
 #define NIL16 0xFFFFu
 #define BLOCK 256
 #define MAXB 128          // buckets per regime (and score table length)
+#ifndef HSA_PREFETCH
+#define HSA_PREFETCH 0    // keep the next pool pop loaded ahead (costs 5 VGPRs)
+#endif
 
 enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT };
 
@@ -292,31 +295,38 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
     // (w * cap + e) * 64 + l, so one wave's accesses stay inside one small region
     // (few pages) and lanes at equal e coalesce
     const size_t wv = gid >> 6;
-#define WG(p) wgrow[(uint32_t)(p) * 64]
 #define POOL(s) a.pool[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
 #define NXT(s) a.nxt[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
 #define HB(i) a.hbuf[(wv * a.hcap * 9 + (uint32_t)(i)) * 64 + lane]
 #define HEAD(b) s_heads[(uint32_t)(b) * BLOCK + tid]
-#define WB(p) s_wb[(uint32_t)(p) * BLOCK + tid]
-#define WS(p) s_ws[(uint32_t)(p) * BLOCK + tid]
+    // pruning elements in LDS, word-interleaved: the word holding elements
+    // [EPW*q, EPW*q + EPW) of a lane is word q * BLOCK + tid, so every lane reads its
+    // own bank whatever position it is at, and a row copies in one store per word
+#define WB(p) s_wb[(((uint32_t)(p) / F::EPW) * BLOCK + tid) * F::EPW + (uint32_t)(p) % F::EPW]
+#define WS(p) s_ws[(((uint32_t)(p) / F::EPW) * BLOCK + tid) * F::EPW + (uint32_t)(p) % F::EPW]
 #define RG(f) (s_reg[C_REG(ctl)].f)
 
-    // ---- persistent per-lane state (~30 registers)
+    // ---- persistent per-lane state
     uint32_t ctl = PH_IDLE;        // control word (C_* accessors)
-    int job = -1;
     uint32_t qpos = 0;             // position of the read in the job list (width row = qpos * 2 + strand)
     uint32_t pen = 0;              // s_mm | s_gapo << 10 | s_gape << 20
     uint32_t rmode = 0;            // mode | max_gapo << 8 | max_gape << 16
     uint32_t pos = 0;              // exact tail: next position
     uint32_t ik = 0, il = 0;       // exact-tail interval
     uint32_t aux = 0;              // exact tail: rev_l
-    uint32_t *wgrow = nullptr;     // full widths of the current strand (HBM)
     int opt_max_diff = 0, max_diff = 0, best_score = 0, best_cnt = 0, n_aln = 0, n_entries = 0;
     uint32_t pool_top = 0;
     BMask<MW> mask;
-    uint4 vt = make_uint4(0, 0, 0, 0);
-    uint4 e = make_uint4(0, 0, 0, 0);    // current entry (k, l, rev_k, meta)
-    uint32_t st_q = 0, st_b = 0, st_p = 0;
+    // the current entry (k, l, rev_k, meta); between an expansion and the next pop
+    // it holds the virtual top when C_VT is set (the last child pushed, when it is
+    // the next pop: it never goes to the pool)
+    uint4 e = make_uint4(0, 0, 0, 0);
+#if HSA_PREFETCH
+    uint4 pf = make_uint4(0, 0, 0, 0);   // POOL(HEAD(lowest bucket)): the next pool pop, loaded ahead
+    uint32_t pfl = NIL16;                //   and its NXT link
+#endif
+    uint32_t st_p = 0;
+    uint64_t st_q = 0, st_b = 0;          // wave-uniform (ballot counts)
 #ifdef HSA_DIAG
     uint32_t dc[16] = {0};
     uint64_t tsec[4] = {0, 0, 0, 0};
@@ -334,13 +344,24 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 
     // base of the current strand's sequence at p (from the LDS element, see WFmt)
     auto getc = [&](int p) -> uint32_t { return F::code(WB(p)); };
+    // stack bucket of an entry: dense index of its score (bwtgap.c:46-75)
+    auto bucket_of = [&](uint32_t m) -> int {
+        const int sc = SCORE(M_MM(m), M_GO(m), M_GE(m));
+        return (uint32_t)sc < MAXB ? (int)s_lds[C_REG(ctl) * MAXB + sc] : 0xFF;
+    };
+    // push to the pool (gap_push, bwtgap.c:46-75); pf/pfl keep the head entry of the
+    // lowest non-empty bucket (the next pool pop) so that pops never wait for a load
     auto flush = [&](uint4 v, int b) {
         if (pool_top >= a.pcap || (uint32_t)b >= a.nb) { ctl |= 1u << 8; return; }
         DC(8);
         const uint32_t slot = pool_top++;
         POOL(slot) = v;
-        NXT(slot) = mask.test(b) ? HEAD(b) : (uint16_t)NIL16;
+        const uint32_t old = mask.test(b) ? (uint32_t)HEAD(b) : NIL16;
+        NXT(slot) = (uint16_t)old;
         HEAD(b) = (uint16_t)slot;
+#if HSA_PREFETCH
+        if (b <= mask.lowest()) { pf = v; pfl = old; }
+#endif
         mask.set(b);
     };
     auto start_search = [&]() {
@@ -348,39 +369,34 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         max_diff = opt_max_diff;
         best_cnt = 0; n_aln = 0;
         mask.clear(); pool_top = 0;
-        vt = make_uint4(0, a.T, 0, meta_pack((uint32_t)C_LEN(ctl), ST_M, 0, 0, 0, 0));   // root (bwtgap.c:142)
+        e = make_uint4(0, a.T, 0, meta_pack((uint32_t)C_LEN(ctl), ST_M, 0, 0, 0, 0));   // root (bwtgap.c:142)
         ctl |= 1u << 6;
         n_entries = 1;
         SET_PH(ctl, PH_POP);
     };
-    // copy the strand's pruning bytes (k_widths) into the lane's LDS columns, then
+    // width row of the current strand: row qpos * 2 + strand, 64 rows interleaved
+    auto row_base = [&](uint32_t cap_words) -> size_t {
+        const uint32_t r = qpos * 2u + C_STRAND(ctl);
+        return (size_t)(r >> 6) * cap_words * 64 + (r & 63u);
+    };
+    // copy the strand's pruning elements (k_widths) into the lane's LDS columns, then
     // start bwt_match_gap (bwtgap.c:141-142)
     auto start_strand = [&]() {
-        const uint32_t r = qpos * 2u + C_STRAND(ctl);
-        const size_t rb = r >> 6, rl = r & 63u;
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.wb) + rb * (a.rb / 4) * 64 + rl;
-        const int len = C_LEN(ctl);
-        for (int q = 0; q <= len; q += F::EPW) {
-            const uint32_t v = src[(q / F::EPW) * 64];
-#pragma unroll
-            for (int b = 0; b < (int)F::EPW; ++b)
-                if (q + b <= len) WB(q + b) = (WT)(v >> (F::EB * b));
-        }
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.wb) + row_base(a.rb / 4);
+        uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + tid;
+        const int nwb = C_LEN(ctl) / (int)F::EPW + 1;
+        for (int q = 0; q < nwb; ++q) db[q * BLOCK] = src[q * 64];
         if (C_SEED(ctl)) {
-            const uint32_t *ss = reinterpret_cast<const uint32_t *>(a.ws) + rb * (a.rs / 4) * 64 + rl;
-            const int sl = C_SLEN(ctl);
-            for (int q = 0; q <= sl; q += F::EPW) {
-                const uint32_t v = ss[(q / F::EPW) * 64];
-#pragma unroll
-                for (int b = 0; b < (int)F::EPW; ++b)
-                    if (q + b <= sl) WS(q + b) = (WT)(v >> (F::EB * b));
-            }
+            const uint32_t *ss = reinterpret_cast<const uint32_t *>(a.ws) + row_base(a.rs / 4);
+            uint32_t *const ds = reinterpret_cast<uint32_t *>(s_ws) + tid;
+            const int nws = C_SLEN(ctl) / (int)F::EPW + 1;
+            for (int q = 0; q < nws; ++q) ds[q * BLOCK] = ss[q * 64];
         }
-        wgrow = a.wg + rb * a.rg * 64 + rl;
         DC(15);
         start_search();
     };
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
+        const int job = a.job_list ? a.job_list[qpos] : (int)qpos;
         a.n_aln[job] = na;
         a.flags[job] = fl;
         a.hit_off[job] = ho;
@@ -431,13 +447,15 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         if (add) {
             if ((uint32_t)n_aln >= a.hcap) { ctl |= 1u << 8; return false; }
             // gap_shadow (bwtgap.c:94-105) on width_back[0, last_diff_pos), then the
-            // pruning bytes of those positions (eq bit of p needs w[p+1])
+            // pruning elements of those positions (eq bit of p needs w[p+1])
             const uint32_t x = l - k + 1u;
             const int ldp = M_ISD(m) ? M_I(m) : 0;
             if (ldp > 0) {
 #ifdef HSA_DIAG
                 DC(13); dc[14] += (uint32_t)ldp;
 #endif
+                uint32_t *const wg = a.wg + row_base(a.rg);
+#define WG(p) wg[(uint32_t)(p) * 64]
                 uint32_t jj = 0;
                 for (int p = 0; p < ldp; ++p) {
                     uint32_t w = WG(p);
@@ -450,6 +468,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                     WB(p) = (WT)((WB(p) & ~F::EQ) | (w == wnext ? F::EQ : 0u));
                     wnext = w;
                 }
+#undef WG
             }
             HB(n_aln * 9 + 0) = (uint32_t)M_MM(m) | (uint32_t)M_GO(m) << 16 | (uint32_t)M_GE(m) << 24;
             HB(n_aln * 9 + 1) = k; HB(n_aln * 9 + 2) = l; HB(n_aln * 9 + 3) = rk; HB(n_aln * 9 + 4) = rl;
@@ -482,8 +501,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
                     if (j < (unsigned long long)a.n_jobs) {
                         qpos = (uint32_t)j;
-                        job = a.job_list ? a.job_list[j] : (int)j;
-                        const hsa_job_t J = a.jobs[job];
+                        const hsa_job_t J = a.jobs[a.job_list ? a.job_list[j] : (int)j];
                         opt_max_diff = J.max_diff;
                         const uint32_t len = J.len;
                         const uint32_t has_seed = (int)len > J.seed_len;
@@ -531,15 +549,29 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             if (n_entries == 0 || n_entries > RG(max_entries)) { end_strand(); continue; }
             if (C_VT(ctl)) {
                 DC(3);
-                e = vt; ctl &= ~(1u << 6);
+                ctl &= ~(1u << 6);                                        // e already holds it
             } else {
                 DC(4);
+                // pop the prefetched head of the lowest bucket, then prefetch the next
+                // one (used at the next pool pop, iterations later)
                 const int b = mask.lowest();
+#if HSA_PREFETCH
+                e = pf;
+                uint32_t nh = pfl;
+                if (nh == NIL16) {
+                    mask.reset(b);
+                    nh = mask.any() ? (uint32_t)HEAD(mask.lowest()) : NIL16;
+                } else {
+                    HEAD(b) = (uint16_t)nh;
+                }
+                if (nh != NIL16) { pf = POOL(nh); pfl = NXT(nh); }
+#else
                 const uint32_t slot = HEAD(b);
                 e = POOL(slot);
                 const uint16_t nx = NXT(slot);
                 if (nx == NIL16) mask.reset(b);
                 else HEAD(b) = nx;
+#endif
             }
             --n_entries;
             ++st_p;
@@ -570,18 +602,18 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 #endif
         // ---------------- (C) the rank step
         uint32_t oa[4], ob[4];
+        const uint64_t rq = __ballot(req);
 #ifdef HSA_DIAG
         {
-            const uint64_t rb = __ballot(req);
-            if (lane == 0) dc[6] += (uint32_t)__popcll(rb);
+            if (lane == 0) dc[6] += (uint32_t)__popcll(rq);
             const uint32_t ph0 = C_PH(ctl);
             if (req) DC(ph0 == PH_EXACT ? 1 : 2);
         }
 #endif
-        if (req) {
-            st_b += hsa_occ_pair(a.fwd, rp1, rp2, oa, ob);
-            st_q += 2;
-        }
+        uint32_t two = 0;
+        if (req) two = hsa_occ_pair(a.fwd, rp1, rp2, oa, ob) - 1u;
+        st_q += 2u * (uint64_t)__popcll(rq);
+        st_b += (uint64_t)__popcll(rq) + (uint64_t)__popcll(__ballot(two));
 
 #ifdef HSA_DIAG
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -609,25 +641,26 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                 if (!on_hit(hk, hl, hrk, hrl) && !C_OVF(ctl)) end_strand();
             }
         } else if (req && ph == PH_EXPAND) {
-            // children of the bidirectional step (2BWT-Interface.c:235-272)
+            // children of the bidirectional step (2BWT-Interface.c:235-272), in place:
+            // oa -> k, ob -> l of child c; srk = rev_k
             const uint32_t m = e.w;
             const uint32_t ek = e.x, el = e.y, erk = e.z, erl = erk + (el - ek);
             const int i = M_I(m) - 1;                                    // --i (bwtgap.c:245)
             const int est = M_ST(m), emm = M_MM(m), ego = M_GO(m), ege = M_GE(m);
             const int em = m_of(m);
             const int len = C_LEN(ctl);
-            uint32_t sk[4], sl[4], srk[4];
+            uint32_t srk[4];
             {
                 uint32_t oc = 0;
 #pragma unroll
                 for (int c = 3; c >= 0; --c) {
-                    sk[c] = a.C[c] + oa[c] + 1u;
-                    sl[c] = a.C[c] + ob[c];
-                    srk[c] = (erl - oc) - (sl[c] - sk[c]);
-                    oc += ob[c] - oa[c];
+                    const uint32_t d = ob[c] - oa[c];
+                    oa[c] = a.C[c] + oa[c] + 1u;
+                    ob[c] = a.C[c] + ob[c];
+                    srk[c] = (erl - oc) - (ob[c] - oa[c]);
+                    oc += d;
                 }
             }
-            const uint32_t occ = el - ek + 1u;
             int allow_diff = 1, allow_M = 1;
             if (i > 0) {
                 // width[i-1].bid, width[i].bid and w[i-1] == w[i] (bwtgap.c:256-258)
@@ -645,57 +678,65 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                     else if (c1 == ems - 1 && c0 == ems - 1 && (s1 & F::EQ)) allow_M = 0;
                 }
             }
-            // pushes (bwtgap.c:267-325): all but the last go to the pool at once;
-            // the last stays pending and becomes the virtual top if it is the next pop
-            int pend = 0, pend_b = 0;
-            uint4 pendv = make_uint4(0, 0, 0, 0);
-            auto push = [&](int pi, uint32_t k, uint32_t l, uint32_t rk, int mm, int go, int ge, int st, int isd) {
-                if (pend) flush(pendv, pend_b);
-                pendv = make_uint4(k, l, rk, meta_pack((uint32_t)pi, (uint32_t)st, (uint32_t)isd, (uint32_t)mm,
-                                                       (uint32_t)go, (uint32_t)ge));
-                const int sc = SCORE(mm, go, ge);
-                pend_b = (uint32_t)sc < MAXB ? (int)s_lds[C_REG(ctl) * MAXB + sc] : 0xFF;
-                pend = 1;
-                ++n_entries;
-            };
-            const int tmp = (R_MODE & MODE_LOGGAP) ? int_log2((uint32_t)(ege + ego)) / 2 + 1 : ego + ege;
+            // The pushes of bwtgap.c:267-325 as a candidate mask in push order:
+            // bit 0 insertion, bits 1-4 deletion with child j = bit-1, bits 5-8
+            // match/mismatch with child (seq[i] + bit-4) & 3.  All but the last go to the
+            // pool in order; the last becomes the virtual top when it is the next pop.
+            const uint32_t sc = getc(i);
+            uint32_t cand = 0;
             if (GAPS && allow_diff && (R_MAXGO > 0 || ego > 0)) {
                 const int ies = RG(indel_end_skip);
+                const int tmp = (R_MODE & MODE_LOGGAP) ? int_log2((uint32_t)(ege + ego)) / 2 + 1 : ego + ege;
                 if (i >= ies + tmp && len - i >= ies + tmp) {
+                    uint32_t dm = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) dm |= (oa[j] <= ob[j] ? 1u : 0u) << j;
+                    const uint32_t occ = el - ek + 1u;
                     if (est == ST_M) {
-                        if (ego < R_MAXGO) {
-                            push(i, ek, el, erk, emm, ego + 1, ege, ST_I, 1);
-#pragma unroll
-                            for (int j = 0; j < 4; ++j)
-                                if (sk[j] <= sl[j]) push(i + 1, sk[j], sl[j], srk[j], emm, ego + 1, ege, ST_D, 1);
-                        }
+                        if (ego < R_MAXGO) cand = 1u | dm << 1;
                     } else if (est == ST_I) {
-                        if (ege < R_MAXGE) push(i, ek, el, erk, emm, ego, ege + 1, ST_I, 1);
-                    } else if (est == ST_D) {
-                        if (ege < R_MAXGE && (ege + ego < max_diff || occ < (uint32_t)RG(max_del_occ))) {
-#pragma unroll
-                            for (int j = 0; j < 4; ++j)
-                                if (sk[j] <= sl[j]) push(i + 1, sk[j], sl[j], srk[j], emm, ego, ege + 1, ST_D, 1);
-                        }
+                        if (ege < R_MAXGE) cand = 1u;
+                    } else if (ege < R_MAXGE && (ege + ego < max_diff || occ < (uint32_t)RG(max_del_occ))) {
+                        cand = dm << 1;
                     }
                 }
             }
-            const uint32_t sc = getc(i);
             if (allow_diff && allow_M) {
 #pragma unroll
                 for (int j = 1; j <= 4; ++j) {
                     const uint32_t c = (sc + (uint32_t)j) & 3u;
-                    const int is_mm = (j != 4 || sc > 3);
-                    const uint32_t ck = pick4(sk, c), cl = pick4(sl, c);
-                    if (ck <= cl) push(i, ck, cl, pick4(srk, c), emm + is_mm, ego, ege, ST_M, is_mm);
+                    cand |= (pick4(oa, c) <= pick4(ob, c) ? 1u : 0u) << (4 + j);
                 }
             } else if (sc < 4) {
-                const uint32_t ck = pick4(sk, sc), cl = pick4(sl, sc);
-                if (ck <= cl) push(i, ck, cl, pick4(srk, sc), emm, ego, ege, ST_M, 0);
+                cand |= (pick4(oa, sc) <= pick4(ob, sc) ? 1u : 0u) << 8;    // == bit 8: c = sc, no mismatch
             }
-            if (pend) {
-                if (pend_b <= mask.lowest()) { vt = pendv; ctl |= 1u << 6; }
-                else flush(pendv, pend_b);
+            // entry of candidate bit b
+            auto entry = [&](uint32_t b) -> uint4 {
+                const bool ins = GAPS && b == 0, del = GAPS && b >= 1 && b <= 4;
+                const uint32_t c = del ? b - 1u : (sc + b - 4u) & 3u;
+                const uint32_t is_mm = (b != 8u || sc > 3) ? 1u : 0u;
+                uint32_t k = pick4(oa, c), l = pick4(ob, c), rk = pick4(srk, c);
+                uint32_t meta;
+                if (GAPS && (ins || del)) {
+                    if (ins) { k = ek; l = el; rk = erk; }
+                    const uint32_t go = (uint32_t)ego + (est == ST_M), ge = (uint32_t)ege + (est != ST_M);
+                    meta = meta_pack((uint32_t)(del ? i + 1 : i), ins ? ST_I : ST_D, 1u, (uint32_t)emm, go, ge);
+                } else {
+                    meta = meta_pack((uint32_t)i, ST_M, is_mm, (uint32_t)emm + is_mm, (uint32_t)ego, (uint32_t)ege);
+                }
+                return make_uint4(k, l, rk, meta);
+            };
+            if (cand) {
+                const uint32_t last = 31u - (uint32_t)__clz(cand);
+                n_entries += __popc(cand);
+                for (uint32_t rest = cand & ~(1u << last); rest; rest &= rest - 1u) {
+                    const uint4 v = entry((uint32_t)__ffs(rest) - 1u);
+                    flush(v, bucket_of(v.w));
+                }
+                const uint4 v = entry(last);
+                const int bk = bucket_of(v.w);
+                if (bk <= mask.lowest()) { e = v; ctl |= 1u << 6; }
+                else flush(v, bk);
             }
             SET_PH(ctl, PH_POP);
         }
@@ -710,21 +751,20 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         g_diag[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memtime();
         g_diag[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
     }
-#endif
-    // statistics
-#ifdef HSA_DIAG
     for (int i = 0; i < 16; ++i)
         if (i < 9 || i > 12) atomicAdd(&g_dctr[i], (unsigned long long)dc[i]);
     if (lane == 0)
         for (int i = 0; i < 4; ++i) atomicAdd(&g_dctr[9 + i], (unsigned long long)tsec[i]);
 #endif
-    atomicAdd(&a.ctr[2], (unsigned long long)st_q);
-    atomicAdd(&a.ctr[3], (unsigned long long)st_b);
+    // statistics
+    if (lane == 0) {
+        atomicAdd(&a.ctr[2], (unsigned long long)st_q);
+        atomicAdd(&a.ctr[3], (unsigned long long)st_b);
+    }
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);
 #undef HEAD
 #undef WB
 #undef WS
-#undef WG
 #undef POOL
 #undef NXT
 #undef HB
@@ -803,8 +843,9 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     const uint32_t esz = wide ? 2u : 1u;
     P.off_heads = 2 * MAXB + 128;   // score tables, then the two regimes
     P.off_wb = P.off_heads + (uint32_t)nb * BLOCK * 2;
-    P.off_ws = P.off_wb + (uint32_t)(max_len + 1) * BLOCK * esz;
-    P.lds = ((size_t)P.off_ws + (size_t)(max_seed + 1) * BLOCK * esz + 15) / 16 * 16;
+    const uint32_t epw = 4u / esz;                       // elements per LDS word (WFmt::EPW)
+    P.off_ws = P.off_wb + ((uint32_t)max_len / epw + 1u) * BLOCK * 4u;
+    P.lds = ((size_t)P.off_ws + ((size_t)max_seed / epw + 1u) * BLOCK * 4u + 15) / 16 * 16;
     if (P.lds > 160 * 1024) { hsa_set_error("reads too long for the LDS budget (%zu bytes)", P.lds); return HSA_E_ARG; }
     // Resident workgroups per CU, from gfx950's own limits: 160 KiB of LDS per CU,
     // and __launch_bounds__(BLOCK, 4) caps VGPRs so 4 workgroups of 4 waves fit.
