@@ -3,8 +3,8 @@
 // The reference keeps, per BWT direction, a 2-bit code array plus two sampled
 // Occ tables (occValue every 256 chars as 16-bit pairs, occValueMajor every 65 536;
 // BWT.c:1018-1059) and answers a rank with two dependent-ish loads and an SSE
-// popcount (BWT.c:532-679).  Here one 64-byte block carries both the absolute
-// counts and the 192 codes they cover, so one rank query = one 64-byte fetch.
+// popcount (BWT.c:532-679).  Here one 16-byte block carries the absolute counts
+// and the 16 codes they precede (hsa_device.h), so one rank query = one load.
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -112,68 +112,50 @@ struct U4Plus {
     }
 };
 
-// full-block counts (valid characters only) for the exclusive scan, and the
-// counts of the block's first 96 characters with padding past T counted as 'A'
-__global__ void k_block_counts(const uint32_t *__restrict__ code, size_t nwords, uint32_t T, size_t nblk,
-                               U4 *__restrict__ cnt, U4 *__restrict__ half)
-{
-    size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nblk) return;
-    uint32_t n1 = 0, n2 = 0, n3 = 0, h1 = 0, h2 = 0, h3 = 0;
-    for (int q = 0; q < 12; ++q) {
-        size_t wi = b * 12 + q;
-        uint32_t v = wi < nwords ? code[wi] : 0u;
-        uint32_t lo = v & 0x55555555u, hi = (v >> 1) & 0x55555555u;
-        uint32_t t3 = __popc(lo & hi), t1 = __popc(lo) - t3, t2 = __popc(hi) - t3;
-        n3 += t3; n1 += t1; n2 += t2;
-        if (q == 5) { h1 = n1; h2 = n2; h3 = n3; }
+// Counts of A, C, G among the valid characters of code word b (the last word may be
+// partial: its padding codes are 0 but are not characters, so A = valid - C - G - T).
+struct WordCounts {
+    const uint32_t *code;
+    size_t nwords;
+    uint32_t T;
+    __host__ __device__ U4 operator()(size_t b) const
+    {
+        const uint32_t v = b < nwords ? code[b] : 0u;
+        const uint32_t lo = v & 0x55555555u, hi = (v >> 1) & 0x55555555u;
+        const uint32_t t3 = __popc(lo & hi), t1 = __popc(lo) - t3, t2 = __popc(hi) - t3;
+        const uint64_t s = (uint64_t)b * HSA_BLK_CHARS;
+        const uint32_t valid = s >= T ? 0u : (uint32_t)((T - s) < HSA_BLK_CHARS ? (T - s) : HSA_BLK_CHARS);
+        return U4{valid - t1 - t2 - t3, t1, t2, 0u};
     }
-    uint64_t s = (uint64_t)b * HSA_BLK_CHARS;
-    uint32_t valid = s >= T ? 0u : (uint32_t)((T - s) < HSA_BLK_CHARS ? (T - s) : HSA_BLK_CHARS);
-    cnt[b] = U4{valid - n1 - n2 - n3, n1, n2, n3};
-    half[b] = U4{96u - h1 - h2 - h3, h1, h2, h3};
-}
+};
 
-__global__ void k_block_write(const uint32_t *__restrict__ code, size_t nwords, size_t nblk,
-                              const U4 *__restrict__ pre, const U4 *__restrict__ half, uint4 *__restrict__ blk)
+// block b = (Occ A, C, G over [0, 16b) from the scan, code word b)
+__global__ void k_block_codes(const uint32_t *__restrict__ code, size_t nwords, size_t nblk, uint4 *__restrict__ blk)
 {
-    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // one thread per dword of output
-    size_t b = t >> 4, d = t & 15;
+    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nblk) return;
-    uint32_t v;
-    if (d < 4) {
-        U4 p = pre[b], h = half[b];
-        v = d == 0 ? p.a + h.a : d == 1 ? p.b + h.b : d == 2 ? p.c + h.c : p.d + h.d;
-    } else {
-        size_t wi = b * 12 + (d - 4);
-        v = wi < nwords ? code[wi] : 0u;
-    }
-    reinterpret_cast<uint32_t *>(blk)[t] = v;
+    blk[b].w = b < nwords ? code[b] : 0u;
 }
 
 static int build_blocks(hsa_index *ix, int dir, uint32_t T, const uint32_t *d_code_lsb, hipStream_t st)
 {
-    size_t nwords = ((size_t)T + 15) / 16;
-    size_t nblk = (size_t)T / HSA_BLK_CHARS + 2;
-    U4 *cnt = nullptr, *pre = nullptr, *half = nullptr;
+    const size_t nwords = ((size_t)T + 15) / 16;
+    const size_t nblk = (size_t)T / HSA_BLK_CHARS + 2;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
-    HSA_HIP(hipMalloc(&cnt, nblk * sizeof(U4)));
-    HSA_HIP(hipMalloc(&pre, nblk * sizeof(U4)));
-    HSA_HIP(hipMalloc(&half, nblk * sizeof(U4)));
-    HSA_HIP(hipMalloc(&ix->blk[dir], nblk * 64));
+    HSA_HIP(hipMalloc(&ix->blk[dir], nblk * 16));
     ix->nblk[dir] = nblk;
-    k_block_counts<<<(unsigned)((nblk + 255) / 256), 256, 0, st>>>(d_code_lsb, nwords, T, nblk, cnt, half);
-    HSA_HIP(hipGetLastError());
-    U4 zero{0, 0, 0, 0};
-    HSA_HIP(rocprim::exclusive_scan(tmp, tmp_bytes, cnt, pre, zero, nblk, U4Plus(), st));
+    auto in = rocprim::make_transform_iterator(rocprim::make_counting_iterator<size_t>(0),
+                                               WordCounts{d_code_lsb, nwords, T});
+    U4 *out = reinterpret_cast<U4 *>(ix->blk[dir]);
+    const U4 zero{0, 0, 0, 0};
+    HSA_HIP(rocprim::exclusive_scan(tmp, tmp_bytes, in, out, zero, nblk, U4Plus(), st));
     HSA_HIP(hipMalloc(&tmp, tmp_bytes ? tmp_bytes : 16));
-    HSA_HIP(rocprim::exclusive_scan(tmp, tmp_bytes, cnt, pre, zero, nblk, U4Plus(), st));
-    size_t nthr = nblk * 16;
-    k_block_write<<<(unsigned)((nthr + 255) / 256), 256, 0, st>>>(d_code_lsb, nwords, nblk, pre, half, ix->blk[dir]);
+    HSA_HIP(rocprim::exclusive_scan(tmp, tmp_bytes, in, out, zero, nblk, U4Plus(), st));
+    k_block_codes<<<(unsigned)((nblk + 255) / 256), 256, 0, st>>>(d_code_lsb, nwords, nblk, ix->blk[dir]);
     HSA_HIP(hipGetLastError());
     HSA_HIP(hipStreamSynchronize(st));
-    (void)hipFree(tmp); (void)hipFree(cnt); (void)hipFree(pre); (void)hipFree(half);
+    (void)hipFree(tmp);
     return 0;
 }
 
@@ -256,7 +238,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     delete ix;
 }
 
-extern "C" size_t hsa_index_bytes(const hsa_index_t *ix) { return (ix->nblk[0] + ix->nblk[1]) * 64; }
+extern "C" size_t hsa_index_bytes(const hsa_index_t *ix) { return (ix->nblk[0] + ix->nblk[1]) * 16; }
 extern "C" int hsa_index_device(const hsa_index_t *ix) { return ix->device; }
 extern "C" void *hsa_index_stream(const hsa_index_t *ix) { return (void *)ix->stream; }
 

@@ -42,6 +42,7 @@ struct hsa_index {
     uint64_t *d_ctr = nullptr;
     unsigned char staged[512];          // last regime block copied to d_in (skip identical re-copies)
     int staged_valid = 0;
+    bool staged_mmb = false;            // staged regimes: bucket == n_mm (see mm_buckets)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evm = nullptr;           // between k_widths and k_search of the last pass (timing split)
 };

@@ -47,6 +47,9 @@
 #define NIL16 0xFFFFu
 #define BLOCK 256
 #define MAXB 128          // buckets per regime (and score table length)
+#ifndef HSA_CTL_LOOP
+#define HSA_CTL_LOOP 0    // 1: loop the control code until every lane needs a rank step
+#endif
 #ifndef HSA_PREFETCH
 #define HSA_PREFETCH 0    // keep the next pool pop loaded ahead (costs 5 VGPRs)
 #endif
@@ -78,6 +81,7 @@ struct SearchArgs {
     uint32_t *hbuf;
     uint32_t pcap, hcap, nb;
     uint32_t off_heads, off_wb, off_ws;   // LDS byte offsets
+    uint32_t mm_buckets;           // 1: the bucket of every score is its n_mm (no gap opens, s_mm > 0)
 };
 
 // entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
@@ -123,6 +127,15 @@ __device__ __forceinline__ int int_log2(uint32_t v)   // bwtgap.c:107-116
 }
 
 template <int MW> struct BMask;
+template <> struct BMask<0> {        // <= 32 buckets: one 32-bit word
+    uint32_t m0 = 0;
+    __device__ __forceinline__ void clear() { m0 = 0; }
+    __device__ __forceinline__ bool any() const { return m0 != 0; }
+    __device__ __forceinline__ int lowest() const { return m0 ? __ffs(m0) - 1 : (1 << 30); }
+    __device__ __forceinline__ bool test(int b) const { return (m0 >> b) & 1u; }
+    __device__ __forceinline__ void set(int b) { m0 |= 1u << b; }
+    __device__ __forceinline__ void reset(int b) { m0 &= ~(1u << b); }
+};
 template <> struct BMask<1> {
     uint64_t m0 = 0;
     __device__ __forceinline__ void clear() { m0 = 0; }
@@ -346,6 +359,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
     auto getc = [&](int p) -> uint32_t { return F::code(WB(p)); };
     // stack bucket of an entry: dense index of its score (bwtgap.c:46-75)
     auto bucket_of = [&](uint32_t m) -> int {
+        if (!GAPS && a.mm_buckets) return M_MM(m);
         const int sc = SCORE(M_MM(m), M_GO(m), M_GE(m));
         return (uint32_t)sc < MAXB ? (int)s_lds[C_REG(ctl) * MAXB + sc] : 0xFF;
     };
@@ -382,16 +396,22 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
     // copy the strand's pruning elements (k_widths) into the lane's LDS columns, then
     // start bwt_match_gap (bwtgap.c:141-142)
     auto start_strand = [&]() {
+        // LDS-DMA (global_load_lds_dword): word q of every active lane lands at
+        // word q * BLOCK + tid, which is exactly the wave's slice of the LDS layout, so
+        // the whole row is in flight at once and one wait covers it
         const uint32_t *src = reinterpret_cast<const uint32_t *>(a.wb) + row_base(a.rb / 4);
-        uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + tid;
-        const int nwb = C_LEN(ctl) / (int)F::EPW + 1;
-        for (int q = 0; q < nwb; ++q) db[q * BLOCK] = src[q * 64];
+        uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + (tid & ~63u);
+        const uint32_t nwb = a.rb / 4;                 // row capacity in words (uniform)
+        for (uint32_t q = 0; q < nwb; ++q)
+            __builtin_amdgcn_global_load_lds(src + q * 64, db + q * BLOCK, 4, 0, 0);
         if (C_SEED(ctl)) {
             const uint32_t *ss = reinterpret_cast<const uint32_t *>(a.ws) + row_base(a.rs / 4);
-            uint32_t *const ds = reinterpret_cast<uint32_t *>(s_ws) + tid;
-            const int nws = C_SLEN(ctl) / (int)F::EPW + 1;
-            for (int q = 0; q < nws; ++q) ds[q * BLOCK] = ss[q * 64];
+            uint32_t *const ds = reinterpret_cast<uint32_t *>(s_ws) + (tid & ~63u);
+            const uint32_t nws = a.rs / 4;
+            for (uint32_t q = 0; q < nws; ++q)
+                __builtin_amdgcn_global_load_lds(ss + q * 64, ds + q * BLOCK, 4, 0, 0);
         }
+        __builtin_amdgcn_s_waitcnt(0);                 // the DMA writes are visible to LDS reads
         DC(15);
         start_search();
     };
@@ -529,7 +549,14 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 #ifdef HSA_DIAG
         if (lane == 0) DC(5);
 #endif
+        // One control pass per iteration (HSA_CTL_LOOP=0): a lane whose pop needs no
+        // rank step (pruned, hit, strand change) just skips this iteration's step
+        // instead of making the whole wave run the control code again.
+#if HSA_CTL_LOOP
         while (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && !req) {
+#else
+        if (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE) do {
+#endif
 #ifdef HSA_DIAG
             { const uint64_t em = __ballot(1); if (lane == __ffsll((unsigned long long)em) - 1) DC(7); }
 #endif
@@ -596,6 +623,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             req = 1; rp1 = e.x; rp2 = e.y + 1u;
             SET_PH(ctl, PH_EXPAND);
         }
+#if !HSA_CTL_LOOP
+        while (0);
+#endif
 
 #ifdef HSA_DIAG
         TMARK(1);
@@ -826,6 +856,22 @@ static int bucket_map(const hsa_regime_t &R, uint8_t map[MAXB])
     return k;
 }
 
+// The dense bucket of a score is simply its n_mm when no gap opens exist and every
+// reachable mismatch count has its own score (k_search skips the table then).
+static bool mm_buckets(const hsa_regime_t *rg, int n, const uint8_t *bmap)
+{
+    for (int r = 0; r < n; ++r) {
+        const hsa_regime_t &R = rg[r];
+        if (R.max_gapo != 0 || R.s_mm <= 0) return false;
+        const int md = R.max_diff < 0 ? 0 : R.max_diff;
+        for (int mm = 0; mm <= md + 1; ++mm) {
+            const int sc = mm * R.s_mm;
+            if (sc >= MAXB || bmap[r * MAXB + sc] != mm) return false;
+        }
+    }
+    return true;
+}
+
 struct LaunchPlan {
     size_t lanes, blocks;
     uint32_t pcap, hcap, nb;
@@ -884,7 +930,10 @@ template <typename WT>
 static void launch_search(const LaunchPlan &P, const SearchArgs &A, hipStream_t st)
 {
     const dim3 g((unsigned)P.blocks), b(BLOCK);
-    if (P.nb <= 64) {
+    if (P.nb <= 32) {
+        if (P.gaps) hipLaunchKernelGGL((k_search<0, true, WT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<0, false, WT>), g, b, P.lds, st, A);
+    } else if (P.nb <= 64) {
         if (P.gaps) hipLaunchKernelGGL((k_search<1, true, WT>), g, b, P.lds, st, A);
         else hipLaunchKernelGGL((k_search<1, false, WT>), g, b, P.lds, st, A);
     } else {
@@ -920,6 +969,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     A.pool = S.pool; A.nxt = S.nxt; A.hbuf = S.hbuf;
     A.pcap = (uint32_t)S.pcap; A.hcap = (uint32_t)S.hcap;
     A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
+    A.mm_buckets = ix->staged_mmb ? 1u : 0u;
     HSA_HIP(hipMemsetAsync(d_ctr, 0, 8 * sizeof(unsigned long long), st));
     size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
     if (wblocks < 1) wblocks = 1;
@@ -975,6 +1025,7 @@ static int stage_regimes(hsa_index *ix, const hsa_regime_t *regimes, int n_regim
         int k = bucket_map(regimes[r], host + 256 + r * MAXB);
         nb = k > nb ? k : nb;
     }
+    ix->staged_mmb = mm_buckets(regimes, n_regimes, host + 256);
     if (!force && ix->staged_valid && memcmp(ix->staged, host, sizeof host) == 0) return 0;
     memcpy(ix->staged, host, sizeof host);
     ix->staged_valid = 1;
