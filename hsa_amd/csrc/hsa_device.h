@@ -29,10 +29,23 @@ struct RankDir {
     uint32_t isa0;
 };
 
-// Occ(p, A..T) of an already $-adjusted position p.
-__device__ __forceinline__ void hsa_occ4_raw(const uint4 *__restrict__ blk, uint32_t p, uint32_t o[4])
+#ifndef HSA_NT_RANK
+#define HSA_NT_RANK 0
+#endif
+__device__ __forceinline__ uint4 hsa_blk_load(const uint4 *__restrict__ blk, uint32_t b)
 {
-    const uint4 q = blk[p >> 4];
+#if HSA_NT_RANK
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(blk) + b);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return blk[b];
+#endif
+}
+
+// Occ(p, A..T) of an already $-adjusted position p, from its block q.
+__device__ __forceinline__ void hsa_occ4_q(const uint4 q, uint32_t p, uint32_t o[4])
+{
     const uint32_t r = p & 15u;
     const uint32_t v = q.w & ((1u << (2u * r)) - 1u);        // r <= 15: shift <= 30
     const uint32_t lo = v & 0x55555555u, hi = (v >> 1) & 0x55555555u;
@@ -44,11 +57,15 @@ __device__ __forceinline__ void hsa_occ4_raw(const uint4 *__restrict__ blk, uint
     o[3] = p - o[0] - o[1] - o[2];
 }
 
-// Occ(p, c) of an already $-adjusted position p: one popcount of the codes equal to c
-// (XOR with the complement pattern of c turns them into 0b11).
-__device__ __forceinline__ uint32_t hsa_occ1_raw(const uint4 *__restrict__ blk, uint32_t p, uint32_t c)
+__device__ __forceinline__ void hsa_occ4_raw(const uint4 *__restrict__ blk, uint32_t p, uint32_t o[4])
 {
-    const uint4 q = blk[p >> 4];
+    hsa_occ4_q(hsa_blk_load(blk, p >> 4), p, o);
+}
+
+// Occ(p, c) of an already $-adjusted position p from its block q: one popcount of the
+// codes equal to c (XOR with the complement pattern of c turns them into 0b11).
+__device__ __forceinline__ uint32_t hsa_occ1_q(const uint4 q, uint32_t p, uint32_t c)
+{
     const uint32_t r = p & 15u;
     const uint32_t x = q.w ^ ~(c * 0x55555555u);
     const uint32_t n = __popc(x & (x >> 1) & 0x55555555u & ((1u << (2u * r)) - 1u));
@@ -62,8 +79,12 @@ __device__ __forceinline__ uint32_t hsa_occ_pair(const RankDir d, uint32_t p1, u
 {
     p1 -= (p1 > d.isa0);
     p2 -= (p2 > d.isa0);
-    hsa_occ4_raw(d.blk, p1, a);
-    hsa_occ4_raw(d.blk, p2, b);
+    // a narrow interval has both ends in one block: then one load serves both
+    const uint4 q1 = hsa_blk_load(d.blk, p1 >> 4);
+    uint4 q2 = q1;
+    if ((p2 >> 4) != (p1 >> 4)) q2 = hsa_blk_load(d.blk, p2 >> 4);
+    hsa_occ4_q(q1, p1, a);
+    hsa_occ4_q(q2, p2, b);
     return 1u + ((p1 >> 6) != (p2 >> 6));
 }
 
@@ -80,7 +101,10 @@ __device__ __forceinline__ uint32_t hsa_occ1_pair(const RankDir d, uint32_t p1, 
 {
     p1 -= (p1 > d.isa0);
     p2 -= (p2 > d.isa0);
-    a = hsa_occ1_raw(d.blk, p1, c);
-    b = hsa_occ1_raw(d.blk, p2, c);
+    const uint4 q1 = hsa_blk_load(d.blk, p1 >> 4);
+    uint4 q2 = q1;
+    if ((p2 >> 4) != (p1 >> 4)) q2 = hsa_blk_load(d.blk, p2 >> 4);
+    a = hsa_occ1_q(q1, p1, c);
+    b = hsa_occ1_q(q2, p2, c);
     return 1u + ((p1 >> 6) != (p2 >> 6));
 }
