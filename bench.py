@@ -38,7 +38,7 @@ BATCH = 1_000_000
 DISTINCT = 3            # distinct read sets the steps cycle over
 METRIC = "aligned reads/sec, 100bp synthetic vs hg19-sized 2BWT, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
-BYTES_PER_QUERY = 64    # one 64-byte rank block per Occ query
+BYTES_PER_QUERY = 64    # one 64-byte HBM sector per Occ query
 
 
 def log(*a):
@@ -207,8 +207,10 @@ def main():
 
     # the measured ceiling for this access pattern: random whole 64-B blocks over a
     # table as large as the rank index (before the timed region, same process)
-    rand_gbs = _lib.probe_gather64(gi.nbytes(), device)
-    log(f"[bench] rank {rank}: random 64-B gather probe over {gi.nbytes() / 2**30:.2f} GiB: {rand_gbs:.0f} GB/s")
+    rand_gbs = _lib.probe_gather(gi.nbytes(), 1, device)
+    rand64_gbs = _lib.probe_gather(gi.nbytes(), 4, device)
+    log(f"[bench] rank {rank}: random-sector gather probe over {gi.nbytes() / 2**30:.2f} GiB: {rand_gbs:.0f} GB/s "
+        f"(16-B loads), {rand64_gbs:.0f} GB/s (whole 64-B sectors)")
 
     lib_stream = torch.cuda.ExternalStream(gi.stream_handle())
     for j in range(a.warmup):
@@ -302,10 +304,11 @@ def main():
                          "kernel": "k_search", "kernel_ms_mean": round(mean_kms, 3),
                          "algorithmic_bytes_per_launch": q_per_launch * BYTES_PER_QUERY,
                          "rank_queries_per_read": round(queries / reads_local, 1),
-                         "blocks_per_query": round(blocks / max(queries, 1), 4),
+                         "sectors_per_query": round(blocks / max(queries, 1), 4),
                          "bytes_per_query": BYTES_PER_QUERY,
-                         "peak_random64_measured": round(rand_gbs, 1),
-                         "frac_of_random64": round(achieved / rand_gbs, 4),
+                         "peak_random_sector_measured": round(rand_gbs, 1),
+                         "peak_random_sector_measured_64B_loads": round(rand64_gbs, 1),
+                         "frac_of_random_sector": round(achieved / rand_gbs, 4),
                          "traffic_source": TRAFFIC_SRC},
             "mapped_frac": round(mapped_all / reads_all, 4), "fallback_frac": round(fallback_all / reads_all, 4),
             "pops_per_read": round(pops / reads_local, 1),

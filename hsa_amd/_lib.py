@@ -24,7 +24,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_index_bytes", "hsa_index_device", "hsa_occ4_batch", "hsa_step_batch", "hsa_width_batch",
     "hsa_search_batch", "hsa_search_device", "hsa_configure", "hsa_free", "hsa_synth_genome_device",
     "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
-    "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather64", "hsa_last_pass_ms",
+    "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather", "hsa_last_pass_ms",
 ]
 
 
@@ -136,7 +136,7 @@ def lib():
     L.hsa_configure.argtypes = [C.c_int, C.c_int, C.c_int]
     L.hsa_free.argtypes = [vp]
     L.hsa_synth_genome_device.argtypes = [C.c_int, C.c_uint64, C.c_uint64, vp]
-    L.hsa_probe_gather64.argtypes = [C.c_int, C.c_uint64, C.POINTER(C.c_double)]
+    L.hsa_probe_gather.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
     L.hsa_build_bwt_device.argtypes = [C.c_int, C.c_uint64, vp, C.c_int, vp, C.POINTER(C.c_uint32), u32]
     L.hsa_cal_sa_reg_gap_flat.restype = C.c_long
     L.hsa_cal_sa_reg_gap_flat.argtypes = [vp, C.POINTER(GapOpt), C.c_int, u32, u64, u8, C.c_size_t, i32, u32, u64,
@@ -155,10 +155,10 @@ def device_count() -> int:
     return lib().hsa_device_count()
 
 
-def probe_gather64(table_bytes: int, device: int = 0) -> float:
-    """Measured random 64-byte block gather bandwidth in GB/s (hsa_probe_gather64)."""
+def probe_gather(table_bytes: int, per_sector: int = 1, device: int = 0) -> float:
+    """Measured random 64-byte-sector gather rate in GB/s (hsa_probe_gather)."""
     g = C.c_double()
-    check(lib().hsa_probe_gather64(device, table_bytes, C.byref(g)))
+    check(lib().hsa_probe_gather(device, table_bytes, per_sector, C.byref(g)))
     return g.value
 
 

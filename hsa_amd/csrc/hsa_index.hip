@@ -399,22 +399,26 @@ extern "C" int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, ui
 }
 
 // ---------------------------------------------------------------- roofline probe
-// Random 64-byte block gather over a table as large as the rank index (the access
-// pattern of every rank query): each lane loads one whole uniformly random 64-B
-// block per iteration, 16 waves per CU.  Gives the measured ceiling the search
-// kernel's achieved bandwidth is compared with (tools/membench.hip is
-// the stand-alone version with more modes).
-__global__ void __launch_bounds__(256) k_gather64(const uint4 *__restrict__ buf, uint64_t nblk, int iters,
-                                                 uint32_t *out)
+// Random 64-byte-sector gather over a table as large as the rank index -- the access
+// pattern of the rank queries.  Each lane loads `per_sector` x 16 bytes of one
+// uniformly random sector per iteration (1: one 16-byte load, what a rank query of
+// the 16-character layout issues; 4: the whole sector), 16 waves per CU.  Gives the
+// measured ceiling the search kernels' achieved bandwidth (one sector per query) is
+// compared with (tools/membench.hip is the stand-alone version).
+template <int PER>
+__global__ void __launch_bounds__(256) k_gather(const uint4 *__restrict__ buf, uint64_t nsec, int iters, uint32_t *out)
 {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t acc = 0;
     uint64_t s = splitmix64(gid + 1);
     for (int it = 0; it < iters; ++it) {
         s = splitmix64(s);
-        const uint4 *p = buf + (s % nblk) * 4;
-        const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
-        acc += a.x ^ b.y ^ c.z ^ d.w;
+        const uint4 *p = buf + (s % nsec) * 4 + (PER == 1 ? (s >> 62) : 0);
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const uint4 v = p[k];
+            acc += v.x ^ v.y ^ v.z ^ v.w;
+        }
     }
     if (acc == 0x12345678u) out[0] = acc;   // keeps the loads live; never true in practice
 }
@@ -425,8 +429,9 @@ __global__ void k_fill_words(uint32_t *buf, uint64_t n)
         buf[i] = (uint32_t)splitmix64(i);
 }
 
-extern "C" int hsa_probe_gather64(int device, uint64_t table_bytes, double *gbps)
+extern "C" int hsa_probe_gather(int device, uint64_t table_bytes, int per_sector, double *gbps)
 {
+    if (per_sector != 1 && per_sector != 4) { hsa_set_error("per_sector must be 1 or 4"); return HSA_E_ARG; }
     HSA_HIP(hipSetDevice(device));
     hipDeviceProp_t prop;
     HSA_HIP(hipGetDeviceProperties(&prop, device));
@@ -439,21 +444,25 @@ extern "C" int hsa_probe_gather64(int device, uint64_t table_bytes, double *gbps
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int rc = 0;
     float ms = 0;
-    const uint64_t nblk = table_bytes / 64;
+    const uint64_t nsec = table_bytes / 64;
     const unsigned blocks = (unsigned)prop.multiProcessorCount * 4;   // 16 waves per CU
     const int iters = 1000;
+    auto launch = [&](int it) {
+        if (per_sector == 1) k_gather<1><<<blocks, 256>>>(buf, nsec, it, out);
+        else k_gather<4><<<blocks, 256>>>(buf, nsec, it, out);
+    };
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { rc = HSA_E_HIP; goto done; }
     k_fill_words<<<4096, 256>>>((uint32_t *)buf, table_bytes / 4);
-    k_gather64<<<blocks, 256>>>(buf, nblk, iters / 4, out);           // warm-up
+    launch(iters / 4);                                               // warm-up
     (void)hipEventRecord(e0, 0);
-    k_gather64<<<blocks, 256>>>(buf, nblk, iters, out);
+    launch(iters);
     (void)hipEventRecord(e1, 0);
     if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
         hsa_set_error("probe: kernel failed");
         rc = HSA_E_HIP;
         goto done;
     }
-    *gbps = (double)blocks * 256 * iters * 64 / (ms * 1e-3) / 1e9;
+    *gbps = (double)blocks * 256 * iters * 64 / (ms * 1e-3) / 1e9;    // sectors touched x 64 B
 done:
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);

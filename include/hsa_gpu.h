@@ -131,11 +131,13 @@ void hsa_free(void *p);
 /* Synthetic workload helpers (bench data generation on the device). */
 int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, uint32_t *d_code_lsb);
 
-/* Roofline probe: measured bandwidth (GB/s) of uniformly random whole 64-byte
- * block loads over a table of `table_bytes` -- the access pattern of a rank query --
- * with all CUs at 16 waves each.  The denominator the search kernel's achieved
- * bandwidth is compared with next to the 8 TB/s spec peak. */
-int hsa_probe_gather64(int device, uint64_t table_bytes, double *gbps);
+/* Roofline probe: measured rate of uniformly random 64-byte-sector gathers over a
+ * table of `table_bytes` (the access pattern of rank queries), in GB/s of sectors
+ * touched (sectors/s x 64 B), all CUs at 16 waves each.  per_sector = 1: one 16-byte
+ * load per sector (what a rank query issues); 4: the whole sector in four loads.
+ * The denominator the search kernel's achieved bandwidth is compared with next to
+ * the 8 TB/s spec peak. */
+int hsa_probe_gather(int device, uint64_t table_bytes, int per_sector, double *gbps);
 
 /* Suffix-array based BWT construction on the device for a text given as LSB-first
  * 2-bit codes (16 per u32).  Produces the $-less BWT codes (LSB-first) and
