@@ -88,7 +88,7 @@ TRAFFIC_SRC = "profiles/r01_pmc_summary.json"
 
 
 def traffic_per_launch():
-    """HBM read+write bytes per k_search launch from the committed PMC pass
+    """HBM read+write bytes per step (k_widths + k_search) from the committed PMC pass
     (FETCH_SIZE calibrated on random 64-B gathers + WRITE_SIZE; tools/profile_run.sh,
     tools/pmc_summary.py) -- counters cannot be read in the timed run itself."""
     try:
@@ -301,7 +301,8 @@ def main():
                        "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_per_launch(),
-                         "kernel": "k_search", "kernel_ms_mean": round(mean_kms, 3),
+                         "kernel": "k_widths+k_search (one step)", "kernel_ms_mean": round(mean_kms, 3),
+                         "kernel_split_ms": {"k_widths": round(split_ms[0], 3), "k_search": round(split_ms[1], 3)},
                          "algorithmic_bytes_per_launch": q_per_launch * BYTES_PER_QUERY,
                          "rank_queries_per_read": round(queries / reads_local, 1),
                          "sectors_per_query": round(blocks / max(queries, 1), 4),

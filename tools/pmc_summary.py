@@ -23,7 +23,7 @@ def counters(d, kernel):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
     for r in rows:
-        if kernel not in r["Kernel_Name"]:
+        if not r["Kernel_Name"].startswith(kernel) and (" " + kernel) not in r["Kernel_Name"]:
             continue
         agg[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
         dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
@@ -42,11 +42,18 @@ def main():
     known = 256 * 16 // 4 * 256 * 2000 * 64
     cal = med(mb, "FETCH_SIZE") * 1024 / known
     out["fetch_calibration_random64"] = round(cal, 4)
-    f, dur = counters(os.path.join(src, "pmc_fetch"), "k_search")
-    w, _ = counters(os.path.join(src, "pmc_write"), "k_search")
-    out["fetch_bytes_per_launch"] = med(f, "FETCH_SIZE") * 1024 / cal
-    out["write_bytes_per_launch"] = med(w, "WRITE_SIZE") * 1024
-    out["launch_ms_median_pmc_pass"] = statistics.median(dur.values())
+    # one step = k_widths + k_search launches: per-kernel medians, summed
+    out["per_kernel"] = {}
+    for k in ("k_widths", "k_search"):
+        f, dur = counters(os.path.join(src, "pmc_fetch"), k)
+        w, _ = counters(os.path.join(src, "pmc_write"), k)
+        if not f:
+            continue
+        out["per_kernel"][k] = {"fetch_bytes": med(f, "FETCH_SIZE") * 1024 / cal,
+                                "write_bytes": med(w, "WRITE_SIZE") * 1024,
+                                "ms_median_pmc_pass": statistics.median(dur.values())}
+    out["fetch_bytes_per_launch"] = sum(v["fetch_bytes"] for v in out["per_kernel"].values())
+    out["write_bytes_per_launch"] = sum(v["write_bytes"] for v in out["per_kernel"].values())
     sq, _ = counters(os.path.join(src, "pmc_sq"), "k_search")
     wc = med(sq, "SQ_WAVE_CYCLES")
     out["sq"] = {"wait_any_frac": med(sq, "SQ_WAIT_ANY") / wc,
