@@ -136,6 +136,9 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--cpu-sample", type=int, default=20000, help="reads timed on the CPU restatement")
     ap.add_argument("--parity-sample", type=int, default=4000, help="reads checked against the CPU restatement")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+                    help="BASELINE.json config: 2 = 0-4 substitutions, -n 4 -o 0 (default, the metric's config); "
+                         "3 = one 1-3 bp indel + 0-2 substitutions, -n 4 -o 1")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0)
     a = ap.parse_args()
@@ -168,17 +171,26 @@ def main():
     batches = []
     for j in range(nd):
         gidx = j * world + rank
-        reads, _ = synth.make_reads(genome, recs, a.batch, READ_LEN, 5 * 1_000_000 + gidx, max_mm=4)
+        if a.config == 2:
+            reads, _ = synth.make_reads(genome, recs, a.batch, READ_LEN, 5 * 1_000_000 + gidx, max_mm=4)
+        else:   # SURVEY §8d config 3 reads (seed 6): one indel of 1-3 bp + 0-2 substitutions
+            reads, _ = synth.make_reads(genome, recs, a.batch, READ_LEN, 6 * 1_000_000 + gidx, indel=True,
+                                        max_mm_indel=2)
         batches.append(reads)
     log(f"[bench] rank {rank}: {nd} x {a.batch} reads generated in {time.time() - t0:.1f} s")
 
-    # bwa_cal_sa_reg_gap prologue on the host (bwtaln.c:254-337): -n 4 -o 0, fixed length
+    # bwa_cal_sa_reg_gap prologue on the host (bwtaln.c:254-337): -n 4 -o 0|1, fixed length.
+    # The timed batches are steady-state batches (not the process's first): GAPE is
+    # already cleared in the caller's block, so both option regimes coincide.
+    max_gapo = 0 if a.config == 2 else 1
+    opt_str = f"-n 4 -o {max_gapo}"
     opt = GapOpt.default()
-    opt.max_diff, opt.fnr, opt.max_gapo = 4, -1.0, 0
+    opt.max_diff, opt.fnr, opt.max_gapo = 4, -1.0, max_gapo
+    opt.mode &= ~0x01
     # aln_score(max_diff+1, max_gapo+1, max_gape+1) of local_opt (bwtaln.c:264-267, bwtgap.c:18)
     n_stacks = (opt.max_diff + 1) * opt.s_mm + (opt.max_gapo + 1) * opt.s_gapo + (opt.max_gape + 1) * opt.s_gape
     rg = Regime(s_mm=opt.s_mm, s_gapo=opt.s_gapo, s_gape=opt.s_gape, mode=0, indel_end_skip=opt.indel_end_skip,
-                max_del_occ=opt.max_del_occ, max_entries=opt.max_entries, max_gapo=0, max_gape=opt.max_gape,
+                max_del_occ=opt.max_del_occ, max_entries=opt.max_entries, max_gapo=max_gapo, max_gape=opt.max_gape,
                 max_seed_diff=opt.max_seed_diff, max_top2=opt.max_top2, n_stacks=n_stacks, max_diff=opt.max_diff)
     jobs = np.zeros(a.batch, _lib.JOB_DTYPE)
     jobs["off"] = np.arange(a.batch, dtype=np.uint64) * READ_LEN
@@ -294,13 +306,14 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": f"{a.batch // 1000}k x 100bp reads per step and GPU, 0-4 substitutions, 50% rc, "
-                                   f"vs synthetic hg19-sized 2BWT ({T} bp, {RECORDS} records), -n 4 -o 0 "
-                                   f"(BASELINE configs[1]); {a.steps} timed steps",
-                       "genome_bp": T, "reads_per_step": a.batch, "read_len": READ_LEN, "options": "-n 4 -o 0",
+            "config": {"workload": f"{a.batch // 1000}k x 100bp reads per step and GPU, "
+                                   + ("0-4 substitutions" if a.config == 2 else "one 1-3 bp indel + 0-2 substitutions")
+                                   + f", 50% rc, vs synthetic hg19-sized 2BWT ({T} bp, {RECORDS} records), {opt_str} "
+                                   f"(BASELINE configs[{a.config - 1}]); {a.steps} timed steps",
+                       "genome_bp": T, "reads_per_step": a.batch, "read_len": READ_LEN, "options": opt_str,
                        "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_per_launch(),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_per_launch() if a.config == 2 else None,
                          "kernel": "k_widths+k_search (one step)", "kernel_ms_mean": round(mean_kms, 3),
                          "kernel_split_ms": {"k_widths": round(split_ms[0], 3), "k_search": round(split_ms[1], 3)},
                          "algorithmic_bytes_per_launch": q_per_launch * BYTES_PER_QUERY,
@@ -322,7 +335,7 @@ def main():
         log(f"[bench] CPU restatement index built in {time.time() - t0:.1f} s")
         from oracle_ctypes import Opt, default_opt
         od = default_opt()
-        od.update(max_diff=4, fnr=-1.0, max_gapo=0)
+        od.update(max_diff=4, fnr=-1.0, max_gapo=max_gapo, mode=od["mode"] & ~0x01)
         if a.parity_sample:
             n = min(a.parity_sample, a.batch)
             r0 = batches[a.warmup % nd][:n]

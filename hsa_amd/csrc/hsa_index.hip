@@ -18,7 +18,7 @@
 
 static thread_local char g_err[1024] = "";
 int g_waves_per_cu = 16;
-int g_pool_entries = 8192;
+int g_pool_entries = 0;      // 0: 8192 per lane, 16384 when gap opens are allowed
 int g_hit_cap = 64;
 
 void hsa_set_error(const char *fmt, ...)
@@ -46,6 +46,8 @@ extern "C" int hsa_configure(int waves_per_cu, int pool_entries, int hit_cap)
     if (pool_entries > 0) {
         if (pool_entries > 65535) { hsa_set_error("pool_entries > 65535"); return HSA_E_ARG; }
         g_pool_entries = pool_entries;
+    } else if (pool_entries < 0) {
+        g_pool_entries = 0;              // back to the per-regime default
     }
     if (hit_cap > 0) g_hit_cap = hit_cap;
     return 0;
@@ -230,7 +232,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     (void)hipSetDevice(ix->device);
     (void)hipFree(ix->blk[0]); (void)hipFree(ix->blk[1]);
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big);
-    (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows);
+    (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
     if (ix->evm) (void)hipEventDestroy(ix->evm);

@@ -39,6 +39,7 @@ struct hsa_index {
     void *d_out = nullptr; size_t d_out_cap = 0;
     // per-(read, strand) width rows written by k_widths, read by k_search
     void *d_wrows = nullptr; size_t d_wrows_cap = 0;
+    void *d_ovf = nullptr; size_t d_ovf_cap = 0;   // device-path list of reads to re-run
     uint64_t *d_ctr = nullptr;
     unsigned char staged[512];          // last regime block copied to d_in (skip identical re-copies)
     int staged_valid = 0;

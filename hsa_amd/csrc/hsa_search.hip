@@ -82,6 +82,12 @@ struct SearchArgs {
     uint32_t pcap, hcap, nb;
     uint32_t off_heads, off_wb, off_ws;   // LDS byte offsets
     uint32_t mm_buckets;           // 1: the bucket of every score is its n_mm (no gap opens, s_mm > 0)
+    // device-side overflow re-run: the main pass appends reads that exceeded their
+    // lane's capacity to ovf_list (count in ctr[8]); the re-run pass takes its read
+    // count from n_dev and its queue head from ctr[qctr]
+    int32_t *ovf_list;
+    const unsigned long long *n_dev;
+    uint32_t qctr;
 };
 
 // entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
@@ -233,7 +239,8 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
 {
     using F = WFmt<WT>;
     const uint32_t R = blockIdx.x * BLOCK + threadIdx.x;     // row = list position * 2 + strand
-    if (R >= 2u * (uint32_t)a.n_jobs) return;
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    if (R >= 2u * n_jobs) return;
     const uint32_t q = R >> 1, strand = R & 1u;
     const hsa_job_t J = a.jobs[a.job_list ? a.job_list[q] : (int)q];
     const uint32_t len = J.len, off = (uint32_t)J.off;
@@ -340,6 +347,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 #endif
     uint32_t st_p = 0;
     uint64_t st_q = 0, st_b = 0;          // wave-uniform (ballot counts)
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
 #ifdef HSA_DIAG
     uint32_t dc[16] = {0};
     uint64_t tsec[4] = {0, 0, 0, 0};
@@ -417,6 +425,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
     };
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
         const int job = a.job_list ? a.job_list[qpos] : (int)qpos;
+        if ((fl & HSA_F_OVERFLOW) && a.ovf_list) a.ovf_list[atomicAdd(&a.ctr[8], 1ull)] = job;
         a.n_aln[job] = na;
         a.flags[job] = fl;
         a.hit_off[job] = ho;
@@ -515,11 +524,11 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
             if (mb) {
                 const int leader = __ffsll((unsigned long long)mb) - 1;
                 unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(&a.ctr[0], (unsigned long long)__popcll(mb));
+                if (lane == leader) base = atomicAdd(&a.ctr[a.qctr], (unsigned long long)__popcll(mb));
                 base = __shfl(base, leader);
                 if (need) {
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
-                    if (j < (unsigned long long)a.n_jobs) {
+                    if (j < (unsigned long long)n_jobs) {
                         qpos = (uint32_t)j;
                         const hsa_job_t J = a.jobs[a.job_list ? a.job_list[j] : (int)j];
                         opt_max_diff = J.max_diff;
@@ -906,7 +915,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     size_t blocks = (size_t)ix->n_cu * per_cu;
     size_t need_blocks = ((size_t)n_jobs + BLOCK - 1) / BLOCK;
     if (big) {
-        blocks = need_blocks < 4 ? need_blocks : 4;
+        blocks = need_blocks < 16 ? need_blocks : 16;
     } else if (need_blocks < blocks) {
         blocks = need_blocks;
     }
@@ -921,7 +930,8 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
         fprintf(stderr, "[hsa] launch: %d CUs x %d workgroups (runtime occupancy query says %d), LDS %zu B, "
                 "%zu workgroups, %d buckets\n", ix->n_cu, per_cu, occ, P.lds, blocks, nb);
     }
-    P.pcap = big ? 65535u : (uint32_t)g_pool_entries;
+    // pool slots are not reused within a search: gapped searches push many more
+    P.pcap = big ? 65535u : (uint32_t)(g_pool_entries ? g_pool_entries : (gaps ? 16384 : 8192));
     P.hcap = big ? 16384u : (uint32_t)g_hit_cap;
     return 0;
 }
@@ -947,7 +957,8 @@ static void launch_search(const LaunchPlan &P, const SearchArgs &A, hipStream_t 
 static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
                        const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
                        int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
-                       uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st)
+                       uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st,
+                       int32_t *ovf_list = nullptr, const unsigned long long *n_dev = nullptr, uint32_t qctr = 0)
 {
     int rc = hsa_scratch_reserve(S, P.lanes, P.pcap, P.hcap);
     if (rc) return rc;
@@ -967,16 +978,17 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     A.wb = wr; A.ws = wr + rows * rb; A.wg = reinterpret_cast<uint32_t *>(wr + rows * (rb + rs));
     A.rb = rb; A.rs = rs; A.rg = rg;
     A.pool = S.pool; A.nxt = S.nxt; A.hbuf = S.hbuf;
-    A.pcap = (uint32_t)S.pcap; A.hcap = (uint32_t)S.hcap;
+    A.pcap = P.pcap; A.hcap = P.hcap;        // the planned capacities (the scratch may be larger)
     A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
     A.mm_buckets = ix->staged_mmb ? 1u : 0u;
-    HSA_HIP(hipMemsetAsync(d_ctr, 0, 8 * sizeof(unsigned long long), st));
+    A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr;
+    if (!n_dev) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
     size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
     if (wblocks < 1) wblocks = 1;
     if (P.wide) hipLaunchKernelGGL(k_widths<uint16_t>, dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
     else hipLaunchKernelGGL(k_widths<uint8_t>, dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
     HSA_HIP(hipGetLastError());
-    if (ix->evm) HSA_HIP(hipEventRecord(ix->evm, st));
+    if (ix->evm && !n_dev) HSA_HIP(hipEventRecord(ix->evm, st));
     if (P.wide) launch_search<uint16_t>(P, A, st);
     else launch_search<uint8_t>(P, A, st);
     HSA_HIP(hipGetLastError());
@@ -1176,10 +1188,25 @@ extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, i
     if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, any_gaps(regimes, n_regimes),
                           need_wide(regimes, n_regimes), false, P)))
         return rc;
+    if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, (size_t)b->n_jobs * 4 + 64))) return rc;
+    unsigned long long *ctr = (unsigned long long *)b->d_counters;
+    const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
+    const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
     HSA_HIP(hipEventRecord(ix->ev0, st));
-    if ((rc = launch_pass(ix, P, ix->main, (const hsa_regime_t *)ix->d_in, (const uint8_t *)ix->d_in + 256, b->d_jobs,
-                          nullptr, b->n_jobs, b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags,
-                          b->d_hit_off, b->d_hits, b->hit_cap, (unsigned long long *)b->d_counters, st)))
+    if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, b->d_jobs, nullptr, b->n_jobs, b->max_len, b->max_seed,
+                          b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st,
+                          (int32_t *)ix->d_ovf)))
+        return rc;
+    // exact re-run of the reads that overflowed their lane's capacity, with the large
+    // per-lane capacity; the read count stays on the device (ctr[8]), so an empty
+    // re-run is a launch whose lanes exit at once
+    LaunchPlan B;
+    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, any_gaps(regimes, n_regimes),
+                          need_wide(regimes, n_regimes), true, B)))
+        return rc;
+    if ((rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, b->d_jobs, (const int32_t *)ix->d_ovf, b->n_jobs,
+                          b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
+                          b->hit_cap, ctr, st, nullptr, ctr + 8, 9)))
         return rc;
     HSA_HIP(hipEventRecord(ix->ev1, st));
     return 0;

@@ -123,7 +123,8 @@ int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regime
 /* Device time of the two kernels of the last pass on this index (k_widths, then
  * k_search); waits for that pass to finish. */
 int hsa_last_pass_ms(hsa_index_t *ix, float *widths_ms, float *search_ms);
-/* Kernel geometry/capacity knobs (0 = default). */
+/* Kernel geometry/capacity knobs: 0 leaves a knob unchanged; pool_entries < 0 restores
+ * its default (8192 entries per lane, 16384 when gap opens are allowed). */
 int hsa_configure(int waves_per_cu, int pool_entries, int hit_cap);
 
 void hsa_free(void *p);

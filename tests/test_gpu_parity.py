@@ -80,7 +80,7 @@ def _compare(name, pool_entries=0):
                                                    g["batch"])
     finally:
         if pool_entries:
-            configure(pool_entries=8192)
+            configure(pool_entries=-1)
     exp_splice = (g["flags"] & 1).astype(bool)
     got_splice = (flags & 1).astype(bool)
     assert np.array_equal(got_splice, exp_splice), np.nonzero(got_splice != exp_splice)[0][:10]
@@ -98,3 +98,56 @@ def test_search_matches_reference(name):
 def test_overflow_rerun_is_exact(name):
     """A tiny per-lane pool forces most reads through the large-capacity re-run."""
     _compare(name, pool_entries=64)
+
+
+def test_device_path_rerun_is_exact():
+    """hsa_search_device (device-resident batch, bench.py's path) re-runs reads that
+    overflow their lane's capacity on the device: with a tiny pool most reads of a
+    gapped case take that route, and every hit must still equal the oracle's."""
+    import torch
+    from hsa_amd._lib import JOB_DTYPE, DeviceBatch, GapOpt, Regime, configure
+    from oracle_ctypes import Opt, OracleIndex, default_opt
+    g = load_case("tiny_gap100_n4o1")
+    fwd, rev = index_io.read_index(INDEX[g["index"]])
+    ix = gpu_index(g["index"])
+    od = parse_opts(g["args"], default_opt())
+    od["mode"] &= ~0x01                      # a steady-state batch: both regimes coincide
+    n = len(g["lens"])
+    e_n, e_f, e_h, _ = OracleIndex(fwd, rev).cal_sa_reg_gap(g["lens"], g["codes"], Opt.from_dict(od))
+    o = GapOpt.from_dict(od)
+    n_stacks = (o.max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape
+    rg = Regime(s_mm=o.s_mm, s_gapo=o.s_gapo, s_gape=o.s_gape, mode=0, indel_end_skip=o.indel_end_skip,
+                max_del_occ=o.max_del_occ, max_entries=o.max_entries, max_gapo=o.max_gapo, max_gape=o.max_gape,
+                max_seed_diff=o.max_seed_diff, max_top2=o.max_top2, n_stacks=n_stacks, max_diff=o.max_diff)
+    jobs = np.zeros(n, JOB_DTYPE)
+    jobs["off"] = np.concatenate([[0], np.cumsum(g["lens"].astype(np.uint64))[:-1]])
+    jobs["len"] = g["lens"]
+    jobs["max_diff"] = o.max_diff
+    jobs["seed_len"] = np.where(g["lens"] > o.seed_len, o.seed_len, 0x7FFFFFFF)
+    d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).cuda()
+    d_codes = torch.from_numpy(np.ascontiguousarray(g["codes"])).cuda()
+    cap = n * 16
+    t = dict(n=torch.zeros(n, dtype=torch.int32, device="cuda"), f=torch.zeros(n, dtype=torch.int32, device="cuda"),
+             o=torch.zeros(n, dtype=torch.int64, device="cuda"), h=torch.zeros(cap * 9, dtype=torch.int32, device="cuda"),
+             c=torch.zeros(16, dtype=torch.int64, device="cuda"))
+    b = DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=n, d_codes=d_codes.data_ptr(), d_n_aln=t["n"].data_ptr(),
+                    d_flags=t["f"].data_ptr(), d_hit_off=t["o"].data_ptr(), d_hits=t["h"].data_ptr(), hit_cap=cap,
+                    d_counters=t["c"].data_ptr(), max_len=int(g["lens"].max()), max_seed=o.seed_len)
+    configure(pool_entries=8)
+    try:
+        ix.search_device([rg], b)
+        torch.cuda.synchronize()
+    finally:
+        configure(pool_entries=-1)
+    reruns = int(t["c"][8].item())
+    assert reruns > 0, reruns
+    g_n = t["n"].cpu().numpy()
+    g_f = t["f"].cpu().numpy().astype(np.uint32)
+    g_o = t["o"].cpu().numpy()
+    g_h = t["h"].cpu().numpy().view(np.uint32).reshape(-1, 9)
+    assert not (g_f & 2).any(), "reads left overflowed after the re-run"
+    assert np.array_equal(g_f & 1, e_f & 1)
+    assert np.array_equal(g_n, e_n)
+    exp = split_hits(e_n, e_h)
+    bad = [i for i in range(n) if not np.array_equal(g_h[g_o[i]:g_o[i] + max(g_n[i], 0)], exp[i])]
+    assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
