@@ -25,6 +25,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_search_batch", "hsa_search_device", "hsa_configure", "hsa_free", "hsa_synth_genome_device",
     "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
     "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather", "hsa_last_pass_ms",
+    "hsa_index_set_sa", "hsa_sa_position_batch", "hsa_sa_position_device",
 ]
 
 
@@ -136,6 +137,8 @@ def lib():
     L.hsa_configure.argtypes = [C.c_int, C.c_int, C.c_int]
     L.hsa_free.argtypes = [vp]
     L.hsa_synth_genome_device.argtypes = [C.c_int, C.c_uint64, C.c_uint64, vp]
+    L.hsa_index_set_sa.argtypes = [vp, u32, C.c_uint64, C.c_uint32, u32, C.c_int]
+    L.hsa_sa_position_batch.argtypes = [vp, C.c_size_t, u32, u32]
     L.hsa_probe_gather.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
     L.hsa_build_bwt_device.argtypes = [C.c_int, C.c_uint64, vp, C.c_int, vp, C.POINTER(C.c_uint32), u32]
     L.hsa_cal_sa_reg_gap_flat.restype = C.c_long
@@ -215,6 +218,22 @@ class GpuIndex:
     def search_device(self, regimes, batch: "DeviceBatch"):
         rg = (Regime * len(regimes))(*regimes)
         check(lib().hsa_search_device(self.h, rg, len(regimes), C.byref(batch), None))
+
+    def set_sa(self, sa, blocks):
+        """Upload the sampled SA (index_io.SaFile) and the block table (rows of
+        chrID, blockStart, blockEnd, ori) for SA -> position (hsa_index_set_sa)."""
+        vals = np.ascontiguousarray(sa.values, np.uint32)
+        blk = np.ascontiguousarray(blocks, np.uint32).reshape(-1)
+        if blk.size == 0:
+            blk = np.zeros(4, np.uint32)
+        check(lib().hsa_index_set_sa(self.h, vals, len(vals), sa.interval, blk, len(blocks)))
+
+    def sa_positions(self, idx):
+        """(SA value, chrID, 1-based position, packed position) per SA index."""
+        idx = np.ascontiguousarray(idx, np.uint32)
+        out = np.zeros((len(idx), 4), np.uint32)
+        check(lib().hsa_sa_position_batch(self.h, len(idx), idx, out))
+        return out
 
     def last_pass_ms(self):
         """(k_widths ms, k_search ms) of the last device pass on this index."""

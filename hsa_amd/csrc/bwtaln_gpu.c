@@ -32,6 +32,8 @@ _Static_assert(sizeof(bwt_aux_t) == 96, "bwt_aux_t layout");
 _Static_assert(sizeof(BWT) == 128, "BWT layout");
 _Static_assert(sizeof(Idx2BWT) == 544, "Idx2BWT layout");
 _Static_assert(sizeof(gap_entry_t) == 28, "gap_entry_t layout");
+_Static_assert(sizeof(HSP) == 48, "HSP layout");
+_Static_assert(sizeof(ChrBlock) == 16, "ChrBlock layout");
 
 #define BWA_AVG_ERR 0.02
 #define SEED_NONE 0x7fffffff
@@ -267,6 +269,11 @@ int hsa_gpu_attach(const Idx2BWT *bi)
     hsa_index_t *ix = NULL;
     int rc = hsa_index_create(g_device, f->textLength, f->inverseSa0, f->cumulativeFreq, f->bwtCode,
                               r->textLength, r->inverseSa0, r->cumulativeFreq, r->bwtCode, &ix);
+    /* SA -> position on the device needs the sampled SA (BWT.c:206-223) and blocks */
+    if (rc == 0 && f->saValue && bi->hsp)
+        rc = hsa_index_set_sa(ix, f->saValue, f->saValueSizeInWord, f->saInterval,
+                              (const uint32_t *)bi->hsp->blockList, bi->hsp->numOfBlock);
+    if (rc != 0 && ix) { hsa_index_free(ix); ix = NULL; }
     if (rc == 0) { g_att[slot].key = bi; g_att[slot].ix = ix; }
     pthread_mutex_unlock(&g_att_mu);
     return rc;

@@ -233,6 +233,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     (void)hipFree(ix->blk[0]); (void)hipFree(ix->blk[1]);
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf);
+    (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
     if (ix->evm) (void)hipEventDestroy(ix->evm);
@@ -258,6 +259,7 @@ extern "C" int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t
 {
     if (dir < 0 || dir > 1) { hsa_set_error("dir"); return HSA_E_ARG; }
     HSA_HIP(hipSetDevice(ix->device));
+    ix->staged_valid = 0;                      // d_in is reused below
     int rc;
     if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, n * 4 + 16)) || (rc = hsa_grow(&ix->d_out, &ix->d_out_cap, n * 16 + 16)))
         return rc;
@@ -292,6 +294,7 @@ __global__ void k_step(RankDir d, const uint32_t *C, const uint32_t *in, size_t 
 extern "C" int hsa_step_batch(hsa_index_t *ix, size_t n, const uint32_t *klrr, uint32_t *out16)
 {
     HSA_HIP(hipSetDevice(ix->device));
+    ix->staged_valid = 0;                      // d_in is reused below
     int rc;
     if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, n * 16 + 64)) || (rc = hsa_grow(&ix->d_out, &ix->d_out_cap, n * 64 + 16)))
         return rc;
@@ -337,6 +340,7 @@ extern "C" int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, 
                                const uint8_t *codes, size_t codes_len, uint32_t *width_out)
 {
     HSA_HIP(hipSetDevice(ix->device));
+    ix->staged_valid = 0;                      // d_in is reused below
     uint64_t *woff = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
     uint64_t tot = 0;
     for (size_t i = 0; i < n; ++i) { woff[i] = tot; tot += 2 * ((uint64_t)lens[i] + 1); }

@@ -40,6 +40,9 @@ struct hsa_index {
     // per-(read, strand) width rows written by k_widths, read by k_search
     void *d_wrows = nullptr; size_t d_wrows_cap = 0;
     void *d_ovf = nullptr; size_t d_ovf_cap = 0;   // device-path list of reads to re-run
+    // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
+    uint32_t *d_sa = nullptr, *d_blocks = nullptr;
+    uint32_t sa_interval = 0, n_blocks = 0;
     uint64_t *d_ctr = nullptr;
     unsigned char staged[512];          // last regime block copied to d_in (skip identical re-copies)
     int staged_valid = 0;

@@ -99,6 +99,34 @@ def write_bwt_files(prefix: str, T: int, isa0: int, C: np.ndarray, codes: np.nda
         f.write(major.tobytes())
 
 
+@dataclass
+class SaFile:
+    interval: int
+    values: np.ndarray     # uint32[(T+s)/s]; values[0] = -1 as BWTLoad sets it (BWT.c:222)
+
+
+def read_sa(prefix: str) -> SaFile:
+    """prefix.index.sa: inverseSa0, C[1..4], saInterval, then (T+s)/s sampled SA
+    values (BWT.c:206-223)."""
+    raw = np.fromfile(prefix + ".index.sa", dtype=np.uint32)
+    T, s = int(raw[4]), int(raw[5])
+    vals = np.ascontiguousarray(raw[6:6 + (T + s) // s]).copy()
+    vals[0] = 0xFFFFFFFF
+    return SaFile(interval=s, values=vals)
+
+
+def read_blocks(prefix: str) -> np.ndarray:
+    """Chromosome blocks of prefix.index.ann (HSP.c:325-337, ChrBlock HSP.h:41-46) as
+    uint32 rows (chrID, blockStart, blockEnd, ori), in file order."""
+    with open(prefix + ".index.ann") as f:
+        lines = f.read().split("\n")
+    n_chr = int(lines[0].split()[1])
+    i = 1 + n_chr
+    nb = int(lines[i].split()[0])
+    rows = [list(map(int, lines[i + 1 + k].split()[:4])) for k in range(nb)]
+    return np.array(rows, dtype=np.int64).astype(np.uint32).reshape(-1, 4)
+
+
 def exists(prefix: str) -> bool:
     return all(os.path.exists(f"{prefix}.index.{e}") for e in ("bwt", "rev.bwt"))
 

@@ -37,7 +37,16 @@ typedef struct BWT {
                  inverseSaSizeInWord, cachedSaIndexSizeInWord;
 } BWT;
 
-struct HSP;
+/* HSP.h:41-46 and :65-72 (the block table feeds SA -> position) */
+typedef struct { int chrID; unsigned int blockStart, blockEnd, ori; } ChrBlock;
+typedef struct HSP {
+    unsigned int *packedDNA;
+    int chrNum;
+    char **chrName;
+    int numOfBlock;
+    ChrBlock *blockList;
+    unsigned int dnaLength;
+} HSP;
 struct MMPool;
 /* 2BWT-Interface.h:29-36 */
 typedef struct _Idx2BWT {

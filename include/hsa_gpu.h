@@ -132,6 +132,18 @@ void hsa_free(void *p);
 /* Synthetic workload helpers (bench data generation on the device). */
 int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, uint32_t *d_code_lsb);
 
+/* SA index -> text position (BWTSaValue BWT.c:1195 + BWTRetrievePositionFromSAIndex
+ * 2BWT-Interface.c:329), batched.  hsa_index_set_sa uploads the sampled suffix array
+ * as BWTLoad holds it (values[0] = -1, (T+s)/s values, interval s) and the chromosome
+ * block table (n_blocks rows of u32 chrID, blockStart, blockEnd, ori; ChrBlock
+ * HSP.h:41-46).  Output: 4 u32 per index -- SA value, chrID, 1-based position in the
+ * chromosome, position in the packed text; chrID and position are 0xFFFFFFFF when no
+ * block holds it. */
+int hsa_index_set_sa(hsa_index_t *ix, const uint32_t *sa_values, uint64_t n_values, uint32_t interval,
+                     const uint32_t *blocks, int n_blocks);
+int hsa_sa_position_batch(hsa_index_t *ix, size_t n, const uint32_t *sa_index, uint32_t *out4);
+int hsa_sa_position_device(hsa_index_t *ix, size_t n, const uint32_t *d_sa_index, uint32_t *d_out4, void *stream);
+
 /* Roofline probe: measured rate of uniformly random 64-byte-sector gathers over a
  * table of `table_bytes` (the access pattern of rank queries), in GB/s of sectors
  * touched (sectors/s x 64 B), all CUs at 16 waves each.  per_sector = 1: one 16-byte

@@ -109,6 +109,63 @@ void or_occ4(const or_index_t *ix, int dir, uint32_t i, uint32_t occ[4])
     occ4(dir ? &ix->r : &ix->f, i, occ);
 }
 
+/* BWTPsiMinusValue (BWT.c:1142-1162) via BWTOccValueOnSpot (BWT.c:924-959): for
+ * index != inverseSa0, i = index + 1 shifted past '$' (BWT.c:949), c = the BWT
+ * character before i, result C[c] + Occ(c, i) (the count includes that character). */
+static uint32_t psi_minus(const or_bwt_t *b, uint32_t index)
+{
+    if (index == b->isa0) return 0;
+    uint32_t i = index + 1;
+    i -= (i > b->isa0);
+    uint32_t p = i - 1, c = (uint32_t)((b->w[p >> 5] >> (2 * (p & 31))) & 3u);
+    /* Occ over the $-less prefix [0, i): occ4 takes a $-including index, so pass the
+     * index that shifts back to i */
+    uint32_t o[4];
+    occ4(b, i + (i > b->isa0 ? 1u : 0u), o);
+    return b->C[c] + o[c];
+}
+
+/* BWTSaValue (BWT.c:1195-1220): LF-walk to a sampled SA index, then add the steps.
+ * sa_values[0] is -1 (BWT.c:222) and PsiMinus(inverseSa0) = 0, so the walk through
+ * '$' lands on that sample with u32 wrap-around, exactly as the reference. */
+uint32_t or_sa_value(const or_index_t *ix, const uint32_t *sa_values, uint32_t interval, uint32_t sa_index)
+{
+    uint32_t skipped = 0;
+    while (sa_index % interval != 0) {
+        ++skipped;
+        sa_index = psi_minus(&ix->f, sa_index);
+    }
+    return sa_values[sa_index / interval] + skipped;
+}
+
+/* BWTRetrievePositionFromSAIndex (2BWT-Interface.c:329-361): SA value, then the
+ * reference's binary search over the chromosome blocks (rows chrID, blockStart,
+ * blockEnd, ori; h starts at nblock).  seq_id / ori_pos are written only when a block
+ * holds the position.  Where the reference would read blockList[nblock] (past its
+ * end: undefined), the restatement stops as "not found". */
+void or_sa_position(const or_index_t *ix, const uint32_t *sa_values, uint32_t interval, const uint32_t *blocks,
+                    int n_blocks, uint32_t sa_index, uint32_t *seq_id, uint32_t *ori_pos, uint32_t *occ_pos)
+{
+    uint32_t occ = or_sa_value(ix, sa_values, interval, sa_index);
+    uint32_t l = 0, h = (uint32_t)n_blocks, m, start, end;
+    *occ_pos = occ;
+    while (l <= h) {
+        m = (h + l) >> 1;
+        if (m >= (uint32_t)n_blocks) break;
+        if ((start = blocks[4 * m + 1]) > occ) {
+            h = m - 1;
+        } else if ((end = blocks[4 * m + 2]) < occ) {
+            l = m + 1;
+        } else if (start <= occ && end >= occ) {
+            *seq_id = blocks[4 * m];
+            *ori_pos = occ - start + blocks[4 * m + 3] + 1;
+            break;
+        } else {
+            break;
+        }
+    }
+}
+
 /* BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235-272). */
 static void step_all(or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl,
                      uint32_t ok[4], uint32_t ol[4], uint32_t ork[4], uint32_t orl[4])

@@ -45,6 +45,14 @@ void or_step_all(const or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint
 /* bwt_cal_width type 1 (bwtaln.c:73-98); width is 2*(len+1) words {w, bid}. */
 int or_cal_width(const or_index_t *ix, int len, const uint8_t *str, uint32_t *width);
 
+/* BWTSaValue (BWT.c:1195) on the forward BWT; sa_values as BWTLoad holds them
+ * (values[0] = -1). */
+uint32_t or_sa_value(const or_index_t *ix, const uint32_t *sa_values, uint32_t interval, uint32_t sa_index);
+/* BWTRetrievePositionFromSAIndex (2BWT-Interface.c:329); blocks: n_blocks rows of
+ * u32 (chrID, blockStart, blockEnd, ori).  seq_id/ori_pos written only when found. */
+void or_sa_position(const or_index_t *ix, const uint32_t *sa_values, uint32_t interval, const uint32_t *blocks,
+                    int n_blocks, uint32_t sa_index, uint32_t *seq_id, uint32_t *ori_pos, uint32_t *occ_pos);
+
 void or_init_opt(or_opt_t *o);                      /* gap_init_opt, bwtaln.c:21-44 */
 int or_cal_maxdiff(int l, double err, double thres); /* bwa_cal_maxdiff, bwtaln.c:46-58 */
 

@@ -17,6 +17,11 @@
  *       BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235) on (k,l,rk,rl).
  *   ref_probe width <prefix> <reads.bin> <out.bin>
  *       bwt_cal_width(type=1) (bwtaln.c:73) of every read: (len+1) x {u32 w, i32 bid}.
+ *   ref_probe sa    <prefix> <idx.bin> <out.bin>
+ *       BWTSaValue (BWT.c:1195) and BWTRetrievePositionFromSAIndex
+ *       (2BWT-Interface.c:329) of each SA index: u32 sa, i32 seqId, u32 ori_pos,
+ *       u32 occ_pos per index (seqId / ori_pos preset to -1: left untouched when
+ *       the block search finds nothing).
  *   ref_probe meta  <prefix>
  *       prints textLength, inverseSa0, C[0..4] of both BWTs and saInterval.
  *
@@ -194,6 +199,25 @@ static int cmd_width(int argc, char **argv)
     return 0;
 }
 
+static int cmd_sa(int argc, char **argv)
+{
+    Idx2BWT *bi = load_index(argv[1]);
+    size_t sz; uint32_t *in = (uint32_t *)slurp(argv[2], &sz);
+    uint32_t n = in[0];
+    FILE *out = fopen(argv[3], "wb");
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t idx = in[1 + i];
+        uint32_t v[4];
+        v[0] = BWTSaValue(bi->bwt, idx);
+        unsigned int sid = 0xffffffffu, ori = 0xffffffffu, occ = 0;
+        BWTRetrievePositionFromSAIndex(bi, idx, &sid, &ori, &occ);
+        v[1] = sid; v[2] = ori; v[3] = occ;
+        fwrite(v, 4, 4, out);
+    }
+    fclose(out);
+    return 0;
+}
+
 static int cmd_meta(int argc, char **argv)
 {
     Idx2BWT *bi = load_index(argv[1]);
@@ -216,6 +240,7 @@ int main(int argc, char **argv)
     if (!strcmp(argv[1], "step")) return cmd_step(argc - 1, argv + 1);
     if (!strcmp(argv[1], "width")) return cmd_width(argc - 1, argv + 1);
     if (!strcmp(argv[1], "meta")) return cmd_meta(argc - 1, argv + 1);
+    if (!strcmp(argv[1], "sa")) return cmd_sa(argc - 1, argv + 1);
     fprintf(stderr, "unknown command %s\n", argv[1]);
     return 1;
 }

@@ -5,7 +5,8 @@ import os
 import numpy as np
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-INDEX = {"tiny": os.path.join(GOLD, "index", "tiny.fa"), "rep": os.path.join(GOLD, "index", "rep.fa")}
+INDEX = {"tiny": os.path.join(GOLD, "index", "tiny.fa"), "rep": os.path.join(GOLD, "index", "rep.fa"),
+         "nrun": os.path.join(GOLD, "index", "nrun.fa")}
 
 
 def cases():

@@ -56,6 +56,10 @@ def lib():
                                         C.POINTER(Opt), np.ctypeslib.ndpointer(np.int32, flags="C"), u32p,
                                         C.POINTER(C.POINTER(C.c_uint32)), np.ctypeslib.ndpointer(np.uint64, flags="C")]
         L.or_free.argtypes = [C.c_void_p]
+        L.or_sa_value.restype = C.c_uint32
+        L.or_sa_value.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32]
+        L.or_sa_position.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_int, C.c_uint32,
+                                     C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -84,6 +88,20 @@ class OracleIndex:
     def step_all(self, k, l, rk, rl):
         out = [np.zeros(4, np.uint32) for _ in range(4)]
         lib().or_step_all(self.h, k, l, rk, rl, *out)
+        return out
+
+    def sa_positions(self, sa, blocks, idx):
+        """BWTSaValue + BWTRetrievePositionFromSAIndex per SA index: (sa, seq_id, ori_pos,
+        occ_pos), seq_id / ori_pos = 0xFFFFFFFF when no block holds the position."""
+        vals = np.ascontiguousarray(sa.values, np.uint32)
+        blk = np.ascontiguousarray(blocks, np.uint32).reshape(-1)
+        out = np.zeros((len(idx), 4), np.uint32)
+        sid, ori, occ = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        for j, i in enumerate(np.asarray(idx, np.uint64)):
+            sid.value = ori.value = 0xFFFFFFFF
+            lib().or_sa_position(self.h, vals, sa.interval, blk, len(blk) // 4, int(i), C.byref(sid), C.byref(ori),
+                                 C.byref(occ))
+            out[j] = (occ.value, sid.value, ori.value, occ.value)
         return out
 
     def cal_width(self, seq):

@@ -2,7 +2,7 @@
 import numpy as np
 import pytest
 
-from golden_io import INDEX, cases, load_case, parse_opts, split_hits
+from golden_io import GOLD, INDEX, cases, load_case, parse_opts, split_hits
 from hsa_amd import index_io
 from oracle_ctypes import OracleIndex, default_opt
 
@@ -89,3 +89,17 @@ def test_batch_matches_reference(name):
     exp = split_hits(g["n_aln"], g["hits"])
     bad = [i for i in range(len(got)) if not exp_splice[i] and not np.array_equal(got[i], exp[i])]
     assert not bad, f"{len(bad)} reads differ, first {bad[:5]}: got {got[bad[0]]} exp {exp[bad[0]]}"
+
+
+@pytest.mark.parametrize("name", ["nrun", "tiny"])
+def test_sa_position_matches_reference(name):
+    """BWTSaValue + BWTRetrievePositionFromSAIndex restated (R11): every SA index of
+    a genome with N-runs (blocks with 'ori' offsets) and a sample of the tiny one."""
+    g = np.load(f"{GOLD}/{name}_sa.npz")
+    fwd, rev = index_io.read_index(INDEX[name])
+    ox = OracleIndex(fwd, rev)
+    got = ox.sa_positions(index_io.read_sa(INDEX[name]), index_io.read_blocks(INDEX[name]), g["idx"])
+    assert np.array_equal(got[:, 0], g["sa"])
+    assert np.array_equal(got[:, 1], g["seq_id"])
+    assert np.array_equal(got[:, 2], g["ori_pos"])
+    assert np.array_equal(got[:, 3], g["occ_pos"])

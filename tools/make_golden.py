@@ -8,6 +8,7 @@ Every fixture is data: synthetic inputs plus the reference's outputs on them.
     python tools/make_golden.py            # tiny fixtures (committed)
     python tools/make_golden.py --ecoli    # E.coli-sized digests (committed)
     python tools/make_golden.py --dropin   # FASTQ + reference SAM for the drop-in test
+    python tools/make_golden.py --sa       # SA -> position golden values (R11)
 """
 from __future__ import annotations
 
@@ -320,10 +321,60 @@ def dropin_cases(work):
         json.dump(man, f, indent=1, sort_keys=True)
 
 
+def nrun_genome_fasta(path):
+    """A 3-record genome with N-runs: runs of >= 10 N split blocks, shorter runs become
+    'G' (HSP.c:275-285), so the block table has offsets ('ori') to restate."""
+    recs = []
+    g = synth.genome_codes(70000, 77)
+    lay = [(0, 21000, [(5000, 40), (12000, 7), (17000, 120)]),
+           (21000, 26000, [(3000, 10), (9000, 9), (15000, 300), (20000, 55)]),
+           (47000, 23000, [(1000, 15), (8000, 3), (14000, 1000)])]
+    with open(path, "wb") as f:
+        for r, (s0, n, runs) in enumerate(lay):
+            txt = bytearray(b"ACGT"[int(c)] for c in g[s0:s0 + n])
+            for p, k in runs:
+                txt[p:p + k] = b"N" * k
+            f.write(b">nr%d\n" % (r + 1))
+            for o in range(0, n, 80):
+                f.write(bytes(txt[o:o + 80]) + b"\n")
+
+
+def sa_cases(work):
+    """BWTSaValue + BWTRetrievePositionFromSAIndex golden values."""
+    idir = os.path.join(GOLD, "index")
+    fa = os.path.join(work, "nrun.fa")
+    nrun_genome_fasta(fa)
+    build_index(fa)
+    for e in INDEX_EXT:
+        shutil.copy(f"{fa}.index.{e}", os.path.join(idir, f"nrun.fa.index.{e}"))
+
+    def run(prefix, idx, name):
+        ib = os.path.join(work, "idx.bin")
+        with open(ib, "wb") as f:
+            f.write(np.uint32(len(idx)).tobytes())
+            f.write(np.asarray(idx, np.uint32).tobytes())
+        ob = os.path.join(work, "sa.bin")
+        sh(os.path.join(REF, "ref_probe"), "sa", prefix, ib, ob)
+        v = np.fromfile(ob, dtype=np.uint32).reshape(-1, 4)
+        np.savez_compressed(os.path.join(GOLD, name + ".npz"), idx=np.asarray(idx, np.uint32), sa=v[:, 0],
+                            seq_id=v[:, 1], ori_pos=v[:, 2], occ_pos=v[:, 3])
+        print(f"{name}: {len(idx)} SA indices")
+
+    T = int(np.fromfile(f"{fa}.index.bwt", dtype=np.uint32, count=5)[4])
+    run(fa, np.arange(0, T + 1), "nrun_sa")               # every SA index of the N-run genome
+    tiny = os.path.join(idir, "tiny.fa")
+    Tt = 200003
+    isa0 = int(np.fromfile(f"{tiny}.index.bwt", dtype=np.uint32, count=1)[0])
+    idx = set(range(0, 300)) | set(range(Tt - 300, Tt + 1)) | set(range(max(isa0 - 20, 0), min(isa0 + 20, Tt + 1)))
+    idx |= set(int(x) for x in (synth._u(123, 6000, 0) % np.uint64(Tt + 1)))
+    run(tiny, np.array(sorted(idx)), "tiny_sa")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ecoli", action="store_true")
     ap.add_argument("--dropin", action="store_true")
+    ap.add_argument("--sa", action="store_true")
     a = ap.parse_args()
     if not os.path.exists(os.path.join(REF, "ref_probe")):
         sys.exit("build oracle/_ref first: make -C oracle -f ref.mk")
@@ -333,6 +384,8 @@ def main():
             ecoli_cases(work)
         elif a.dropin:
             dropin_cases(work)
+        elif a.sa:
+            sa_cases(work)
         else:
             tiny_cases(work)
 
