@@ -482,6 +482,23 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
     }
 }
 
+/* bwt_match_gap (bwtgap.c:118-331) called directly, as bwt_splice_match does
+ * (bwtgap.c:812, :919, :1192): the caller's widths, mutated in place by gap_shadow
+ * (Q6); seed 0 = width_seed NULL, 1 = its own array, 2 = aliased to width
+ * (bwtgap.c:809).  The stack has the caller's n_stacks (aux->stack). */
+int or_match_gap(const or_index_t *cix, const or_opt_t *opt, int n_stacks, const uint8_t *seq, int len, int strand,
+                 uint32_t *width, int seed, const uint32_t *width_seed, uint32_t **hits)
+{
+    or_index_t *ix = (or_index_t *)cix;
+    stack_t_ *st = stack_new(n_stacks);
+    hitv_t hv = {0, 0, NULL};
+    const uint32_t *ws = seed == 2 ? width : seed == 1 ? width_seed : NULL;
+    match_gap(ix, st, opt, seq, len, strand, width, ws, &hv, NULL);
+    stack_del(st);
+    *hits = hv.a ? hv.a : (uint32_t *)calloc(9, sizeof(uint32_t));
+    return hv.n;
+}
+
 static void revcomp(int len, const uint8_t *s, uint8_t *d)   /* seq_reverse(.., 1), bwaseqio.c:73-84 */
 {
     for (int i = 0; i < len; ++i) {

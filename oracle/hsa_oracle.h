@@ -64,6 +64,13 @@ int or_cal_maxdiff(int l, double err, double thres); /* bwa_cal_maxdiff, bwtaln.
 long or_cal_sa_reg_gap(const or_index_t *ix, int n, const uint32_t *lens, const uint8_t *codes,
                        or_opt_t *opt, int32_t *n_aln, uint32_t *flags, uint32_t **hits,
                        uint64_t *stats);
+/* bwt_match_gap (bwtgap.c:118-331) with caller-supplied widths, as bwt_splice_match
+ * calls it.  width: 2*(len+1) words {w, bid}, mutated by gap_shadow (bwtgap.c:217).
+ * seed: 0 = width_seed NULL, 1 = width_seed (2*(opt->seed_len+1) words),
+ * 2 = width_seed aliases width (bwtgap.c:809).  n_stacks = aux->stack->n_stacks.
+ * Returns n_aln; *hits (9 u32 per bwt_aln1_t, start/end 0) is malloc'd. */
+int or_match_gap(const or_index_t *ix, const or_opt_t *opt, int n_stacks, const uint8_t *seq, int len, int strand,
+                 uint32_t *width, int seed, const uint32_t *width_seed, uint32_t **hits);
 void or_free(void *p);
 
 #ifdef __cplusplus

@@ -15,7 +15,7 @@ REFOBJS   = bwtaln bwtgap BWT BWTConstruct utils dictionary DNACount HSP inipars
             bamlite 2BWT-Interface bwaseqio r250 cs2nt bwtse kstring stdaln bwt_array
 OBJS      = $(addprefix $(OUT)/obj/,$(addsuffix .o,$(REFOBJS)))
 
-all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/HSA_gpu
+all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/ref_mgcap $(OUT)/HSA_gpu $(OUT)/HSA_gpu_mg
 
 $(OUT)/obj/%.o: $(REF)/%.c
 	@mkdir -p $(OUT)/obj
@@ -47,6 +47,34 @@ $(OUT)/obj/bwtaln_weak.o: $(OUT)/obj/bwtaln.o
 
 $(OUT)/HSA_gpu: $(OUT)/obj/main.o $(WEAKOBJS) $(GPUOBJ) $(GPULIB)
 	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(WEAKOBJS) $(GPUOBJ) -L$(dir $(GPULIB)) -lhsa_gpu \
+	    -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
+
+# ref_mgcap.c is ours: it records every bwt_match_gap call (inputs, widths before and
+# after, hits).  bwtgap.o enters twice: weakened, so that every call -- including
+# bwt_splice_match's own, which go through the PLT under -fPIC -- reaches the
+# recorder; and renamed (ref_bwt_match_gap) with every other global made local, the
+# unmodified reference function the recorder calls.
+$(OUT)/obj/bwtgap_weak.o: $(OUT)/obj/bwtgap.o
+	objcopy --weaken-symbol=bwt_match_gap $< $@
+
+$(OUT)/obj/bwtgap_ren.o: $(OUT)/obj/bwtgap.o
+	objcopy --redefine-sym bwt_match_gap=ref_bwt_match_gap $< $@.tmp
+	objcopy --keep-global-symbol=ref_bwt_match_gap $@.tmp $@
+	rm -f $@.tmp
+
+CAPOBJS   = $(filter-out $(OUT)/obj/bwtgap.o,$(OBJS)) $(OUT)/obj/bwtgap_weak.o $(OUT)/obj/bwtgap_ren.o
+
+$(OUT)/ref_mgcap: ref_mgcap.c $(CAPOBJS)
+	$(CC) $(REFFLAGS) -I$(REF) ref_mgcap.c $(CAPOBJS) -lm -lz -o $@
+
+# HSA_gpu_mg: as HSA_gpu, with bwt_match_gap weakened too, so the host's splice path
+# (bwt_splice_match, bwtgap.c:748) calls OUR bwt_match_gap for its seed and anchor
+# searches (bwtgap.c:812, :919, :1192).
+MGOBJS    = $(filter-out $(OUT)/obj/bwtaln.o $(OUT)/obj/bwtgap.o,$(OBJS)) $(OUT)/obj/bwtaln_weak.o \
+            $(OUT)/obj/bwtgap_weak.o
+
+$(OUT)/HSA_gpu_mg: $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPULIB)
+	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) -L$(dir $(GPULIB)) -lhsa_gpu \
 	    -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
 
 clean:

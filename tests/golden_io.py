@@ -80,6 +80,29 @@ def main_path_digest(n_aln, flags, hits):
     return h.hexdigest()
 
 
+MGCAP_CASES = ["mgcap_default", "mgcap_n4o1"]
+
+
+def load_mgcap(name):
+    """bwt_match_gap calls recorded from the reference (tools/make_golden.py --mgcap):
+    per call strand, len, seed kind (0 NULL, 1 own, 2 aliased), n_stacks, the option
+    block, the searched sequence, widths before/after and the hits."""
+    z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    hdr, opt = z["hdr"], z["opt"]
+    L = hdr[:, 1].astype(np.int64)
+    so = np.concatenate([[0], np.cumsum(L)])
+    wo = np.concatenate([[0], np.cumsum(L + 1)])
+    sd = np.concatenate([[0], np.cumsum(hdr[:, 4].astype(np.int64))])
+    ho = np.concatenate([[0], np.cumsum(np.maximum(z["n_aln"], 0).astype(np.int64))])
+    calls = []
+    for j in range(len(hdr)):
+        calls.append(dict(strand=int(hdr[j, 0]), len=int(L[j]), seed=int(hdr[j, 2]), n_stacks=int(hdr[j, 3]),
+                          opt=opt[j].copy(), seq=z["seq"][so[j]:so[j + 1]],
+                          wb=z["wb"][wo[j]:wo[j + 1]], ws=z["ws"][sd[j]:sd[j + 1]],
+                          hits=z["hits"][ho[j]:ho[j + 1]], wo=z["wo"][wo[j]:wo[j + 1]]))
+    return calls
+
+
 def ecoli_manifest():
     with open(os.path.join(GOLD, "manifest_ecoli.json")) as f:
         return json.load(f)

@@ -56,6 +56,10 @@ def lib():
                                         C.POINTER(Opt), np.ctypeslib.ndpointer(np.int32, flags="C"), u32p,
                                         C.POINTER(C.POINTER(C.c_uint32)), np.ctypeslib.ndpointer(np.uint64, flags="C")]
         L.or_free.argtypes = [C.c_void_p]
+        i32p = np.ctypeslib.ndpointer(np.int32, flags="C")
+        L.or_match_gap.restype = C.c_int
+        L.or_match_gap.argtypes = [C.c_void_p, C.POINTER(Opt), C.c_int, np.ctypeslib.ndpointer(np.uint8, flags="C"),
+                                   C.c_int, C.c_int, i32p, C.c_int, C.c_void_p, C.POINTER(C.POINTER(C.c_uint32))]
         L.or_sa_value.restype = C.c_uint32
         L.or_sa_value.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32]
         L.or_sa_position.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_int, C.c_uint32,
@@ -109,6 +113,19 @@ class OracleIndex:
         w = np.zeros(2 * (len(seq) + 1), np.uint32)
         lib().or_cal_width(self.h, len(seq), seq, w)
         return w.reshape(-1, 2)
+
+    def match_gap(self, opt: Opt, n_stacks, seq, strand, width, seed, width_seed=None):
+        """bwt_match_gap with caller widths (or_match_gap): width (len+1, 2) int32 is
+        copied, returns (hits (n, 9), width after gap_shadow)."""
+        seq = np.ascontiguousarray(seq, np.uint8)
+        w = np.ascontiguousarray(width, np.int32).copy()
+        ws = np.ascontiguousarray(width_seed, np.int32) if seed == 1 else None
+        hp = C.POINTER(C.c_uint32)()
+        n = lib().or_match_gap(self.h, C.byref(opt), int(n_stacks), seq, len(seq), int(strand), w, int(seed),
+                               ws.ctypes.data if ws is not None else None, C.byref(hp))
+        hits = np.ctypeslib.as_array(hp, shape=(max(n, 1) * 9,))[:n * 9].reshape(n, 9).copy()
+        lib().or_free(hp)
+        return hits, w
 
     def cal_sa_reg_gap(self, lens, codes, opt: Opt):
         """One batch; returns (n_aln, flags, hits(H,9), stats[queries, pops]); mutates opt."""

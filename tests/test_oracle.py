@@ -91,6 +91,26 @@ def test_batch_matches_reference(name):
     assert not bad, f"{len(bad)} reads differ, first {bad[:5]}: got {got[bad[0]]} exp {exp[bad[0]]}"
 
 
+@pytest.mark.parametrize("name", ["mgcap_default", "mgcap_n4o1"])
+def test_match_gap_calls_match_reference(name):
+    """bwt_match_gap called with caller widths, restated (or_match_gap): every call the
+    reference's splice path made (aliased seeds, NULL-seed anchors) and a sample of
+    main-path calls -- hits word for word, and the widths after gap_shadow (Q6)."""
+    from golden_io import load_mgcap
+    from oracle_ctypes import Opt
+    ix = oracle_index("tiny")
+    calls = load_mgcap(name)
+    kinds = {c["seed"] for c in calls}
+    assert kinds == {0, 1, 2}, kinds
+    bad = []
+    for j, c in enumerate(calls):
+        opt = Opt.from_buffer_copy(c["opt"].tobytes())
+        hits, w = ix.match_gap(opt, c["n_stacks"], c["seq"], c["strand"], c["wb"], c["seed"], c["ws"])
+        if not (np.array_equal(hits, c["hits"]) and np.array_equal(w, c["wo"])):
+            bad.append(j)
+    assert not bad, f"{len(bad)} of {len(calls)} calls differ, first {bad[:5]}"
+
+
 @pytest.mark.parametrize("name", ["nrun", "tiny"])
 def test_sa_position_matches_reference(name):
     """BWTSaValue + BWTRetrievePositionFromSAIndex restated (R11): every SA index of

@@ -370,11 +370,101 @@ def sa_cases(work):
     run(tiny, np.array(sorted(idx)), "tiny_sa")
 
 
+def read_mgcap(path):
+    """Records of oracle/ref_mgcap.c: every bwt_match_gap call of a reference run."""
+    raw = open(path, "rb").read()
+    assert raw[:4] == b"MGCP"
+    o = 4
+    recs = []
+    while o < len(raw):
+        hdr = np.frombuffer(raw[o:o + 20], np.int32).copy()
+        o += 20
+        strand, L, seed, n_stacks, n_seed = (int(x) for x in hdr)
+        opt = np.frombuffer(raw[o:o + 64], np.uint32).copy()
+        o += 64
+        seq = np.frombuffer(raw[o:o + L], np.uint8).copy()
+        o += L
+        wb = np.frombuffer(raw[o:o + 8 * (L + 1)], np.int32).reshape(L + 1, 2).copy()
+        o += 8 * (L + 1)
+        ws = np.frombuffer(raw[o:o + 8 * n_seed], np.int32).reshape(n_seed, 2).copy()
+        o += 8 * n_seed
+        na = int(np.frombuffer(raw[o:o + 4], np.int32)[0])
+        o += 4
+        hits = np.frombuffer(raw[o:o + 36 * max(na, 0)], np.uint32).reshape(-1, 9).copy()
+        o += 36 * max(na, 0)
+        wo = np.frombuffer(raw[o:o + 8 * (L + 1)], np.int32).reshape(L + 1, 2).copy()
+        o += 8 * (L + 1)
+        recs.append(dict(hdr=hdr, opt=opt, seq=seq, wb=wb, ws=ws, n_aln=na, hits=hits, wo=wo))
+    return recs
+
+
+def mgcap_cases(work):
+    """bwt_match_gap called directly with caller widths: every call the
+    reference makes on the drop-in read set -- the splice path's seed searches
+    (width_seed aliased to width_back, bwtgap.c:809-812), its 12-mer anchors (width_seed
+    NULL, :919 and :1192) -- plus a sample of main-path calls (own width_seed)."""
+    T, seed = 200003, 7
+    g = synth.genome_codes(T, seed)
+    rec = synth.record_layout(T, 3)
+    seqs = []
+    r, _ = synth.make_reads(g, rec, 60, 100, 41, max_mm=4)
+    seqs += list(r)
+    r, _ = synth.make_reads(g, rec, 60, 100, 42, indel=True, max_mm_indel=2)
+    seqs += list(r)
+    for i in range(400):   # spliced: exon A + exon B 200-2000 bp downstream
+        st = int(synth._u(43, 1, i)[0] % np.uint64(T - 3000))
+        L = (100, 150, 75, 120)[i % 4]
+        cut = 30 + (i * 7) % (L - 50)
+        intron = 200 + (i * 37) % 1800
+        s = np.concatenate([g[st:st + cut], g[st + cut + intron:st + L + intron]]).astype(np.uint8)
+        if i % 5 == 1:
+            s = synth.revcomp_codes(s)
+        if i % 7 == 3:
+            s[(i * 13) % L] = (s[(i * 13) % L] + 1) % 4
+        seqs.append(s)
+    # the anchor call at bwtgap.c:1192 needs seeds 1 and 2 mapped > 50 bp apart with
+    # seed 0 unmapped (seg_mtype 6): reads of 180-210 bp (seed_len >= 60) whose
+    # junction lies inside the first third
+    for i in range(200):
+        st = int(synth._u(44, 1, i)[0] % np.uint64(T - 3000))
+        L = 180 + 10 * (i % 4)
+        cut = 15 + (i * 11) % 30
+        intron = 300 + (i * 53) % 1500
+        s = np.concatenate([g[st:st + cut], g[st + cut + intron:st + L + intron]]).astype(np.uint8)
+        seqs.append(synth.revcomp_codes(s) if i % 2 else s)
+    rb = os.path.join(work, "mg_reads.bin")
+    synth.write_reads_bin(rb, seqs)
+    idx = os.path.join(GOLD, "index", "tiny.fa")
+    for name, args in (("mgcap_default", []), ("mgcap_n4o1", ["-n", "4", "-o", "1"])):
+        ob = os.path.join(work, name + ".bin")
+        r = subprocess.run([os.path.join(REF, "ref_mgcap"), idx, rb, ob, *args], check=True, capture_output=True,
+                           text=True)
+        recs = read_mgcap(ob)
+        main = [x for x in recs if x["hdr"][2] == 1]
+        keep = [x for x in recs if x["hdr"][2] != 1] + main[:300]
+        hdr = np.stack([x["hdr"] for x in keep])
+        cnt = np.bincount(hdr[:, 2], minlength=3)
+        out = dict(hdr=hdr, opt=np.stack([x["opt"] for x in keep]),
+                   seq=np.concatenate([x["seq"] for x in keep]),
+                   wb=np.concatenate([x["wb"] for x in keep]),
+                   ws=np.concatenate([x["ws"] for x in keep]) if any(len(x["ws"]) for x in keep) else
+                   np.zeros((0, 2), np.int32),
+                   n_aln=np.array([x["n_aln"] for x in keep], np.int32),
+                   hits=np.concatenate([x["hits"] for x in keep]),
+                   wo=np.concatenate([x["wo"] for x in keep]))
+        np.savez_compressed(os.path.join(GOLD, name + ".npz"), **out)
+        changed = sum(int(not np.array_equal(x["wb"], x["wo"])) for x in keep)
+        print(f"{name}: {len(recs)} calls recorded ({r.stderr.strip()}); kept {len(keep)}: "
+              f"{cnt[0]} width_seed NULL, {cnt[2]} aliased, {cnt[1]} own; {int((out['n_aln'] > 0).sum())} with hits, "
+              f"{changed} with widths changed by gap_shadow")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ecoli", action="store_true")
     ap.add_argument("--dropin", action="store_true")
     ap.add_argument("--sa", action="store_true")
+    ap.add_argument("--mgcap", action="store_true")
     a = ap.parse_args()
     if not os.path.exists(os.path.join(REF, "ref_probe")):
         sys.exit("build oracle/_ref first: make -C oracle -f ref.mk")
@@ -386,6 +476,8 @@ def main():
             dropin_cases(work)
         elif a.sa:
             sa_cases(work)
+        elif a.mgcap:
+            mgcap_cases(work)
         else:
             tiny_cases(work)
 
