@@ -25,7 +25,8 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_search_batch", "hsa_search_device", "hsa_configure", "hsa_free", "hsa_synth_genome_device",
     "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
     "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather", "hsa_last_pass_ms",
-    "hsa_index_set_sa", "hsa_sa_position_batch", "hsa_sa_position_device",
+    "hsa_index_set_sa", "hsa_sa_position_batch", "hsa_sa_position_device", "hsa_match_gap_batch",
+    "bwt_match_gap", "bwt_match_gap_batch",
 ]
 
 
@@ -67,6 +68,21 @@ class Regime(C.Structure):
 
 JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("max_diff", "<i4"), ("seed_len", "<i4"),
                       ("regime", "<i4")])
+# hsa_mg_job_t (include/hsa_gpu.h): one direct bwt_match_gap call's widths and strand
+MG_DTYPE = np.dtype([("wb_off", "<u8"), ("ws_off", "<u8"), ("strand", "<i4"), ("seed", "<i4")])
+SEED_NONE, SEED_OWN, SEED_ALIAS = 0, 1, 2
+
+
+def regime_of(opt: dict, n_stacks: int, max_diff: int) -> "Regime":
+    """The fields of one option block bwt_match_gap reads (bwtaln_gpu.c hsa_regime_of)."""
+    mode = opt["mode"] & (0x01 | 0x04 | 0x10)
+    if opt["max_gapo"] == 0:
+        mode &= ~(0x01 | 0x04)
+    return Regime(s_mm=opt["s_mm"], s_gapo=opt["s_gapo"], s_gape=opt["s_gape"], mode=mode,
+                  indel_end_skip=opt["indel_end_skip"], max_del_occ=opt["max_del_occ"],
+                  max_entries=opt["max_entries"], max_gapo=opt["max_gapo"], max_gape=opt["max_gape"],
+                  max_seed_diff=opt["max_seed_diff"], max_top2=opt["max_top2"], n_stacks=n_stacks,
+                  max_diff=max_diff)
 
 
 class Stats(C.Structure):
@@ -141,6 +157,9 @@ def lib():
     L.hsa_sa_position_batch.argtypes = [vp, C.c_size_t, u32, u32]
     L.hsa_probe_gather.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
     L.hsa_build_bwt_device.argtypes = [C.c_int, C.c_uint64, vp, C.c_int, vp, C.POINTER(C.c_uint32), u32]
+    L.hsa_match_gap_batch.restype = C.c_long
+    L.hsa_match_gap_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, vp, C.c_int, u8, C.c_size_t, i32, C.c_size_t,
+                                      i32, i32, u64, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(Stats)]
     L.hsa_cal_sa_reg_gap_flat.restype = C.c_long
     L.hsa_cal_sa_reg_gap_flat.argtypes = [vp, C.POINTER(GapOpt), C.c_int, u32, u64, u8, C.c_size_t, i32, u32, u64,
                                           C.POINTER(C.POINTER(C.c_uint32)), i32, C.POINTER(Stats)]
@@ -279,6 +298,25 @@ class GpuIndex:
         tot = check(lib().hsa_search_batch(self.h, rg, len(regimes), jobs.ctypes.data, n, codes, len(codes), n_aln,
                                            flags, hoff, C.byref(hp), C.byref(st)))
         return n_aln, flags, hoff, _take_hits(hp, tot), st.as_dict()
+
+    def match_gap(self, regimes, jobs, mg, codes, widths):
+        """hsa_match_gap_batch: direct bwt_match_gap calls with caller widths.
+        widths (P, 2) int32 pairs; returns (n_aln, hit_off, hits, widths after, stats)."""
+        jobs = np.ascontiguousarray(jobs, JOB_DTYPE)
+        mg = np.ascontiguousarray(mg, MG_DTYPE)
+        n = len(jobs)
+        rg = (Regime * len(regimes))(*regimes)
+        w = np.ascontiguousarray(widths, np.int32).reshape(-1)
+        wout = w.copy()
+        n_aln = np.zeros(n, np.int32)
+        hoff = np.zeros(n, np.uint64)
+        hp = C.POINTER(C.c_uint32)()
+        st = Stats()
+        codes = np.ascontiguousarray(codes, np.uint8)
+        tot = check(lib().hsa_match_gap_batch(self.h, rg, len(regimes), jobs.ctypes.data, mg.ctypes.data, n, codes,
+                                              len(codes), w, len(w) // 2, wout, n_aln, hoff, C.byref(hp),
+                                              C.byref(st)))
+        return n_aln, hoff, _take_hits(hp, tot), wout.reshape(-1, 2), st.as_dict()
 
     def cal_sa_reg_gap(self, lens, codes, opt: GapOpt):
         """bwa_cal_sa_reg_gap semantics over one batch (mutates opt like the reference)."""

@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include "../../include/hsa_bwtaln.h"
+#include "bwtaln_gpu.h"
 
 _Static_assert(sizeof(bwt_aln1_t) == 36, "bwt_aln1_t layout");
 _Static_assert(sizeof(gap_opt_t) == 64, "gap_opt_t layout");
@@ -54,9 +55,9 @@ static int cal_maxdiff(int l, double err, double thres)
     return 2;
 }
 
-static int aln_score(const gap_opt_t *o, int m, int g, int e) { return m * o->s_mm + g * o->s_gapo + e * o->s_gape; }
+int hsa_aln_score(const gap_opt_t *o, int m, int g, int e) { return m * o->s_mm + g * o->s_gapo + e * o->s_gape; }
 
-static hsa_regime_t regime_of(const gap_opt_t *o, int n_stacks, int max_diff)
+hsa_regime_t hsa_regime_of(const gap_opt_t *o, int n_stacks, int max_diff)
 {
     hsa_regime_t r;
     memset(&r, 0, sizeof r);
@@ -171,9 +172,9 @@ long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint3
     }
     if (opt->fnr > 0.0) local.max_diff = cal_maxdiff(max_len, BWA_AVG_ERR, opt->fnr);
     if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;
-    const int n_stacks = aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
+    const int n_stacks = hsa_aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
     /* every per-read max_diff of the call is <= local_opt.max_diff (bwtaln.c:264-267) */
-    hsa_regime_t rg[2] = {regime_of(opt, n_stacks, local.max_diff), regime_of(&local, n_stacks, local.max_diff)};
+    hsa_regime_t rg[2] = {hsa_regime_of(opt, n_stacks, local.max_diff), hsa_regime_of(&local, n_stacks, local.max_diff)};
     const int equivalent = same_len && memcmp(&rg[0], &rg[1], sizeof rg[0]) == 0;
 
     int8_t *kind = (int8_t *)malloc((size_t)n + 1);
@@ -287,6 +288,18 @@ void hsa_gpu_detach(const Idx2BWT *bi)
     pthread_mutex_unlock(&g_att_mu);
 }
 
+/* The device index of a loaded Idx2BWT, attached on first use (bwtaln_gpu.h). */
+hsa_index_t *hsa_gpu_index_of(const Idx2BWT *bi)
+{
+    hsa_index_t *ix = lookup(bi);
+    if (!ix) {
+        long rc = hsa_gpu_attach(bi);
+        if (rc) hsa_gpu_fatal("hsa_gpu_attach", rc);
+        ix = lookup(bi);
+    }
+    return ix;
+}
+
 /* gap_init_stack layout (bwtgap.c:13-27), for the host's bwt_splice_match */
 static gap_stack_t *ref_stack_new(int n_stacks)
 {
@@ -307,7 +320,7 @@ static void ref_stack_free(gap_stack_t *s)
     free(s);
 }
 
-static void fatal(const char *what, long rc)
+void hsa_gpu_fatal(const char *what, long rc)
 {
     /* the reference's convention for unrecoverable errors: message + exit(1) */
     fprintf(stderr, "[bwa_cal_sa_reg_gap] %s failed (%ld): %s\n", what, rc, hsa_last_error());
@@ -319,12 +332,7 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
 {
     (void)tid;
     gap_opt_t *opt = (gap_opt_t *)copt;     /* mutated, as the reference does through aux->opt */
-    hsa_index_t *ix = lookup(bi_bwt);
-    if (!ix) {
-        long rc = hsa_gpu_attach(bi_bwt);
-        if (rc) fatal("hsa_gpu_attach", rc);
-        ix = lookup(bi_bwt);
-    }
+    hsa_index_t *ix = hsa_gpu_index_of(bi_bwt);
     uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)n_seqs + 1));
     uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n_seqs + 1));
     size_t tot = 0;
@@ -342,7 +350,7 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     gap_opt_t local = *opt;                 /* local_opt as of :254, before the call mutates *opt */
     uint32_t *hits = NULL;
     long nh = hsa_cal_sa_reg_gap_flat(ix, opt, n_seqs, lens, offs, codes, tot, n_aln, flags, hoff, &hits, sp, NULL);
-    if (nh < 0) fatal("GPU search", nh);
+    if (nh < 0) hsa_gpu_fatal("GPU search", nh);
     if (opt->fnr > 0.0) local.max_diff = cal_maxdiff(max_len, BWA_AVG_ERR, opt->fnr);
     if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;
 

@@ -1,0 +1,16 @@
+/* bwtaln_gpu.h -- internals shared by the reference-ABI host sources (bwtaln_gpu.c,
+ * bwtgap_gpu.c).  Not part of the public boundary (include/). */
+#ifndef BWTALN_GPU_H
+#define BWTALN_GPU_H
+#include "../../include/hsa_bwtaln.h"
+
+/* the device index of a loaded Idx2BWT, attached on first use */
+hsa_index_t *hsa_gpu_index_of(const Idx2BWT *bi);
+/* the reference's convention for unrecoverable errors: message + exit(1) */
+void hsa_gpu_fatal(const char *what, long rc) __attribute__((noreturn));
+/* aln_score (bwtgap.h) */
+int hsa_aln_score(const gap_opt_t *o, int m, int g, int e);
+/* the search options of one option block (the fields bwt_match_gap reads) */
+hsa_regime_t hsa_regime_of(const gap_opt_t *o, int n_stacks, int max_diff);
+
+#endif

@@ -88,6 +88,13 @@ struct SearchArgs {
     int32_t *ovf_list;
     const unsigned long long *n_dev;
     uint32_t qctr;
+    // caller-width mode (hsa_match_gap_batch, bwt_match_gap called directly): per job
+    // strand and width_seed kind; k_widths_import builds the rows from the caller's
+    // bwt_width_t pairs (cw), the search takes that one strand, and gap_shadow keeps
+    // the full bid values (wbid) so the mutated widths can be handed back
+    const hsa_mg_job_t *mg;
+    int32_t *cw;
+    int32_t *wbid;
 };
 
 // entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
@@ -103,12 +110,13 @@ __device__ __forceinline__ uint32_t meta_pack(uint32_t i, uint32_t st, uint32_t 
 #define M_GO(m) ((int)(((m) >> 20) & 15u))
 #define M_GE(m) ((int)((m) >> 24))
 
-// control word: ph:3 | strand:1 | has_seed:1 | reg:1 | has_vt:1 | -:1 | ovf:2 | len:10 | seed_len:10
+// control word: ph:3 | strand:1 | has_seed:1 | reg:1 | has_vt:1 | seed_alias:1 | ovf:2 | len:10 | seed_len:10
 #define C_PH(c) ((c) & 7u)
 #define C_STRAND(c) (((c) >> 3) & 1u)
 #define C_SEED(c) (((c) >> 4) & 1u)
 #define C_REG(c) (((c) >> 5) & 1u)
 #define C_VT(c) (((c) >> 6) & 1u)
+#define C_ALIAS(c) (((c) >> 7) & 1u)
 #define C_OVF(c) (((c) >> 8) & 3u)
 #define C_LEN(c) ((int)(((c) >> 10) & 1023u))
 #define C_SLEN(c) ((int)(((c) >> 20) & 1023u))
@@ -271,6 +279,66 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
     atomicAdd(&a.ctr[7], (unsigned long long)st_q);
 }
 
+// Caller-width mode: the width rows of each call from the caller's bwt_width_t pairs
+// (hsa_match_gap_batch) -- the same element format and row layout k_widths writes;
+// the row of list position q is q * 2 + strand.  Besides the pruning elements and the
+// full w values, the full bids go to wbid: gap_shadow rewrites them (bwtgap.c:101).
+template <typename WT>
+__global__ void __launch_bounds__(BLOCK) k_widths_import(SearchArgs a)
+{
+    using F = WFmt<WT>;
+    const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    if (q >= n_jobs) return;
+    const int job = a.job_list ? a.job_list[q] : (int)q;
+    const hsa_job_t J = a.jobs[job];
+    const hsa_mg_job_t M = a.mg[job];
+    const uint32_t R = q * 2u + (uint32_t)(M.strand & 1);
+    const size_t rb = R >> 6, rl = R & 63u;
+    uint32_t *const brow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.wb)) + rb * (a.rb / 4) * 64 + rl;
+    uint32_t *const srow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.ws)) + rb * (a.rs / 4) * 64 + rl;
+    uint32_t *const wrow = a.wg + rb * a.rg * 64 + rl;
+    int32_t *const drow = a.wbid + rb * a.rg * 64 + rl;
+    // elements 0..n of one row; element t: min(bid, BIDM) | (w[t] == w[t+1]) | base code
+    auto emit = [&](uint32_t *row, const int32_t *w, uint32_t n, bool read_row) {
+        uint32_t acc = 0;
+        uint32_t wt = (uint32_t)w[0];
+        for (uint32_t t = 0; t <= n; ++t) {
+            const uint32_t bid = (uint32_t)w[2 * t + 1];
+            const uint32_t wn = t < n ? (uint32_t)w[2 * t + 2] : 0u;
+            uint32_t e = bid < F::BIDM ? bid : F::BIDM;
+            if (t < n && wt == wn) e |= F::EQ;
+            if (read_row && t < n) e |= F::code_bits(a.codes[J.off + t]);
+            acc |= e << ((t % F::EPW) * F::EB);
+            if (t % F::EPW == F::EPW - 1 || t == n) { row[(t / F::EPW) * 64] = acc; acc = 0; }
+            if (read_row) { wrow[t * 64] = wt; drow[t * 64] = (int32_t)bid; }
+            wt = wn;
+        }
+    };
+    emit(brow, a.cw + 2 * M.wb_off, J.len, true);
+    if (M.seed == HSA_SEED_OWN) emit(srow, a.cw + 2 * M.ws_off, (uint32_t)J.seed_len, false);
+}
+
+// Caller-width mode: width_back after the search (gap_shadow rewrote it in the rows)
+// back into the caller's pairs.  Reads that overflowed this pass are skipped: the
+// re-run that completes them exports them.
+__global__ void __launch_bounds__(BLOCK) k_widths_export(SearchArgs a)
+{
+    const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
+    if (q >= (uint32_t)a.n_jobs) return;
+    const int job = a.job_list ? a.job_list[q] : (int)q;
+    if (a.flags[job] & HSA_F_OVERFLOW) return;
+    const hsa_job_t J = a.jobs[job];
+    const hsa_mg_job_t M = a.mg[job];
+    const uint32_t R = q * 2u + (uint32_t)(M.strand & 1);
+    const size_t base = (R >> 6) * (size_t)a.rg * 64 + (R & 63u);
+    int32_t *const o = a.cw + 2 * M.wb_off;
+    for (uint32_t t = 0; t <= J.len; ++t) {
+        o[2 * t] = (int32_t)a.wg[base + t * 64];
+        o[2 * t + 1] = a.wbid[base + t * 64];
+    }
+}
+
 #ifdef HSA_DIAG
 // Diagnostic build only (-DHSA_DIAG, never the product library): per-workgroup
 // start/end s_memtime and s_memrealtime of the last launch, for the in-kernel
@@ -412,7 +480,7 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
         const uint32_t nwb = a.rb / 4;                 // row capacity in words (uniform)
         for (uint32_t q = 0; q < nwb; ++q)
             __builtin_amdgcn_global_load_lds(src + q * 64, db + q * BLOCK, 4, 0, 0);
-        if (C_SEED(ctl)) {
+        if (C_SEED(ctl) && !C_ALIAS(ctl)) {
             const uint32_t *ss = reinterpret_cast<const uint32_t *>(a.ws) + row_base(a.rs / 4);
             uint32_t *const ds = reinterpret_cast<uint32_t *>(s_ws) + (tid & ~63u);
             const uint32_t nws = a.rs / 4;
@@ -445,10 +513,13 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                 dst[h * 9 + 4] = HB(h * 9 + 4);
                 dst[h * 9 + 5] = s30;
                 dst[h * 9 + 6] = 0;
-                dst[h * 9 + 7] = h == 0 ? (uint32_t)(C_LEN(ctl) - 1) : 0u;   // bwtaln.c:371-372
+                // bwtaln.c:371-372 (a direct bwt_match_gap call leaves start/end 0)
+                dst[h * 9 + 7] = h == 0 && !a.mg ? (uint32_t)(C_LEN(ctl) - 1) : 0u;
                 dst[h * 9 + 8] = HB(h * 9 + 8);
             }
             finish_job(0, n_aln, o);
+        } else if (a.mg) {
+            finish_job(0, 0, 0);        // one call, one strand
         } else if (C_STRAND(ctl)) {
             ctl &= ~(1u << 3);          // strand 0
             start_strand();
@@ -484,12 +555,17 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                 DC(13); dc[14] += (uint32_t)ldp;
 #endif
                 uint32_t *const wg = a.wg + row_base(a.rg);
+                int32_t *const wd = a.wbid ? a.wbid + row_base(a.rg) : nullptr;
 #define WG(p) wg[(uint32_t)(p) * 64]
                 uint32_t jj = 0;
                 for (int p = 0; p < ldp; ++p) {
                     uint32_t w = WG(p);
                     if (w > x) { w -= x; WG(p) = w; }
-                    else if (w == x) { WB(p) = (WT)((WB(p) & ~F::BIDM) | 1u); WG(p) = a.T - (++jj); }
+                    else if (w == x) {
+                        WB(p) = (WT)((WB(p) & ~F::BIDM) | 1u);
+                        WG(p) = a.T - (++jj);
+                        if (wd) wd[(uint32_t)p * 64] = 1;
+                    }
                 }
                 uint32_t wnext = WG(ldp);
                 for (int p = ldp - 1; p >= 0; --p) {
@@ -530,12 +606,23 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
                     if (j < (unsigned long long)n_jobs) {
                         qpos = (uint32_t)j;
-                        const hsa_job_t J = a.jobs[a.job_list ? a.job_list[j] : (int)j];
+                        const int job = a.job_list ? a.job_list[j] : (int)j;
+                        const hsa_job_t J = a.jobs[job];
                         opt_max_diff = J.max_diff;
                         const uint32_t len = J.len;
-                        const uint32_t has_seed = (int)len > J.seed_len;
-                        ctl = 8u | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 | len << 10 |
-                              (has_seed ? (uint32_t)J.seed_len : 0u) << 20;     // strand 1 (rc first, bwtaln.c:343)
+                        if (a.mg) {
+                            // one direct bwt_match_gap call: its strand, its width_seed kind
+                            // (host-checked: 0 <= seed_len <= len when width_seed is given)
+                            const hsa_mg_job_t M = a.mg[job];
+                            const uint32_t has_seed = M.seed != HSA_SEED_NONE;
+                            ctl = (uint32_t)(M.strand & 1) << 3 | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 |
+                                  (M.seed == HSA_SEED_ALIAS ? 1u : 0u) << 7 | len << 10 |
+                                  (has_seed ? (uint32_t)J.seed_len : 0u) << 20;
+                        } else {
+                            const uint32_t has_seed = (int)len > J.seed_len;
+                            ctl = 8u | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 | len << 10 |
+                                  (has_seed ? (uint32_t)J.seed_len : 0u) << 20;     // strand 1 (rc first, bwtaln.c:343)
+                        }
                         const hsa_regime_t *R = s_reg + (J.regime & 1);
                         pen = (uint32_t)R->s_mm | (uint32_t)R->s_gapo << 10 | (uint32_t)R->s_gape << 20;
                         rmode = (uint32_t)R->mode | (uint32_t)R->max_gapo << 8 | (uint32_t)R->max_gape << 16;
@@ -711,7 +798,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
                 if (C_SEED(ctl) && ii > 0) {
                     int ems = RG(max_seed_diff) - (emm + ego);
                     if (R_MODE & MODE_GAPE) ems -= ege;
-                    const uint32_t s1 = WS(ii - 1), s0 = WS(ii);
+                    // width_seed aliased to width_back (bwtgap.c:809): the same LDS row
+                    const uint32_t s1 = C_ALIAS(ctl) ? (uint32_t)WB(ii - 1) : (uint32_t)WS(ii - 1);
+                    const uint32_t s0 = C_ALIAS(ctl) ? (uint32_t)WB(ii) : (uint32_t)WS(ii);
                     const int c1 = (int)(s1 & F::BIDM), c0 = (int)(s0 & F::BIDM);
                     if (c1 > ems - 1) allow_diff = 0;
                     else if (c1 == ems - 1 && c0 == ems - 1 && (s1 & F::EQ)) allow_M = 0;
@@ -954,19 +1043,21 @@ static void launch_search(const LaunchPlan &P, const SearchArgs &A, hipStream_t 
 
 // One search pass over jobs (or a job_list subset) with device pointers: k_widths
 // fills the width rows of every (read, strand), then k_search runs the reads.
-static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
-                       const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
-                       int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
-                       uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st,
-                       int32_t *ovf_list = nullptr, const unsigned long long *n_dev = nullptr, uint32_t qctr = 0)
+// caller-width mode of a pass (hsa_match_gap_batch)
+struct MgPass {
+    const hsa_mg_job_t *d_mg;
+    int32_t *d_cw;
+};
+
+static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
+                            const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
+                            int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
+                            uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, const MgPass *mg)
 {
-    int rc = hsa_scratch_reserve(S, P.lanes, P.pcap, P.hcap);
-    if (rc) return rc;
     const uint32_t esz = P.wide ? 2u : 1u;
     const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;
     const uint32_t rg = (uint32_t)max_len + 1u;
     const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
-    if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * (rb + rs + 4 * (size_t)rg) + 256))) return rc;
     uint8_t *wr = (uint8_t *)ix->d_wrows;
     SearchArgs A;
     A.fwd = RankDir{ix->blk[0], ix->isa0};
@@ -981,6 +1072,46 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     A.pcap = P.pcap; A.hcap = P.hcap;        // the planned capacities (the scratch may be larger)
     A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
     A.mm_buckets = ix->staged_mmb ? 1u : 0u;
+    A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0;
+    A.mg = mg ? mg->d_mg : nullptr;
+    A.cw = mg ? mg->d_cw : nullptr;
+    A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + 4 * (size_t)rg)) : nullptr;
+    return A;
+}
+
+static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
+                       const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
+                       int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
+                       uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st,
+                       int32_t *ovf_list = nullptr, const unsigned long long *n_dev = nullptr, uint32_t qctr = 0,
+                       const MgPass *mg = nullptr)
+{
+    int rc = hsa_scratch_reserve(S, P.lanes, P.pcap, P.hcap);
+    if (rc) return rc;
+    const uint32_t esz = P.wide ? 2u : 1u;
+    const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;
+    const uint32_t rg = (uint32_t)max_len + 1u;
+    const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
+    const size_t row_bytes = rb + rs + 4 * (size_t)rg + (mg ? 4 * (size_t)rg : 0);   // + full bids (caller widths)
+    if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * row_bytes + 256))) return rc;
+    if (mg) {
+        SearchArgs A = pass_args(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
+                                 d_ho, d_hits, hit_cap, d_ctr, mg);
+        HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));
+        const unsigned nb = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
+        if (P.wide) hipLaunchKernelGGL(k_widths_import<uint16_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
+        else hipLaunchKernelGGL(k_widths_import<uint8_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
+        HSA_HIP(hipGetLastError());
+        if (ix->evm) HSA_HIP(hipEventRecord(ix->evm, st));
+        if (P.wide) launch_search<uint16_t>(P, A, st);
+        else launch_search<uint8_t>(P, A, st);
+        HSA_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_widths_export, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
+        HSA_HIP(hipGetLastError());
+        return 0;
+    }
+    SearchArgs A = pass_args(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
+                             d_ho, d_hits, hit_cap, d_ctr, nullptr);
     A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr;
     if (!n_dev) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
     size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
@@ -1046,9 +1177,48 @@ static int stage_regimes(hsa_index *ix, const hsa_regime_t *regimes, int n_regim
     return 0;
 }
 
-extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs,
-                                 int n_jobs, const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
-                                 uint64_t *hit_off, uint32_t **hits_out, hsa_stats_t *stats)
+// Caller-width inputs of hsa_match_gap_batch (null for hsa_search_batch).
+struct MgHost {
+    const hsa_mg_job_t *mg;
+    const int32_t *widths;
+    size_t width_pairs;
+    int32_t *widths_out;
+};
+
+// Checks of a caller-width batch; max_seed = the longest own width_seed.  A width_seed
+// with seed_len > len makes the reference read outside it: refused.
+static int mg_limits(const hsa_job_t *jobs, const hsa_mg_job_t *mg, int n, const MgHost &mh, int &max_seed)
+{
+    max_seed = 0;
+    for (int j = 0; j < n; ++j) {
+        const hsa_mg_job_t &M = mg[j];
+        const uint32_t len = jobs[j].len;
+        if (M.strand != 0 && M.strand != 1) { hsa_set_error("call %d: strand %d", j, M.strand); return HSA_E_ARG; }
+        if (M.seed < HSA_SEED_NONE || M.seed > HSA_SEED_ALIAS) { hsa_set_error("call %d: seed kind", j); return HSA_E_ARG; }
+        if (M.seed != HSA_SEED_NONE && (jobs[j].seed_len < 0 || jobs[j].seed_len > (int)len)) {
+            hsa_set_error("call %d: width_seed with seed_len %d outside [0, len %u] (undefined in the reference)", j,
+                          jobs[j].seed_len, len);
+            return HSA_E_ARG;
+        }
+        if (M.wb_off + len + 1 > mh.width_pairs ||
+            (M.seed == HSA_SEED_OWN && M.ws_off + (uint64_t)jobs[j].seed_len + 1 > mh.width_pairs)) {
+            hsa_set_error("call %d: widths outside the width array", j);
+            return HSA_E_ARG;
+        }
+        for (uint32_t t = 0; t <= len; ++t)
+            if (mh.widths[2 * (M.wb_off + t) + 1] < 0) { hsa_set_error("call %d: negative bid", j); return HSA_E_ARG; }
+        if (M.seed == HSA_SEED_OWN) {
+            for (int t = 0; t <= jobs[j].seed_len; ++t)
+                if (mh.widths[2 * (M.ws_off + t) + 1] < 0) { hsa_set_error("call %d: negative bid", j); return HSA_E_ARG; }
+            if (jobs[j].seed_len > max_seed) max_seed = jobs[j].seed_len;
+        }
+    }
+    return 0;
+}
+
+static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs,
+                              int n_jobs, const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
+                              uint64_t *hit_off, uint32_t **hits_out, hsa_stats_t *stats, const MgHost *mh)
 {
     *hits_out = nullptr;
     if (n_regimes < 1 || n_regimes > 2) { hsa_set_error("1 or 2 regimes"); return HSA_E_ARG; }
@@ -1056,16 +1226,21 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
     if (rc) return rc;
     int max_len, max_seed;
     if ((rc = jobs_limits(jobs, n_jobs, max_len, max_seed))) return rc;
+    if (mh && (rc = mg_limits(jobs, mh->mg, n_jobs, *mh, max_seed))) return rc;
     if (codes_len >= 0xFFFFFFFFull) { hsa_set_error("read codes of one call must be < 4 GiB"); return HSA_E_ARG; }
     HSA_HIP(hipSetDevice(ix->device));
     hipStream_t st = ix->stream;
     if (stats) memset(stats, 0, sizeof *stats);
     if (n_jobs == 0) { *hits_out = (uint32_t *)calloc(9, 4); return 0; }
 
-    // device staging: regimes+bmap | jobs | list | codes
-    const size_t o_reg = 0, o_jobs = 1024, o_list = o_jobs + ((size_t)n_jobs * sizeof(hsa_job_t) + 255) / 256 * 256;
-    const size_t o_codes = o_list + ((size_t)n_jobs * 4 + 255) / 256 * 256;
-    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, o_codes + codes_len + 256))) return rc;
+    // device staging: regimes+bmap | jobs | list | codes [| mg jobs | caller widths]
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t o_reg = 0, o_jobs = 1024, o_list = o_jobs + al((size_t)n_jobs * sizeof(hsa_job_t));
+    const size_t o_codes = o_list + al((size_t)n_jobs * 4);
+    const size_t o_mg = o_codes + al(codes_len + 1);
+    const size_t o_cw = o_mg + (mh ? al((size_t)n_jobs * sizeof(hsa_mg_job_t)) : 0);
+    const size_t cw_bytes = mh ? mh->width_pairs * 8 : 0;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, o_cw + cw_bytes + 256))) return rc;
     char *din = (char *)ix->d_in;
     int nb = 0;
     if ((rc = stage_regimes(ix, regimes, n_regimes, din + o_reg, nb, st, true))) return rc;
@@ -1073,6 +1248,13 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
     const uint8_t *d_bmap = (const uint8_t *)(din + o_reg + 256);
     HSA_HIP(hipMemcpyAsync(din + o_jobs, jobs, sizeof(hsa_job_t) * n_jobs, hipMemcpyHostToDevice, st));
     HSA_HIP(hipMemcpyAsync(din + o_codes, codes, codes_len, hipMemcpyHostToDevice, st));
+    MgPass mgp{nullptr, nullptr};
+    if (mh) {
+        HSA_HIP(hipMemcpyAsync(din + o_mg, mh->mg, sizeof(hsa_mg_job_t) * n_jobs, hipMemcpyHostToDevice, st));
+        HSA_HIP(hipMemcpyAsync(din + o_cw, mh->widths, cw_bytes, hipMemcpyHostToDevice, st));
+        mgp = MgPass{(const hsa_mg_job_t *)(din + o_mg), (int32_t *)(din + o_cw)};
+    }
+    const MgPass *mgpp = mh ? &mgp : nullptr;
     // outputs: n_aln | flags | hit_off | hits
     uint64_t hit_cap = (uint64_t)n_jobs * 4 + 4096;
     const size_t o_fl = ((size_t)n_jobs * 4 + 255) / 256 * 256;
@@ -1092,7 +1274,8 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
     if ((rc = plan_launch(ix, n_jobs, max_len, max_seed, nb, gaps, wide, false, P))) return rc;
     HSA_HIP(hipEventRecord(ix->ev0, st));
     if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs), nullptr, n_jobs,
-                          max_len, max_seed, (const uint8_t *)(din + o_codes), d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, st)))
+                          max_len, max_seed, (const uint8_t *)(din + o_codes), d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, st,
+                          nullptr, nullptr, 0, mgpp)))
         return rc;
     HSA_HIP(hipEventRecord(ix->ev1, st));
     unsigned long long ctr[8];
@@ -1133,7 +1316,7 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
                               (const int32_t *)(din + o_list), n_over, max_len, max_seed,
                               (const uint8_t *)(din + o_codes), (int32_t *)c2,
                               (uint32_t *)(c2 + o2_fl), (uint64_t *)(c2 + o2_ho), (uint32_t *)(c2 + o2_hits), cap2,
-                              d_ctr, st))) {
+                              d_ctr, st, nullptr, nullptr, 0, mgpp))) {
             free(list); free(h); (void)hipFree(d2); return rc;
         }
         HSA_HIP(hipEventRecord(ix->ev1, st));
@@ -1163,8 +1346,39 @@ extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, i
     }
     for (int j = 0; j < n_jobs; ++j)
         if (flags[j] & HSA_F_OVERFLOW) { hsa_set_error("read %d exceeds the large-pass capacity", j); free(h); return HSA_E_ARG; }
+    if (mh) {
+        // width_back of every call after its search (k_widths_export wrote them in place)
+        int32_t *cw = (int32_t *)malloc(cw_bytes + 8);
+        HSA_HIP(hipMemcpy(cw, din + o_cw, cw_bytes, hipMemcpyDeviceToHost));
+        for (int j = 0; j < n_jobs; ++j)
+            memcpy(mh->widths_out + 2 * mh->mg[j].wb_off, cw + 2 * mh->mg[j].wb_off, 8 * ((size_t)jobs[j].len + 1));
+        free(cw);
+    }
     *hits_out = h;
     return (long)total;
+}
+
+extern "C" long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs,
+                                 int n_jobs, const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
+                                 uint64_t *hit_off, uint32_t **hits_out, hsa_stats_t *stats)
+{
+    return search_batch_impl(ix, regimes, n_regimes, jobs, n_jobs, codes, codes_len, n_aln, flags, hit_off, hits_out,
+                             stats, nullptr);
+}
+
+extern "C" long hsa_match_gap_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs,
+                                    const hsa_mg_job_t *mg, int n_jobs, const uint8_t *codes, size_t codes_len,
+                                    const int32_t *widths, size_t width_pairs, int32_t *widths_out, int32_t *n_aln,
+                                    uint64_t *hit_off, uint32_t **hits_out, hsa_stats_t *stats)
+{
+    *hits_out = nullptr;
+    if (n_jobs > 0 && (!mg || !widths || !widths_out)) { hsa_set_error("hsa_match_gap_batch: null argument"); return HSA_E_ARG; }
+    uint32_t *flags = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)n_jobs + 1));
+    const MgHost mh{mg, widths, width_pairs, widths_out};
+    const long r = search_batch_impl(ix, regimes, n_regimes, jobs, n_jobs, codes, codes_len, n_aln, flags, hit_off,
+                                     hits_out, stats, &mh);
+    free(flags);
+    return r;
 }
 
 extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes,

@@ -6,6 +6,8 @@
  * INTEGRATION.md) keeps the host program unchanged:
  *
  *   bwa_cal_sa_reg_gap   replaces bwtaln.c:246  (declared bwtaln.h:199-200)
+ *   bwt_match_gap        replaces bwtgap.c:118  (declared bwtgap.h:26)
+ *   bwt_match_gap_batch  new: many bwt_match_gap calls in one GPU pass
  *   hsa_gpu_attach       new hook, called once after BWTLoad2BWT (bwtaln.c:467)
  *   hsa_gpu_detach       new hook, before BWTFree2BWT (bwtaln.c:527)
  *   hsa_gpu_set_devices  new hook (multi-GPU: reads of one call are split over devices)
@@ -143,6 +145,14 @@ typedef struct _bwt_aux_t {
 /* ---- drop-in entry points (reference ABI) ---- */
 void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, const gap_opt_t *opt,
                         struct bwt_array_t *arr);
+/* bwt_match_gap: replaces bwtgap.c:118 (declared bwtgap.h:26).  The host's splice path
+ * (bwt_splice_match, bwtgap.c:748) calls it with its own widths; the result array is
+ * calloc'd (capacity as the reference's, never NULL) and aux->width_back is left as
+ * gap_shadow leaves it. */
+bwt_aln1_t *bwt_match_gap(bwt_aux_t *aux, int *_n_aln);
+/* n independent bwt_match_gap calls in one GPU pass: out[i] / n_out[i] as
+ * bwt_match_gap would return them for aux[i] (new entry point). */
+int  bwt_match_gap_batch(bwt_aux_t *const *aux, int n, bwt_aln1_t **out, int *n_out);
 int  hsa_gpu_attach(const Idx2BWT *bi_bwt);
 void hsa_gpu_detach(const Idx2BWT *bi_bwt);
 int  hsa_gpu_set_devices(int n);

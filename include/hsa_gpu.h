@@ -132,6 +132,35 @@ void hsa_free(void *p);
 /* Synthetic workload helpers (bench data generation on the device). */
 int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, uint32_t *d_code_lsb);
 
+/* ---- bwt_match_gap with caller-supplied widths (bwtgap.c:118-331) ----
+ * The splice path calls bwt_match_gap directly (bwtgap.c:812, :919, :1192) with widths
+ * it computed itself -- of the read prefix, not of the searched sequence
+ * (bwtgap.c:807) -- with width_seed NULL or aliased to width_back (bwtgap.c:809), and
+ * the search mutates width_back through gap_shadow (bwtgap.c:217).  One
+ * hsa_mg_job_t per call, next to its hsa_job_t: jobs[j].off/len address the searched
+ * sequence itself (aux->seq or aux->rc_seq as aux->strand selects), jobs[j].max_diff
+ * and seed_len are the call's opt->max_diff and opt->seed_len. */
+#define HSA_SEED_NONE  0          /* width_seed == NULL */
+#define HSA_SEED_OWN   1          /* width_seed: its own array, seed_len + 1 entries */
+#define HSA_SEED_ALIAS 2          /* width_seed == width_back */
+typedef struct {
+    uint64_t wb_off;              /* width_back[0..len]: pairs (w, bid) at widths + 2 * wb_off */
+    uint64_t ws_off;              /* width_seed[0..seed_len] (HSA_SEED_OWN only) */
+    int32_t strand;               /* aux->strand (0 or 1), stamped into the hits (bwtgap.c:235) */
+    int32_t seed;                 /* HSA_SEED_* */
+} hsa_mg_job_t;
+
+/* One search per job with the caller's widths (bwt_cal_width's bwt_width_t pairs, int32
+ * w then bid; bids must be >= 0 as bwt_cal_width produces them).  The jobs' width
+ * ranges must not overlap.  widths_out (width_pairs pairs, may equal widths) receives
+ * each job's width_back after the search; other entries are left as they are.  Hits
+ * as hsa_search_batch, with start = end = 0 (bwt_match_gap leaves them to its caller).
+ * Returns the total hit count >= 0. */
+long hsa_match_gap_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs,
+                         const hsa_mg_job_t *mg, int n_jobs, const uint8_t *codes, size_t codes_len,
+                         const int32_t *widths, size_t width_pairs, int32_t *widths_out,
+                         int32_t *n_aln, uint64_t *hit_off, uint32_t **hits, hsa_stats_t *stats);
+
 /* SA index -> text position (BWTSaValue BWT.c:1195 + BWTRetrievePositionFromSAIndex
  * 2BWT-Interface.c:329), batched.  hsa_index_set_sa uploads the sampled suffix array
  * as BWTLoad holds it (values[0] = -1, (T+s)/s values, interval s) and the chromosome

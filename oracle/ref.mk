@@ -73,8 +73,10 @@ $(OUT)/ref_mgcap: ref_mgcap.c $(CAPOBJS)
 MGOBJS    = $(filter-out $(OUT)/obj/bwtaln.o $(OUT)/obj/bwtgap.o,$(OBJS)) $(OUT)/obj/bwtaln_weak.o \
             $(OUT)/obj/bwtgap_weak.o
 
-$(OUT)/HSA_gpu_mg: $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPULIB)
-	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) -L$(dir $(GPULIB)) -lhsa_gpu \
+GPUOBJ_MG = $(CURDIR)/../hsa_amd/csrc/bwtgap_gpu.o
+
+$(OUT)/HSA_gpu_mg: $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPULIB)
+	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPUOBJ_MG) -L$(dir $(GPULIB)) -lhsa_gpu \
 	    -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
 
 clean:

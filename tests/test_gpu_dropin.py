@@ -29,17 +29,18 @@ MAN = json.load(open(os.path.join(GOLD, "manifest_dropin.json")))
 needs_bin = pytest.mark.skipif(not os.path.exists(HSA_GPU), reason="oracle/_ref/HSA_gpu not built (make -C oracle)")
 
 
-def run_hsa_gpu(args):
+def run_hsa_gpu(args, reads="reads"):
     idx = os.path.join(GOLD, "index", "tiny.fa")
-    fq = os.path.join(GOLD, MAN["reads"])
+    fq = os.path.join(GOLD, MAN[reads])
     return subprocess.run([HSA_GPU, "aln", *args, idx, fq], capture_output=True, timeout=120)
 
 
 @needs_bin
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["default", "n4o0"])
-def test_dropin_sam_identical(name):
-    r = run_hsa_gpu(MAN[name]["args"])
+@pytest.mark.parametrize("name,reads", [("default", "reads"), ("n4o0", "reads"), ("splice_default", "splice_reads"),
+                                        ("splice_n4o1", "splice_reads")])
+def test_dropin_sam_identical(name, reads):
+    r = run_hsa_gpu(MAN[name]["args"], reads)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     sam = r.stdout
     if hashlib.sha256(sam).hexdigest() != MAN[name]["sam_sha256"]:

@@ -1,0 +1,125 @@
+"""bwt_match_gap called directly with the caller's widths, on the GPU:
+every call the reference's splice path made on the splice read set -- seed searches
+with width_seed aliased to width_back (bwtgap.c:809-812), 12-mer anchors with
+width_seed NULL (bwtgap.c:1192) -- and a sample of main-path calls (own width_seed,
+bwtaln.c:350), recorded from the compiled reference (tools/make_golden.py --mgcap).
+Hits must be identical word for word, and width_back after the call must equal the
+reference's (gap_shadow, bwtgap.c:94-105).  Then the whole host program: the
+reference's HSA binary with our bwa_cal_sa_reg_gap AND bwt_match_gap linked in
+(oracle/ref.mk HSA_gpu_mg) prints byte-identical SAM, splice reads included."""
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from golden_io import GOLD, INDEX, MGCAP_CASES, load_mgcap
+from hsa_amd import index_io
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OPT_NAMES = ["s_mm", "s_gapo", "s_gape", "mode", "indel_end_skip", "max_del_occ", "max_entries", "fnr", "max_diff",
+             "max_gapo", "max_gape", "max_seed_diff", "seed_len", "n_threads", "max_top2", "trim_qual"]
+
+
+def opt_dict(words):
+    d = {k: int(np.int32(np.uint32(w))) for k, w in zip(OPT_NAMES, words)}
+    d["fnr"] = float(np.uint32(words[7]).view(np.float32))
+    return d
+
+
+def run_calls(gi, calls, pool_entries=0):
+    """Group the calls by option regime (two per launch), run hsa_match_gap_batch."""
+    from hsa_amd import _lib
+    from hsa_amd._lib import JOB_DTYPE, MG_DTYPE, regime_of
+    keys = {}
+    for c in calls:
+        o = opt_dict(c["opt"])
+        k = (tuple(sorted((n, v) for n, v in o.items() if n not in ("max_diff", "seed_len", "fnr", "n_threads"))),
+             c["n_stacks"])
+        keys.setdefault(k, []).append(c)
+    out = {}
+    groups = list(keys.items())
+    if pool_entries:
+        _lib.configure(pool_entries=pool_entries)
+    try:
+        for g0 in range(0, len(groups), 2):
+            part = groups[g0:g0 + 2]
+            sel = [(r, c) for r, (_, cs) in enumerate(part) for c in cs]
+            regimes = []
+            for _, cs in part:
+                o = opt_dict(cs[0]["opt"])
+                regimes.append(regime_of(o, cs[0]["n_stacks"], max(opt_dict(c["opt"])["max_diff"] for c in cs)))
+            jobs = np.zeros(len(sel), JOB_DTYPE)
+            mg = np.zeros(len(sel), MG_DTYPE)
+            codes, widths = [], []
+            co = wo = 0
+            for j, (r, c) in enumerate(sel):
+                o = opt_dict(c["opt"])
+                jobs[j] = (co, c["len"], o["max_diff"], o["seed_len"], r)
+                codes.append(c["seq"])
+                co += c["len"]
+                mg[j]["wb_off"], mg[j]["strand"], mg[j]["seed"] = wo, c["strand"], c["seed"]
+                widths.append(c["wb"])
+                wo += c["len"] + 1
+                if c["seed"] == 1:
+                    mg[j]["ws_off"] = wo
+                    widths.append(c["ws"])
+                    wo += len(c["ws"])
+            n_aln, hoff, hits, wout, _ = gi.match_gap(regimes, jobs, mg, np.concatenate(codes),
+                                                      np.concatenate(widths))
+            for j, (r, c) in enumerate(sel):
+                out[id(c)] = (hits[int(hoff[j]):int(hoff[j]) + n_aln[j]],
+                              wout[int(mg[j]["wb_off"]):int(mg[j]["wb_off"]) + c["len"] + 1])
+    finally:
+        if pool_entries:
+            _lib.configure(pool_entries=-1)
+    return out
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    from hsa_amd._lib import GpuIndex
+    return GpuIndex(*index_io.read_index(INDEX["tiny"]))
+
+
+@pytest.mark.parametrize("name", MGCAP_CASES)
+def test_match_gap_calls_match_reference(tiny, name):
+    calls = load_mgcap(name)
+    assert {c["seed"] for c in calls} == {0, 1, 2}
+    got = run_calls(tiny, calls)
+    bad = [j for j, c in enumerate(calls)
+           if not (np.array_equal(got[id(c)][0], c["hits"]) and np.array_equal(got[id(c)][1], c["wo"]))]
+    assert not bad, f"{len(bad)} of {len(calls)} calls differ; first {bad[:5]}"
+
+
+def test_match_gap_overflow_rerun_is_exact(tiny):
+    """A tiny per-lane pool sends the calls through the large-capacity re-run, whose
+    width rows are rebuilt from the caller's widths (not from the first pass's)."""
+    calls = load_mgcap("mgcap_n4o1")[:600]
+    got = run_calls(tiny, calls, pool_entries=16)
+    bad = [j for j, c in enumerate(calls)
+           if not (np.array_equal(got[id(c)][0], c["hits"]) and np.array_equal(got[id(c)][1], c["wo"]))]
+    assert not bad, f"{len(bad)} of {len(calls)} calls differ; first {bad[:5]}"
+
+
+HSA_GPU_MG = os.path.join(ROOT, "oracle", "_ref", "HSA_gpu_mg")
+MAN = json.load(open(os.path.join(GOLD, "manifest_dropin.json")))
+
+
+@pytest.mark.skipif(not os.path.exists(HSA_GPU_MG), reason="oracle/_ref/HSA_gpu_mg not built (make -C oracle)")
+@pytest.mark.parametrize("name,reads", [("splice_default", "splice_reads"), ("splice_n4o1", "splice_reads"),
+                                        ("default", "reads"), ("n4o0", "reads")])
+def test_dropin_both_entry_points_sam_identical(name, reads):
+    fq = os.path.join(GOLD, MAN[reads])
+    r = subprocess.run([HSA_GPU_MG, "aln", *MAN[name]["args"], INDEX["tiny"], fq], capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    if hashlib.sha256(r.stdout).hexdigest() != MAN[name]["sam_sha256"]:
+        ref = gzip.open(os.path.join(GOLD, f"dropin_ref_{name}.sam.gz")).read().splitlines()
+        got = r.stdout.splitlines()
+        diff = [(i, a, b) for i, (a, b) in enumerate(zip(ref, got)) if a != b][:5]
+        pytest.fail(f"SAM differs: {len(got)} vs {len(ref)} lines; first differences {diff}")

@@ -1,0 +1,9 @@
+# GPU test pass only (tests named in $TESTS, default all -m gpu), log under gpurun_out/
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -40 gpurun_out/pytest_gpu.log
+exit $rc

@@ -273,6 +273,7 @@ def ecoli_cases(work):
 
 
 DROPIN_ARGS = {"default": [], "n4o0": ["-n", "4", "-o", "0"]}
+DROPIN_SPLICE_ARGS = {"splice_default": [], "splice_n4o1": ["-n", "4", "-o", "1"]}
 
 
 def write_fastq_mixed(path, seqs):
@@ -314,6 +315,18 @@ def dropin_cases(work):
         sam = r.stdout
         out = os.path.join(GOLD, f"dropin_ref_{name}.sam.gz")
         with gzip.GzipFile(out, "wb", compresslevel=9, mtime=0) as f:
+            f.write(sam)
+        man[name] = {"args": args, "sam_sha256": hashlib.sha256(sam).hexdigest(), "sam_lines": sam.count(b"\n")}
+        print(name, man[name])
+    # the splice read set: the drop-in with OUR bwt_match_gap under the host's
+    # bwt_splice_match (oracle/ref.mk HSA_gpu_mg) must reproduce these SAMs too
+    fq2 = os.path.join(GOLD, "dropin_splice_reads.fq.gz")
+    write_fastq_mixed(fq2, splice_reads())
+    man["splice_reads"] = os.path.basename(fq2)
+    for name, args in DROPIN_SPLICE_ARGS.items():
+        r = subprocess.run([os.path.join(REF, "HSA"), "aln", *args, idx, fq2], check=True, capture_output=True)
+        sam = r.stdout
+        with gzip.GzipFile(os.path.join(GOLD, f"dropin_ref_{name}.sam.gz"), "wb", compresslevel=9, mtime=0) as f:
             f.write(sam)
         man[name] = {"args": args, "sam_sha256": hashlib.sha256(sam).hexdigest(), "sam_lines": sam.count(b"\n")}
         print(name, man[name])
@@ -398,11 +411,10 @@ def read_mgcap(path):
     return recs
 
 
-def mgcap_cases(work):
-    """bwt_match_gap called directly with caller widths (SURVEY §8f #1): every call the
-    reference makes on the drop-in read set -- the splice path's seed searches
-    (width_seed aliased to width_back, bwtgap.c:809-812), its 12-mer anchors (width_seed
-    NULL, :919 and :1192) -- plus a sample of main-path calls (own width_seed)."""
+def splice_reads():
+    """Reads that exercise bwt_splice_match and its direct bwt_match_gap calls on the
+    tiny index: mismatched and gapped reads, spliced reads of 75-150 bp, and 180-210 bp
+    spliced reads whose seeds 1 and 2 map (the anchor call at bwtgap.c:1192)."""
     T, seed = 200003, 7
     g = synth.genome_codes(T, seed)
     rec = synth.record_layout(T, 3)
@@ -432,6 +444,15 @@ def mgcap_cases(work):
         intron = 300 + (i * 53) % 1500
         s = np.concatenate([g[st:st + cut], g[st + cut + intron:st + L + intron]]).astype(np.uint8)
         seqs.append(synth.revcomp_codes(s) if i % 2 else s)
+    return seqs
+
+
+def mgcap_cases(work):
+    """bwt_match_gap called directly with caller widths (SURVEY §8f #1): every call the
+    reference makes on the drop-in read set -- the splice path's seed searches
+    (width_seed aliased to width_back, bwtgap.c:809-812), its 12-mer anchors (width_seed
+    NULL, :919 and :1192) -- plus a sample of main-path calls (own width_seed)."""
+    seqs = splice_reads()
     rb = os.path.join(work, "mg_reads.bin")
     synth.write_reads_bin(rb, seqs)
     idx = os.path.join(GOLD, "index", "tiny.fa")
