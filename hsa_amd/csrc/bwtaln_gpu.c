@@ -26,6 +26,11 @@
 #include "../../include/hsa_bwtaln.h"
 #include "bwtaln_gpu.h"
 
+#pragma weak hsa_splice_prefetch_active
+#pragma weak hsa_splice_prefetch
+#pragma weak hsa_splice_memo_clear
+#pragma weak hsa_splice_memo_stats
+
 _Static_assert(sizeof(bwt_aln1_t) == 36, "bwt_aln1_t layout");
 _Static_assert(sizeof(gap_opt_t) == 64, "gap_opt_t layout");
 _Static_assert(sizeof(bwa_seq_t) == 208, "bwa_seq_t layout");
@@ -358,6 +363,45 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     bwt_aux_t aux;
     memset(&aux, 0, sizeof aux);
     int have_splice = bwt_splice_match != NULL;
+    const int n_stacks = hsa_aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
+    /* the splice path's seed searches of every fallback read in one GPU batch, when
+     * the host's bwt_splice_match calls our bwt_match_gap (bwtgap_gpu.c) */
+    int prefetched = 0;
+    if (have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active()) {
+        int nf = 0;
+        for (int i = 0; i < n_seqs; ++i)
+            nf += !(flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) && n_aln[i] == 0 && (flags[i] & HSA_F_FALLBACK);
+        if (nf > 0) {
+            bwt_aux_t *fa = (bwt_aux_t *)calloc((size_t)nf, sizeof(bwt_aux_t));
+            bwt_aux_t **fp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)nf);
+            gap_opt_t *fo = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nf);
+            ubyte_t *rc = (ubyte_t *)malloc(tot + 1);
+            gap_stack_t st_shape;                       /* only n_stacks is read */
+            memset(&st_shape, 0, sizeof st_shape);
+            st_shape.n_stacks = n_stacks;
+            int q = 0;
+            for (int i = 0; i < n_seqs; ++i) {
+                if ((flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) || n_aln[i] != 0 || !(flags[i] & HSA_F_FALLBACK)) continue;
+                const bwa_seq_t *p = seqs + i;
+                ubyte_t *r = rc + offs[i];
+                for (int j = 0; j < (int)p->len; ++j) {
+                    ubyte_t c = p->seq[p->len - 1 - j];
+                    r[j] = c < 4 ? (ubyte_t)(3 - c) : c;
+                }
+                fo[q] = local;
+                fo[q].max_diff = sp[2 * i];
+                fo[q].seed_len = sp[2 * i + 1];
+                fa[q].bi_bwt = (Idx2BWT *)bi_bwt; fa[q].arr = arr; fa[q].max_len = max_len;
+                fa[q].seq = p->seq; fa[q].rc_seq = r; fa[q].len = (int)p->len; fa[q].opt = fo + q;
+                fa[q].stack = &st_shape;
+                fp[q] = fa + q;
+                ++q;
+            }
+            hsa_splice_prefetch(bi_bwt, nf, fp);
+            prefetched = 1;
+            free(fa); free(fp); free(fo); free(rc);
+        }
+    }
     for (int i = 0; i < n_seqs; ++i) {
         bwa_seq_t *p = seqs + i;
         if (flags[i] & HSA_RF_NFILTER) continue;               /* untouched (:314-317) */
@@ -379,8 +423,7 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
             aux.width_fore = (bwt_width_t *)calloc(max_len + 1, sizeof(bwt_width_t));
             aux.width_seed = (bwt_width_t *)calloc(max_len + 1, sizeof(bwt_width_t));
             aux.rc_seq = (ubyte_t *)calloc(max_len + 1, 1);
-            aux.stack = ref_stack_new(local.s_mm * (local.max_diff + 1) + local.s_gapo * (local.max_gapo + 1) +
-                                      local.s_gape * (local.max_gape + 1));
+            aux.stack = ref_stack_new(n_stacks);
         }
         gap_opt_t lo = local;                                   /* aux->opt = &local_opt (:363) */
         lo.max_diff = sp[2 * i];
@@ -402,6 +445,15 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     if (aux.stack) {
         free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);
         ref_stack_free(aux.stack);
+    }
+    if (prefetched) {
+        if (getenv("HSA_VERBOSE") && hsa_splice_memo_stats) {
+            uint64_t mh = 0, mm = 0;
+            hsa_splice_memo_stats(&mh, &mm);
+            fprintf(stderr, "[hsa] splice prefetch: %llu bwt_match_gap calls answered from the batch, %llu run alone\n",
+                    (unsigned long long)mh, (unsigned long long)mm);
+        }
+        hsa_splice_memo_clear();
     }
     hsa_free(hits);
     free(lens); free(offs); free(codes); free(n_aln); free(flags); free(hoff); free(sp);

@@ -13,4 +13,11 @@ int hsa_aln_score(const gap_opt_t *o, int m, int g, int e);
 /* the search options of one option block (the fields bwt_match_gap reads) */
 hsa_regime_t hsa_regime_of(const gap_opt_t *o, int n_stacks, int max_diff);
 
+/* splice prefetch (bwtgap_gpu.c; bwtaln_gpu.c refers to them weakly, so that a host
+ * that takes only bwtaln_gpu.o still links) */
+int hsa_splice_prefetch_active(void);
+int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux);
+void hsa_splice_memo_clear(void);
+void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses);
+
 #endif

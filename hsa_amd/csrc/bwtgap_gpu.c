@@ -127,13 +127,242 @@ int bwt_match_gap_batch(bwt_aux_t *const *aux, int n, bwt_aln1_t **out, int *n_o
     return 0;
 }
 
+/* ------------------------------------------------------------ splice prefetch
+ * bwt_splice_match (bwtgap.c:748) asks for its six seed searches one call at a time
+ * (bwtgap.c:797-848), each a GPU round trip.  Which seeds it asks for depends on
+ * earlier answers, but every seed it can ask for is known in advance: so
+ * bwa_cal_sa_reg_gap runs all six of every fallback read in one batch first
+ * (hsa_splice_prefetch) and bwt_match_gap answers from that table.  A table entry
+ * is keyed by everything the search reads -- index, strand, length, sequence,
+ * width_back (and an own width_seed), the width_seed kind, the option block and the
+ * stack's bucket count -- and compared in full, so an answer from the table is the
+ * answer the search would give.  Any other call (the 12-mer anchors, :919 and
+ * :1192) misses and runs on its own. */
+typedef struct {
+    uint64_t h;
+    uint8_t *key;          /* the call's inputs, serialised */
+    size_t key_len;
+    int n_aln;
+    bwt_aln1_t *hits;
+    bwt_width_t *wout;     /* width_back after the search */
+    int len;
+} memo_ent_t;
+
+static memo_ent_t *g_memo;
+static size_t g_memo_cap, g_memo_n;
+static uint64_t g_memo_hits, g_memo_misses;
+
+static size_t key_of(const bwt_aux_t *a, uint8_t *buf)
+{
+    const ubyte_t *seq = a->strand == 1 ? a->rc_seq : a->seq;
+    const int seed = !a->width_seed ? 0 : a->width_seed == a->width_back ? 2 : 1;
+    const int n_stacks = a->stack ? a->stack->n_stacks : -1;
+    size_t o = 0;
+#define PUT(p, n) do { if (buf) memcpy(buf + o, (p), (n)); o += (n); } while (0)
+    PUT(&a->bi_bwt, sizeof a->bi_bwt);
+    PUT(&a->strand, 4); PUT(&a->len, 4); PUT(&seed, 4); PUT(&n_stacks, 4);
+    PUT(a->opt, sizeof(gap_opt_t));
+    PUT(seq, (size_t)a->len);
+    PUT(a->width_back, sizeof(bwt_width_t) * ((size_t)a->len + 1));
+    if (seed == 1 && a->opt->seed_len >= 0) PUT(a->width_seed, sizeof(bwt_width_t) * ((size_t)a->opt->seed_len + 1));
+#undef PUT
+    return o;
+}
+
+static uint64_t fnv1a(const uint8_t *p, size_t n)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return h | 1;                          /* 0 marks an empty slot */
+}
+
+void hsa_splice_memo_clear(void)
+{
+    for (size_t i = 0; i < g_memo_cap; ++i)
+        if (g_memo[i].h) { free(g_memo[i].key); free(g_memo[i].hits); free(g_memo[i].wout); }
+    free(g_memo);
+    g_memo = NULL;
+    g_memo_cap = g_memo_n = 0;
+}
+
+static void memo_put(const bwt_aux_t *in, const bwt_width_t *wout, const bwt_aln1_t *hits, int n_aln)
+{
+    if (2 * (g_memo_n + 1) > g_memo_cap) {     /* grow: open addressing at <= 1/2 load */
+        size_t cap = g_memo_cap ? g_memo_cap * 2 : 1024;
+        memo_ent_t *t = (memo_ent_t *)calloc(cap, sizeof(memo_ent_t));
+        for (size_t i = 0; i < g_memo_cap; ++i) {
+            if (!g_memo[i].h) continue;
+            size_t j = g_memo[i].h & (cap - 1);
+            while (t[j].h) j = (j + 1) & (cap - 1);
+            t[j] = g_memo[i];
+        }
+        free(g_memo);
+        g_memo = t;
+        g_memo_cap = cap;
+    }
+    const size_t kl = key_of(in, NULL);
+    uint8_t *key = (uint8_t *)malloc(kl);
+    key_of(in, key);
+    const uint64_t h = fnv1a(key, kl);
+    size_t j = h & (g_memo_cap - 1);
+    while (g_memo[j].h) {
+        if (g_memo[j].h == h && g_memo[j].key_len == kl && !memcmp(g_memo[j].key, key, kl)) { free(key); return; }
+        j = (j + 1) & (g_memo_cap - 1);
+    }
+    memo_ent_t *e = g_memo + j;
+    e->h = h; e->key = key; e->key_len = kl; e->n_aln = n_aln; e->len = in->len;
+    e->hits = (bwt_aln1_t *)malloc(sizeof(bwt_aln1_t) * (size_t)(n_aln > 0 ? n_aln : 1));
+    if (n_aln > 0) memcpy(e->hits, hits, sizeof(bwt_aln1_t) * (size_t)n_aln);
+    e->wout = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)in->len + 1));
+    memcpy(e->wout, wout, sizeof(bwt_width_t) * ((size_t)in->len + 1));
+    ++g_memo_n;
+}
+
+static const memo_ent_t *memo_get(const bwt_aux_t *a)
+{
+    if (!g_memo_n) return NULL;
+    const size_t kl = key_of(a, NULL);
+    uint8_t stackbuf[4096];
+    uint8_t *key = kl <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc(kl);
+    key_of(a, key);
+    const uint64_t h = fnv1a(key, kl);
+    const memo_ent_t *hit = NULL;
+    for (size_t j = h & (g_memo_cap - 1); g_memo[j].h; j = (j + 1) & (g_memo_cap - 1))
+        if (g_memo[j].h == h && g_memo[j].key_len == kl && !memcmp(g_memo[j].key, key, kl)) { hit = g_memo + j; break; }
+    if (key != stackbuf) free(key);
+    return hit;
+}
+
+/* The six seed searches bwt_splice_match can ask for (bwtgap.c:762-812) of each
+ * read it will be called on: aux[r] as bwt_splice_match receives it (seq, rc_seq,
+ * len, opt = local_opt of that read, stack).  Widths of the read prefixes on the
+ * GPU (bwt_cal_width type 1, as bwtgap.c:807 computes them), then one batch of
+ * searches; the answers go to the table bwt_match_gap consults. */
+int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
+{
+    if (n <= 0) return 0;
+    hsa_index_t *ix = hsa_gpu_index_of(bi);
+    /* widths: per read, strand s, the prefix of seed_len and of seed_len + len % 3 */
+    int nw = 0;
+    size_t wcodes = 0, wpairs = 0;
+    for (int r = 0; r < n; ++r) {
+        const int L = aux[r]->len, sl = L / 3;
+        if (sl < 1) continue;
+        nw += 4;
+        wcodes += 4 * (size_t)sl + 2 * (size_t)(L % 3);
+        wpairs += 4 * (size_t)(sl + 1) + 2 * (size_t)(L % 3);
+    }
+    if (nw == 0) return 0;
+    uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)nw);
+    uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)nw);
+    uint8_t *codes = (uint8_t *)malloc(wcodes + 1);
+    uint32_t *wout = (uint32_t *)malloc(sizeof(uint32_t) * 2 * (wpairs + 1));
+    size_t co = 0;
+    int q = 0;
+    for (int r = 0; r < n; ++r) {
+        const int L = aux[r]->len, sl = L / 3;
+        if (sl < 1) continue;
+        for (int s = 0; s < 2; ++s)
+            for (int k = 0; k < 2; ++k) {
+                const int la = sl + (k ? L % 3 : 0);
+                offs[q] = co; lens[q] = (uint32_t)la;
+                memcpy(codes + co, s ? aux[r]->rc_seq : aux[r]->seq, (size_t)la);
+                co += (size_t)la;
+                ++q;
+            }
+    }
+    int rc = hsa_width_batch(ix, (size_t)nw, offs, lens, codes, co, wout);
+    if (rc) hsa_gpu_fatal("GPU bwt_cal_width", rc);
+    /* the seed calls, set up as bwtgap.c:797-810 sets up aux_seed */
+    const int nc = 6 * (nw / 4);
+    bwt_aux_t *calls = (bwt_aux_t *)calloc((size_t)nc, sizeof(bwt_aux_t));
+    bwt_aux_t **cp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)nc);
+    gap_opt_t *opts = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nc);
+    bwt_width_t **win = (bwt_width_t **)malloc(sizeof(bwt_width_t *) * (size_t)nc);
+    bwt_aln1_t **out = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)nc);
+    int *n_out = (int *)malloc(sizeof(int) * (size_t)nc);
+    size_t wo = 0;
+    int c = 0, w = 0;
+    for (int r = 0; r < n; ++r) {
+        const bwt_aux_t *a = aux[r];
+        const int L = a->len, sl = L / 3;
+        if (sl < 1) continue;
+        size_t woff[4];
+        for (int k = 0; k < 4; ++k) { woff[k] = wo; wo += 2 * ((size_t)lens[w + k] + 1); }
+        for (int i = 0; i < 6; ++i) {
+            const int s = i / 3, la = sl + (i % 3 == 2 ? L % 3 : 0);
+            bwt_aux_t *x = calls + c;
+            *x = *a;                                            /* bwtgap.c:756-757 */
+            gap_opt_t *o = opts + c;
+            *o = *a->opt;                                       /* :769-774 */
+            o->mode &= ~BWA_MODE_GAPE;
+            o->max_gapo = 0;
+            o->max_gape = 0;
+            o->max_diff = a->opt->max_seed_diff;
+            o->seed_len = la;                                   /* :802 */
+            x->opt = o;
+            x->len = la;
+            x->strand = s;
+            if (s) x->rc_seq = a->rc_seq + (i % 3) * sl;       /* :805-806 */
+            else x->seq = a->seq + (i % 3) * sl;
+            const size_t wk = woff[2 * s + (i % 3 == 2 && L % 3 ? 1 : 0)];
+            win[c] = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)la + 1));
+            memcpy(win[c], wout + wk, sizeof(bwt_width_t) * ((size_t)la + 1));
+            x->width_seed = x->width_back = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)la + 1));
+            memcpy(x->width_back, win[c], sizeof(bwt_width_t) * ((size_t)la + 1));   /* :804-809 */
+            cp[c] = x;
+            ++c;
+        }
+        w += 4;
+    }
+    bwt_match_gap_batch(cp, c, out, n_out);
+    for (int i = 0; i < c; ++i) {
+        /* the table is keyed by the inputs: widths as they were before the search */
+        bwt_width_t *after = calls[i].width_back;
+        calls[i].width_back = calls[i].width_seed = win[i];
+        memo_put(calls + i, after, out[i], n_out[i]);
+        free(after); free(win[i]); free(out[i]);
+    }
+    free(offs); free(lens); free(codes); free(wout);
+    free(calls); free(cp); free(opts); free(win); free(out); free(n_out);
+    return 0;
+}
+
+/* Table statistics since the last call (hits, misses), for logs. */
+void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses)
+{
+    *hits = g_memo_hits; *misses = g_memo_misses;
+    g_memo_hits = g_memo_misses = 0;
+}
+
 /* bwt_match_gap (bwtgap.c:118, declared bwtgap.h:26): the reference's entry point,
- * one call at a time (a batch of one).  Same return contract: a calloc'd array,
- * never NULL, freed by the caller with free(). */
+ * one call at a time (a batch of one), or an answer prefetched for the splice path.
+ * Same return contract: a calloc'd array, never NULL, freed by the caller. */
 bwt_aln1_t *bwt_match_gap(bwt_aux_t *aux, int *_n_aln)
 {
+    const memo_ent_t *e = memo_get(aux);
+    if (e) {
+        ++g_memo_hits;
+        bwt_aln1_t *out = (bwt_aln1_t *)calloc((size_t)aln_capacity(e->n_aln), sizeof(bwt_aln1_t));
+        if (e->n_aln > 0) memcpy(out, e->hits, sizeof(bwt_aln1_t) * (size_t)e->n_aln);
+        memcpy(aux->width_back, e->wout, sizeof(bwt_width_t) * ((size_t)e->len + 1));
+        *_n_aln = e->n_aln;
+        return out;
+    }
+    if (g_memo_n) ++g_memo_misses;
     bwt_aln1_t *out = NULL;
     bwt_match_gap_batch(&aux, 1, &out, _n_aln);
     return out;
 }
 
+/* This object's own bwt_match_gap, whatever the host's symbol table resolves
+ * bwt_match_gap to. */
+extern __typeof__(bwt_match_gap) hsa_own_match_gap __attribute__((alias("bwt_match_gap"), visibility("hidden")));
+
+/* Whether the host's bwt_splice_match calls this bwt_match_gap (the host linked
+ * bwtgap_gpu.o, or weakened its own): only then does a prefetch pay. */
+int hsa_splice_prefetch_active(void)
+{
+    bwt_aln1_t *(*volatile resolved)(bwt_aux_t *, int *) = bwt_match_gap;
+    return resolved == hsa_own_match_gap;
+}

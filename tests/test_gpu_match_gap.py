@@ -11,6 +11,7 @@ import gzip
 import hashlib
 import json
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -116,8 +117,13 @@ MAN = json.load(open(os.path.join(GOLD, "manifest_dropin.json")))
                                         ("default", "reads"), ("n4o0", "reads")])
 def test_dropin_both_entry_points_sam_identical(name, reads):
     fq = os.path.join(GOLD, MAN[reads])
-    r = subprocess.run([HSA_GPU_MG, "aln", *MAN[name]["args"], INDEX["tiny"], fq], capture_output=True, timeout=300)
+    env = dict(os.environ, HSA_VERBOSE="1")
+    r = subprocess.run([HSA_GPU_MG, "aln", *MAN[name]["args"], INDEX["tiny"], fq], capture_output=True, timeout=300,
+                       env=env)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
+    # the splice path's seed searches were answered from the batched prefetch
+    m = re.findall(rb"splice prefetch: (\d+) bwt_match_gap calls answered from the batch, (\d+) run alone", r.stderr)
+    assert m and sum(int(a) for a, _ in m) > 0, r.stderr.decode()[-2000:]
     if hashlib.sha256(r.stdout).hexdigest() != MAN[name]["sam_sha256"]:
         ref = gzip.open(os.path.join(GOLD, f"dropin_ref_{name}.sam.gz")).read().splitlines()
         got = r.stdout.splitlines()
