@@ -29,9 +29,13 @@ typedef struct {
     uint32_t *cnt;  /* cnt[b*4+c] = #c in codes [0, 32b) */
 } or_bwt_t;
 
+/* rank queries issued by this thread (statistics only; thread-local so that threads
+ * sharing one index do not contend on a counter) */
+static __thread uint64_t tl_queries;
+
 struct or_index {
     or_bwt_t f, r;
-    uint64_t queries;   /* rank queries issued (statistics only) */
+    int unused;
 };
 
 static uint32_t rev_pairs32(uint32_t x)   /* reverse the order of the 16 2-bit fields */
@@ -174,7 +178,7 @@ static void step_all(or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint32
     (void)rk;
     occ4(&ix->f, k, oL);
     occ4(&ix->f, l + 1, oR);
-    ix->queries += 2;
+    tl_queries += 2;
     oC[3] = 0;
     for (int c = 2; c >= 0; --c) oC[c] = oC[c + 1] + oR[c + 1] - oL[c + 1];
     for (int c = 0; c < 4; ++c) {
@@ -230,7 +234,7 @@ static int cal_width(or_index_t *ix, int len, const uint8_t *str, uint32_t *w)
             uint32_t a[4], b[4];
             occ4(&ix->r, k, a);
             occ4(&ix->r, l + 1, b);
-            ix->queries += 2;
+            tl_queries += 2;
             k = ix->f.C[c] + a[c] + 1;
             l = ix->f.C[c] + b[c];
         }
@@ -517,7 +521,7 @@ long or_cal_sa_reg_gap(const or_index_t *cix, int n, const uint32_t *lens, const
     or_opt_t local = *opt;                 /* :254, copied before the GAPE clear */
     or_opt_t *cur = opt;                   /* aux->opt (:259) */
     int max_len = 0;
-    uint64_t pops = 0, q0 = ix->queries;
+    uint64_t pops = 0, q0 = tl_queries;
     opt->mode &= ~MODE_GAPE;               /* :261 */
     for (int i = 0; i < n; ++i) if ((int)lens[i] > max_len) max_len = (int)lens[i];
     if (opt->fnr > 0.0) local.max_diff = or_cal_maxdiff(max_len, 0.02, opt->fnr);
@@ -573,7 +577,7 @@ long or_cal_sa_reg_gap(const or_index_t *cix, int n, const uint32_t *lens, const
     }
     free(wb); free(ws); free(rc); free(hv.a);
     stack_del(st);
-    if (stats) { stats[0] = ix->queries - q0; stats[1] = pops; }
+    if (stats) { stats[0] = tl_queries - q0; stats[1] = pops; }
     *hits_out = all.a ? all.a : (uint32_t *)calloc(9, sizeof(uint32_t));
     return all.n;
 }
