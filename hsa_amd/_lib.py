@@ -26,7 +26,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
     "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather", "hsa_last_pass_ms",
     "hsa_index_set_sa", "hsa_sa_position_batch", "hsa_sa_position_device", "hsa_match_gap_batch",
-    "bwt_match_gap", "bwt_match_gap_batch",
+    "bwt_match_gap", "bwt_match_gap_batch", "hsa_splice_seeds_device",
 ]
 
 
@@ -101,6 +101,13 @@ class DeviceBatch(C.Structure):
                 ("max_seed", C.c_int32)]
 
 
+class SeedBatch(C.Structure):
+    """hsa_seed_batch_t (include/hsa_gpu.h): the splice seeds of a device batch."""
+    _fields_ = [("d_jobs", C.c_void_p), ("n_jobs", C.c_int), ("d_codes", C.c_void_p), ("d_flags", C.c_void_p),
+                ("d_n_aln", C.c_void_p), ("d_hit_off", C.c_void_p), ("d_hits", C.c_void_p), ("hit_cap", C.c_uint64),
+                ("d_counters", C.c_void_p), ("max_len", C.c_int32)]
+
+
 _lib = None
 
 
@@ -160,6 +167,7 @@ def lib():
     L.hsa_match_gap_batch.restype = C.c_long
     L.hsa_match_gap_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, vp, C.c_int, u8, C.c_size_t, i32, C.c_size_t,
                                       i32, i32, u64, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(Stats)]
+    L.hsa_splice_seeds_device.argtypes = [vp, C.POINTER(Regime), C.POINTER(SeedBatch), vp]
     L.hsa_cal_sa_reg_gap_flat.restype = C.c_long
     L.hsa_cal_sa_reg_gap_flat.argtypes = [vp, C.POINTER(GapOpt), C.c_int, u32, u64, u8, C.c_size_t, i32, u32, u64,
                                           C.POINTER(C.POINTER(C.c_uint32)), i32, C.POINTER(Stats)]
@@ -237,6 +245,11 @@ class GpuIndex:
     def search_device(self, regimes, batch: "DeviceBatch"):
         rg = (Regime * len(regimes))(*regimes)
         check(lib().hsa_search_device(self.h, rg, len(regimes), C.byref(batch), None))
+
+    def splice_seeds_device(self, seed_regime, batch: "SeedBatch"):
+        """The six splice seed searches of every fallback read of a device batch
+        (hsa_splice_seeds_device); records 6 r + i on the device."""
+        check(lib().hsa_splice_seeds_device(self.h, C.byref(seed_regime), C.byref(batch), None))
 
     def set_sa(self, sa, blocks):
         """Upload the sampled SA (index_io.SaFile) and the block table (rows of

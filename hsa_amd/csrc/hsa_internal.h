@@ -40,6 +40,7 @@ struct hsa_index {
     // per-(read, strand) width rows written by k_widths, read by k_search
     void *d_wrows = nullptr; size_t d_wrows_cap = 0;
     void *d_ovf = nullptr; size_t d_ovf_cap = 0;   // device-path list of reads to re-run
+    void *d_seed = nullptr; size_t d_seed_cap = 0; // splice seed calls (hsa_splice_seeds_device)
     // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;

@@ -325,7 +325,8 @@ __global__ void __launch_bounds__(BLOCK) k_widths_import(SearchArgs a)
 __global__ void __launch_bounds__(BLOCK) k_widths_export(SearchArgs a)
 {
     const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
-    if (q >= (uint32_t)a.n_jobs) return;
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    if (q >= n_jobs) return;
     const int job = a.job_list ? a.job_list[q] : (int)q;
     if (a.flags[job] & HSA_F_OVERFLOW) return;
     const hsa_job_t J = a.jobs[job];
@@ -906,6 +907,103 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 #undef SCORE
 }
 
+
+// ---------------------------------------------------------------- splice seeds
+// The seed calls of bwt_splice_match (bwtgap.c:797-812) for every read the main pass
+// flagged HSA_F_FALLBACK: one thread per (read, strand).  The strand's three seeds
+// t = 0, 1, 2 (sl = len / 3, la_t = sl + (t == 2 ? len % 3 : 0)) search [t sl, t sl +
+// la_t) of the strand sequence with the widths of its PREFIX of length la_t
+// (bwtgap.c:807-809; bwt_cal_width type 1, bwtaln.c:84-97: forward extension on the
+// reverse BWT).  The three prefixes share their first sl positions, so one chain over
+// la_2 characters fills all three width slots; each slot ends with its own terminal
+// {0, bid + 1} (bwtaln.c:113-114).
+struct SeedArgs {
+    RankDir rev;
+    uint32_t T;
+    uint32_t C[5];
+    const hsa_job_t *rjobs;
+    const uint8_t *rcodes;
+    const uint32_t *rflags;
+    uint32_t n_reads;
+    int32_t max_seed_diff;
+    uint32_t code_stride, pair_stride;   // per read: seed codes (bytes), width pairs
+    hsa_job_t *jobs;
+    hsa_mg_job_t *mg;
+    uint8_t *codes;
+    int32_t *cw;
+    int32_t *list;
+    unsigned long long *count;
+    unsigned long long *ctr;
+};
+
+__global__ void __launch_bounds__(BLOCK) k_seed_prep(SeedArgs a)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t r = t >> 1, s = t & 1u;
+    if (r >= a.n_reads || !(a.rflags[r] & HSA_F_FALLBACK)) return;
+    const hsa_job_t R = a.rjobs[r];
+    const uint32_t L = R.len, sl = L / 3u;
+    if (sl < 1) return;
+    const uint32_t la2 = sl + L % 3u;
+    auto base = [&](uint32_t p) -> uint32_t {          // strand s, position p
+        const uint32_t c = a.rcodes[R.off + (s ? L - 1u - p : p)];
+        return s && c < 4 ? 3u - c : c;
+    };
+    // call i = 3 s + tt of read r: codes and width pairs at fixed offsets in the read's slots
+    uint32_t coff[3], poff[3], la[3];
+    {
+        uint32_t co = 0, po = 0;
+        for (uint32_t i = 0; i < 6; ++i) {
+            const uint32_t l_i = sl + (i % 3 == 2 ? L % 3u : 0u);
+            if (i / 3 == s) { coff[i % 3] = co; poff[i % 3] = po; la[i % 3] = l_i; }
+            co += l_i; po += l_i + 1;
+        }
+    }
+    uint8_t *const cbase = a.codes + (size_t)r * a.code_stride;
+    int32_t *const wbase = a.cw + 2 * (size_t)r * a.pair_stride;
+    uint32_t k = 0, l = a.T, bid = 0, bid_sl = 0, q = 0;
+    for (uint32_t p = 0; p < la2; ++p) {
+        const uint32_t c = base(p);
+        if (c < 4) {
+            uint32_t ok, ol;
+            hsa_occ1_pair(a.rev, k, l + 1u, c, ok, ol);
+            q += 2;
+            const uint32_t cc = c == 0 ? a.C[0] : c == 1 ? a.C[1] : c == 2 ? a.C[2] : a.C[3];
+            k = cc + ok + 1u;
+            l = cc + ol;
+        }
+        if (k > l || c > 3) { k = 0; l = a.T; ++bid; }
+        const int32_t w = (int32_t)(l - k + 1u);
+        for (uint32_t tt = 0; tt < 3; ++tt)
+            if (p < la[tt]) { wbase[2 * (poff[tt] + p)] = w; wbase[2 * (poff[tt] + p) + 1] = (int32_t)bid; }
+        if (p + 1 == sl) bid_sl = bid;
+        // seed codes: strand position p belongs to seed tt = p / sl (the last seed runs to la2 + 2 sl)
+    }
+    for (uint32_t tt = 0; tt < 3; ++tt) {
+        const uint32_t term_bid = (la[tt] == sl ? bid_sl : bid) + 1u;
+        wbase[2 * (poff[tt] + la[tt])] = 0;
+        wbase[2 * (poff[tt] + la[tt]) + 1] = (int32_t)term_bid;
+        for (uint32_t p = 0; p < la[tt]; ++p) cbase[coff[tt] + p] = (uint8_t)base(tt * sl + p);
+        const uint32_t j = r * 6u + 3u * s + tt;
+        hsa_job_t J;
+        J.off = (uint64_t)r * a.code_stride + coff[tt];
+        J.len = la[tt];
+        J.max_diff = a.max_seed_diff;
+        J.seed_len = (int32_t)la[tt];
+        J.regime = 0;
+        a.jobs[j] = J;
+        hsa_mg_job_t M;
+        M.wb_off = (uint64_t)r * a.pair_stride + poff[tt];
+        M.ws_off = 0;
+        M.strand = (int32_t)s;
+        M.seed = HSA_SEED_ALIAS;
+        a.mg[j] = M;
+    }
+    const unsigned long long b0 = atomicAdd(a.count, 3ull);
+    for (uint32_t tt = 0; tt < 3; ++tt) a.list[b0 + tt] = (int32_t)(r * 6u + 3u * s + tt);
+    atomicAdd(&a.ctr[7], (unsigned long long)q);
+}
+
 // ---------------------------------------------------------------- host side
 #ifdef HSA_DIAG
 extern "C" int hsa_diag_read(unsigned long long *out, int n_blocks)
@@ -1097,7 +1195,8 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     if (mg) {
         SearchArgs A = pass_args(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
                                  d_ho, d_hits, hit_cap, d_ctr, mg);
-        HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));
+        A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr;
+        if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
         const unsigned nb = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
         if (P.wide) hipLaunchKernelGGL(k_widths_import<uint16_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
         else hipLaunchKernelGGL(k_widths_import<uint8_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
@@ -1113,7 +1212,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     SearchArgs A = pass_args(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
                              d_ho, d_hits, hit_cap, d_ctr, nullptr);
     A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr;
-    if (!n_dev) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
+    if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
     size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
     if (wblocks < 1) wblocks = 1;
     if (P.wide) hipLaunchKernelGGL(k_widths<uint16_t>, dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
@@ -1421,6 +1520,69 @@ extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, i
     if ((rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, b->d_jobs, (const int32_t *)ix->d_ovf, b->n_jobs,
                           b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
                           b->hit_cap, ctr, st, nullptr, ctr + 8, 9)))
+        return rc;
+    HSA_HIP(hipEventRecord(ix->ev1, st));
+    return 0;
+}
+
+extern "C" int hsa_splice_seeds_device(hsa_index_t *ix, const hsa_regime_t *seed_regime, const hsa_seed_batch_t *b,
+                                       void *stream)
+{
+    int rc = check_regimes(seed_regime, 1);
+    if (rc) return rc;
+    if (seed_regime->max_gapo != 0) { hsa_set_error("seed searches have no gap opens (bwtgap.c:772)"); return HSA_E_ARG; }
+    if (b->max_len < 3 || b->max_len > 1023 || b->n_jobs < 0) { hsa_set_error("max_len/n_jobs out of range"); return HSA_E_ARG; }
+    const size_t n = (size_t)b->n_jobs, calls = 6 * n;
+    if (n == 0) return 0;
+    HSA_HIP(hipSetDevice(ix->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+    const uint32_t code_stride = (uint32_t)(2 * b->max_len), pair_stride = (uint32_t)(2 * b->max_len + 6);
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t o_mg = al(calls * sizeof(hsa_job_t)), o_list = o_mg + al(calls * sizeof(hsa_mg_job_t));
+    const size_t o_fl = o_list + al(calls * 4), o_cnt = o_fl + al(calls * 4), o_codes = o_cnt + 256;
+    const size_t o_cw = o_codes + al(n * code_stride), total = o_cw + n * pair_stride * 8 + 256;
+    if ((rc = hsa_grow(&ix->d_seed, &ix->d_seed_cap, total))) return rc;
+    char *d = (char *)ix->d_seed;
+    unsigned long long *cnt = (unsigned long long *)(d + o_cnt);
+    unsigned long long *ctr = (unsigned long long *)b->d_counters;
+    HSA_HIP(hipMemsetAsync(cnt, 0, 8, st));
+    SeedArgs S;
+    S.rev = RankDir{ix->blk[1], ix->risa0};
+    S.T = ix->T;
+    memcpy(S.C, ix->C, sizeof S.C);
+    S.rjobs = b->d_jobs; S.rcodes = b->d_codes; S.rflags = b->d_flags; S.n_reads = (uint32_t)n;
+    S.max_seed_diff = seed_regime->max_diff;
+    S.code_stride = code_stride; S.pair_stride = pair_stride;
+    S.jobs = (hsa_job_t *)d; S.mg = (hsa_mg_job_t *)(d + o_mg); S.codes = (uint8_t *)(d + o_codes);
+    S.cw = (int32_t *)(d + o_cw); S.list = (int32_t *)(d + o_list); S.count = cnt; S.ctr = ctr;
+    // the search pass zeroes the counters first; the width queries are added after it
+    void *before = ix->d_in;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1024))) return rc;
+    int nb = 0;
+    if ((rc = stage_regimes(ix, seed_regime, 1, (char *)ix->d_in, nb, st, before != ix->d_in))) return rc;
+    const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
+    const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
+    const int seed_max = b->max_len / 3 + 2;
+    LaunchPlan P, B;
+    const bool wide = need_wide(seed_regime, 1);
+    if ((rc = plan_launch(ix, (int)calls, seed_max, 0, nb, false, wide, false, P)) ||
+        (rc = plan_launch(ix, (int)calls, seed_max, 0, nb, false, wide, true, B)))
+        return rc;
+    if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, calls * 4 + 64))) return rc;
+    HSA_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_seed_prep, dim3((unsigned)((2 * n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, S);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipEventRecord(ix->ev0, st));
+    const MgPass mgp{S.mg, S.cw};
+    uint32_t *sfl = (uint32_t *)(d + o_fl);
+    // qctr 10: the pass's queue head, so that counter [7] (width queries) survives
+    if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, S.jobs, S.list, (int)calls, seed_max, 0, S.codes,
+                          b->d_n_aln, sfl, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st, (int32_t *)ix->d_ovf, cnt, 10,
+                          &mgp)))
+        return rc;
+    if ((rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, S.jobs, (const int32_t *)ix->d_ovf, (int)calls, seed_max, 0,
+                          S.codes, b->d_n_aln, sfl, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st, nullptr, ctr + 8, 9,
+                          &mgp)))
         return rc;
     HSA_HIP(hipEventRecord(ix->ev1, st));
     return 0;

@@ -161,6 +161,26 @@ long hsa_match_gap_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_reg
                          const int32_t *widths, size_t width_pairs, int32_t *widths_out,
                          int32_t *n_aln, uint64_t *hit_off, uint32_t **hits, hsa_stats_t *stats);
 
+/* ---- the splice path's seed searches on the device ----
+ * For every read of a device batch that the main pass flagged HSA_F_FALLBACK, the six
+ * seed searches bwt_splice_match can make (bwtgap.c:797-812, restated in
+ * hsa_amd/splice.py): seed t of strand s (t = 0, 1, 2; sl = len / 3) searches the
+ * strand sequence [t sl, t sl + la) with la = sl (+ len % 3 for t = 2), width_back =
+ * width_seed = the widths of the strand's PREFIX of length la, and the seed options
+ * (GAPE cleared, no gaps, max_diff = max_seed_diff, seed_len = la) given as one regime.
+ * Prefix widths, the calls and their searches all run on the device.  Call 3 s + t of
+ * read r is output record 6 r + 3 s + t; records of other reads are left untouched. */
+typedef struct {
+    const hsa_job_t *d_jobs; int n_jobs;  /* the main pass's reads (off, len) */
+    const uint8_t *d_codes;
+    const uint32_t *d_flags;              /* the main pass's per-read flags */
+    int32_t *d_n_aln; uint64_t *d_hit_off; /* 6 * n_jobs records each */
+    uint32_t *d_hits; uint64_t hit_cap;   /* hit records (9 u32) */
+    uint64_t *d_counters;                 /* >= 16 u64 of device scratch: [1] hits, [2] rank queries, [4] pops */
+    int32_t max_len;                      /* longest read */
+} hsa_seed_batch_t;
+int hsa_splice_seeds_device(hsa_index_t *ix, const hsa_regime_t *seed_regime, const hsa_seed_batch_t *b, void *stream);
+
 /* SA index -> text position (BWTSaValue BWT.c:1195 + BWTRetrievePositionFromSAIndex
  * 2BWT-Interface.c:329), batched.  hsa_index_set_sa uploads the sampled suffix array
  * as BWTLoad holds it (values[0] = -1, (T+s)/s values, interval s) and the chromosome

@@ -129,3 +129,86 @@ def test_dropin_both_entry_points_sam_identical(name, reads):
         got = r.stdout.splitlines()
         diff = [(i, a, b) for i, (a, b) in enumerate(zip(ref, got)) if a != b][:5]
         pytest.fail(f"SAM differs: {len(got)} vs {len(ref)} lines; first differences {diff}")
+
+
+def test_splice_seeds_device_match_oracle(tiny):
+    """hsa_splice_seeds_device: after a device main pass over the splice read set
+    (-n 4 -o 1, steady state), the six seed searches of every fallback read -- prefix
+    widths, calls and searches all on the device -- equal the restated bwt_match_gap on
+    the calls hsa_amd/splice.py builds (which test_splice_seeds.py pins to the
+    reference's own seed calls)."""
+    import torch
+    from hsa_amd import splice
+    from hsa_amd._lib import JOB_DTYPE, DeviceBatch, SeedBatch, regime_of
+    from oracle_ctypes import Opt, OracleIndex, default_opt
+    from test_splice_seeds import read_fastq
+    lens, codes = read_fastq(os.path.join(GOLD, MAN["splice_reads"]))
+    n = len(lens)
+    opt = dict(default_opt(), max_diff=4, fnr=-1.0, max_gapo=1)
+    opt["mode"] &= ~0x01
+    ox = OracleIndex(*index_io.read_index(INDEX["tiny"]))
+    e_n, e_f, _, _ = ox.cal_sa_reg_gap(lens, codes, Opt.from_dict(opt))
+    n_stacks = splice.n_stacks_of(opt)
+    rg = regime_of(opt, n_stacks, opt["max_diff"])
+    jobs = np.zeros(n, JOB_DTYPE)
+    jobs["off"] = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]])
+    jobs["len"] = lens
+    jobs["max_diff"] = opt["max_diff"]
+    jobs["seed_len"] = np.where(lens > opt["seed_len"], opt["seed_len"], 0x7FFFFFFF)
+
+    def dev(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+    d_jobs, d_codes = dev(jobs.view(np.uint8)), dev(codes)
+    cap = n * 64
+    m = dict(n=torch.zeros(n, dtype=torch.int32, device="cuda"), f=torch.zeros(n, dtype=torch.int32, device="cuda"),
+             o=torch.zeros(n, dtype=torch.int64, device="cuda"), h=torch.zeros(cap * 9, dtype=torch.int32, device="cuda"),
+             c=torch.zeros(16, dtype=torch.int64, device="cuda"))
+    b = DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=n, d_codes=d_codes.data_ptr(), d_n_aln=m["n"].data_ptr(),
+                    d_flags=m["f"].data_ptr(), d_hit_off=m["o"].data_ptr(), d_hits=m["h"].data_ptr(), hit_cap=cap,
+                    d_counters=m["c"].data_ptr(), max_len=int(lens.max()), max_seed=opt["seed_len"])
+    tiny.search_device([rg], b)
+    torch.cuda.synchronize()
+    g_f = m["f"].cpu().numpy().astype(np.uint32)
+    assert np.array_equal(g_f & 1, e_f & 1)
+    # the seeds on the device
+    so = splice.seed_options(opt)
+    srg = regime_of(so, n_stacks, so["max_diff"])
+    sn = torch.full((6 * n,), -7, dtype=torch.int32, device="cuda")
+    so_ = torch.zeros(6 * n, dtype=torch.int64, device="cuda")
+    sh = torch.zeros(cap * 9, dtype=torch.int32, device="cuda")
+    sc = torch.zeros(16, dtype=torch.int64, device="cuda")
+    sb = SeedBatch(d_jobs=d_jobs.data_ptr(), n_jobs=n, d_codes=d_codes.data_ptr(), d_flags=m["f"].data_ptr(),
+                   d_n_aln=sn.data_ptr(), d_hit_off=so_.data_ptr(), d_hits=sh.data_ptr(), hit_cap=cap,
+                   d_counters=sc.data_ptr(), max_len=int(lens.max()))
+    tiny.splice_seeds_device(srg, sb)
+    torch.cuda.synchronize()
+    g_n = sn.cpu().numpy()
+    g_o = so_.cpu().numpy()
+    g_h = sh.cpu().numpy().view(np.uint32).reshape(-1, 9)
+    fb = np.flatnonzero(e_f & 1)
+    fb = fb[lens[fb] >= 3]
+    assert len(fb) > 100
+    # records of reads that did not fall back stay untouched
+    others = np.setdiff1d(np.arange(n), fb)
+    assert (g_n.reshape(n, 6)[others] == -7).all()
+
+    def width_fn(wl, wc):
+        out, o = [], 0
+        for L in wl:
+            out.append(ox.cal_width(wc[o:o + int(L)]).reshape(-1))
+            o += int(L)
+        return np.concatenate(out).astype(np.uint32)
+
+    hb = splice.seed_calls(lens, codes, fb, opt, width_fn)
+    bad = 0
+    for c in hb["calls"]:
+        o = Opt.from_dict(dict(so, seed_len=int(c["len"])))
+        seq = hb["codes"][c["off"]:c["off"] + c["len"]]
+        w = hb["widths"][c["wb_off"]:c["wb_off"] + c["len"] + 1]
+        exp, _ = ox.match_gap(o, n_stacks, seq, c["strand"], w, 2)
+        r = 6 * int(c["read"]) + int(c["i"])
+        got = g_h[g_o[r]:g_o[r] + g_n[r]]
+        bad += not np.array_equal(got, exp)
+    assert bad == 0, f"{bad} of {len(hb['calls'])} seed calls differ"
+    assert int(sc[7].item()) > 0     # prefix-width rank queries were counted
