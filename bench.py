@@ -127,6 +127,15 @@ def diag_dump(path):
         json.dump(out, f)
 
 
+def cpu_widths(ox, wl, wc):
+    """bwt_cal_width type 1 of each sequence on the CPU restatement (flat pairs)."""
+    out, o = [], 0
+    for L in wl:
+        out.append(ox.cal_width(wc[o:o + int(L)]).reshape(-1))
+        o += int(L)
+    return np.concatenate(out).astype(np.uint32)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -136,9 +145,10 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--cpu-sample", type=int, default=20000, help="reads timed on the CPU restatement")
     ap.add_argument("--parity-sample", type=int, default=4000, help="reads checked against the CPU restatement")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
                     help="BASELINE.json config: 2 = 0-4 substitutions, -n 4 -o 0 (default, the metric's config); "
-                         "3 = one 1-3 bp indel + 0-2 substitutions, -n 4 -o 1")
+                         "3 = one 1-3 bp indel + 0-2 substitutions, -n 4 -o 1; "
+                         "4 = 150 bp spliced reads, -n 4 -o 1, main path + the splice path's seed searches")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0)
     a = ap.parse_args()
@@ -158,6 +168,7 @@ def main():
     _lib.configure(a.waves, a.pool, 0)
 
     T = a.genome
+    RL = 150 if a.config == 4 else READ_LEN
     t0 = time.time()
     gi, res = build_index(T, GENOME_SEED, device)
     log(f"[bench] rank {rank}: index ready ({gi.nbytes() / 2**30:.2f} GiB of rank blocks) in {time.time() - t0:.1f} s")
@@ -173,6 +184,8 @@ def main():
         gidx = j * world + rank
         if a.config == 2:
             reads, _ = synth.make_reads(genome, recs, a.batch, READ_LEN, 5 * 1_000_000 + gidx, max_mm=4)
+        elif a.config == 4:  # SURVEY §8d config 4 (seed 7): exon A 40-110, GT..AG intron 200-5000
+            reads, _ = synth.make_spliced_reads(genome, recs, a.batch, RL, 7 * 1_000_000 + gidx)
         else:   # SURVEY §8d config 3 reads (seed 6): one indel of 1-3 bp + 0-2 substitutions
             reads, _ = synth.make_reads(genome, recs, a.batch, READ_LEN, 6 * 1_000_000 + gidx, indel=True,
                                         max_mm_indel=2)
@@ -193,8 +206,8 @@ def main():
                 max_del_occ=opt.max_del_occ, max_entries=opt.max_entries, max_gapo=max_gapo, max_gape=opt.max_gape,
                 max_seed_diff=opt.max_seed_diff, max_top2=opt.max_top2, n_stacks=n_stacks, max_diff=opt.max_diff)
     jobs = np.zeros(a.batch, _lib.JOB_DTYPE)
-    jobs["off"] = np.arange(a.batch, dtype=np.uint64) * READ_LEN
-    jobs["len"] = READ_LEN
+    jobs["off"] = np.arange(a.batch, dtype=np.uint64) * RL
+    jobs["len"] = RL
     jobs["max_diff"] = opt.max_diff
     jobs["seed_len"] = opt.seed_len
     d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).cuda()
@@ -207,6 +220,16 @@ def main():
                          o=torch.zeros(a.batch, dtype=torch.int64, device="cuda"),
                          h=torch.zeros(hit_cap * 9, dtype=torch.int32, device="cuda"),
                          c=torch.zeros(16, dtype=torch.int64, device="cuda")))
+        if a.config == 4:   # the splice seeds: six records per read
+            outs[-1].update(sn=torch.zeros(6 * a.batch, dtype=torch.int32, device="cuda"),
+                            so=torch.zeros(6 * a.batch, dtype=torch.int64, device="cuda"),
+                            sh=torch.zeros(6 * a.batch * 4 * 9, dtype=torch.int32, device="cuda"),
+                            sc=torch.zeros(16, dtype=torch.int64, device="cuda"))
+    if a.config == 4:
+        from hsa_amd import splice
+        from hsa_amd._lib import SeedBatch, regime_of
+        so_opt = splice.seed_options(opt.as_dict())
+        srg = regime_of(so_opt, n_stacks, so_opt["max_diff"])
 
     def launch(j):
         j %= nd
@@ -214,8 +237,13 @@ def main():
         b = DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[j].data_ptr(),
                         d_n_aln=o["n"].data_ptr(), d_flags=o["f"].data_ptr(), d_hit_off=o["o"].data_ptr(),
                         d_hits=o["h"].data_ptr(), hit_cap=hit_cap, d_counters=o["c"].data_ptr(),
-                        max_len=READ_LEN, max_seed=opt.seed_len)
+                        max_len=RL, max_seed=opt.seed_len)
         gi.search_device([rg], b)
+        if a.config == 4:   # same stream: the seeds read the main pass's flags
+            gi.splice_seeds_device(srg, SeedBatch(
+                d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[j].data_ptr(), d_flags=o["f"].data_ptr(),
+                d_n_aln=o["sn"].data_ptr(), d_hit_off=o["so"].data_ptr(), d_hits=o["sh"].data_ptr(),
+                hit_cap=6 * a.batch * 4, d_counters=o["sc"].data_ptr(), max_len=RL))
 
     # the measured ceiling for this access pattern: random whole 64-B blocks over a
     # table as large as the rank index (before the timed region, same process)
@@ -245,10 +273,25 @@ def main():
     elapsed = time.perf_counter() - t0
     kms = [e0.elapsed_time(e1) for e0, e1 in ev]
     # per-kernel split of one more (untimed) step: k_widths, then k_search
-    launch(a.warmup + a.steps)
-    split_ms = gi.last_pass_ms()
-    torch.cuda.synchronize()
-    log(f"[bench] rank {rank}: kernel split of one step: k_widths {split_ms[0]:.2f} ms, k_search {split_ms[1]:.2f} ms")
+    if a.config == 4:   # main path, then the splice seeds
+        e3 = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e3[0].record(lib_stream)
+        gi.search_device([rg], DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[0].data_ptr(),
+                                           d_n_aln=outs[0]["n"].data_ptr(), d_flags=outs[0]["f"].data_ptr(),
+                                           d_hit_off=outs[0]["o"].data_ptr(), d_hits=outs[0]["h"].data_ptr(),
+                                           hit_cap=hit_cap, d_counters=outs[0]["c"].data_ptr(), max_len=RL,
+                                           max_seed=opt.seed_len))
+        e3[1].record(lib_stream)
+        launch(0)
+        e3[2].record(lib_stream)
+        torch.cuda.synchronize()
+        split_ms = (e3[0].elapsed_time(e3[1]), e3[1].elapsed_time(e3[2]) - e3[0].elapsed_time(e3[1]))
+        log(f"[bench] rank {rank}: split of one step: main path {split_ms[0]:.2f} ms, splice seeds {split_ms[1]:.2f} ms")
+    else:
+        launch(a.warmup + a.steps)
+        split_ms = gi.last_pass_ms()
+        torch.cuda.synchronize()
+        log(f"[bench] rank {rank}: kernel split of one step: k_widths {split_ms[0]:.2f} ms, k_search {split_ms[1]:.2f} ms")
     if os.environ.get("HSA_DIAG_OUT"):
         diag_dump(os.environ["HSA_DIAG_OUT"])
     log(f"[bench] rank {rank}: per-step device ms {[round(x, 2) for x in kms]}, wall {elapsed * 1e3:.1f} ms")
@@ -262,6 +305,11 @@ def main():
     per = {j: sum(1 for s in range(a.steps) if (a.warmup + s) % nd == j) for j in used}
     ctr = np.stack([outs[j]["c"].cpu().numpy() * per[j] for j in used])
     queries = int(ctr[:, 2].sum())
+    seed_queries = 0
+    if a.config == 4:   # the seed searches' rank queries and their prefix widths'
+        sctr = np.stack([outs[j]["sc"].cpu().numpy() * per[j] for j in used])
+        seed_queries = int(sctr[:, 2].sum() + sctr[:, 7].sum())
+        queries += seed_queries
     blocks = int(ctr[:, 3].sum())
     pops = int(ctr[:, 4].sum())
     flags = np.concatenate([np.tile(outs[j]["f"].cpu().numpy(), per[j]) for j in used])
@@ -306,16 +354,23 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": f"{a.batch // 1000}k x 100bp reads per step and GPU, "
-                                   + ("0-4 substitutions" if a.config == 2 else "one 1-3 bp indel + 0-2 substitutions")
+            "config": {"workload": f"{a.batch // 1000}k x {RL}bp reads per step and GPU, "
+                                   + {2: "0-4 substitutions", 3: "one 1-3 bp indel + 0-2 substitutions",
+                                      4: "spliced (exon 40-110 bp, GT..AG intron 200-5000 bp), main path + the splice "
+                                         "path's 6 seed searches per fallback read on the GPU (the host's "
+                                         "correlation/extension not included)"}[a.config]
                                    + f", 50% rc, vs synthetic hg19-sized 2BWT ({T} bp, {RECORDS} records), {opt_str} "
                                    f"(BASELINE configs[{a.config - 1}]); {a.steps} timed steps",
-                       "genome_bp": T, "reads_per_step": a.batch, "read_len": READ_LEN, "options": opt_str,
+                       "genome_bp": T, "reads_per_step": a.batch, "read_len": RL, "options": opt_str,
                        "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_per_launch() if a.config == 2 else None,
-                         "kernel": "k_widths+k_search (one step)", "kernel_ms_mean": round(mean_kms, 3),
-                         "kernel_split_ms": {"k_widths": round(split_ms[0], 3), "k_search": round(split_ms[1], 3)},
+                         "kernel": "k_widths+k_search (one step)" if a.config != 4 else
+                                   "main path (k_widths+k_search) + splice seeds (k_seed_prep+k_widths_import+k_search+"
+                                   "k_widths_export)", "kernel_ms_mean": round(mean_kms, 3),
+                         "kernel_split_ms": {"k_widths": round(split_ms[0], 3), "k_search": round(split_ms[1], 3)}
+                         if a.config != 4 else {"main_path": round(split_ms[0], 3),
+                                                "splice_seeds": round(split_ms[1], 3)},
                          "algorithmic_bytes_per_launch": q_per_launch * BYTES_PER_QUERY,
                          "rank_queries_per_read": round(queries / reads_local, 1),
                          "sectors_per_query": round(blocks / max(queries, 1), 4),
@@ -327,6 +382,8 @@ def main():
             "mapped_frac": round(mapped_all / reads_all, 4), "fallback_frac": round(fallback_all / reads_all, 4),
             "pops_per_read": round(pops / reads_local, 1),
         }
+        if a.config == 4:
+            result["seed_rank_queries_per_read"] = round(seed_queries / reads_local, 1)
 
     # parity on a sample and the CPU baseline (rank 0 at N=1 only)
     if rank == 0 and world == 1 and (a.parity_sample or a.cpu_sample):
@@ -339,7 +396,7 @@ def main():
         if a.parity_sample:
             n = min(a.parity_sample, a.batch)
             r0 = batches[a.warmup % nd][:n]
-            o_n, o_f, o_h, _ = ox.cal_sa_reg_gap(np.full(n, READ_LEN, np.uint32), r0.reshape(-1), Opt.from_dict(od))
+            o_n, o_f, o_h, _ = ox.cal_sa_reg_gap(np.full(n, RL, np.uint32), r0.reshape(-1), Opt.from_dict(od))
             last = outs[a.warmup % nd]
             g_n = last["n"].cpu().numpy()[:n]
             g_f = last["f"].cpu().numpy()[:n].astype(np.uint32)
@@ -353,14 +410,47 @@ def main():
                     bad += 1
             result["parity_sample"] = {"reads": n, "mismatching_reads": bad, "against": "oracle (C restatement)"}
             log(f"[bench] parity sample: {n} reads, {bad} differ from the CPU restatement")
-        if a.cpu_sample:
+            if a.config == 4:   # the seed searches of the sample's first fallback reads
+                fb = np.flatnonzero(o_f & 1)[:300]
+                sb = splice.seed_calls_fixed(r0[fb], od, lambda wl, wc: cpu_widths(ox, wl, wc))
+                g_sn = last["sn"].cpu().numpy()
+                g_so = last["so"].cpu().numpy()
+                g_sh = last["sh"].cpu().numpy().view(np.uint32).reshape(-1, 9)
+                sbad = 0
+                for c in sb["calls"]:
+                    o = Opt.from_dict(dict(sb["opt"], seed_len=int(c["len"])))
+                    exp, _ = ox.match_gap(o, n_stacks, sb["codes"][c["off"]:c["off"] + c["len"]], c["strand"],
+                                          sb["widths"][c["wb_off"]:c["wb_off"] + c["len"] + 1], 2)
+                    r = 6 * int(fb[c["read"]]) + int(c["i"])
+                    sbad += not np.array_equal(g_sh[g_so[r]:g_so[r] + g_sn[r]], exp)
+                result["parity_sample"]["seed_calls"] = len(sb["calls"])
+                result["parity_sample"]["mismatching_seed_calls"] = sbad
+                log(f"[bench] parity sample: {len(sb['calls'])} seed calls, {sbad} differ from the CPU restatement")
+        if a.cpu_sample and a.config == 4:
+            # main path + the seed searches of its fallback reads, 1 thread (the seed calls
+            # are driven from Python one by one, so threads would contend on the GIL)
+            n = min(a.cpu_sample // 4, a.batch)
+            rs = batches[(a.warmup + 1) % nd][-n:]
+            t0 = time.perf_counter()
+            _, fl, _, _ = ox.cal_sa_reg_gap(np.full(n, RL, np.uint32), rs.reshape(-1), Opt.from_dict(od))
+            sb = splice.seed_calls_fixed(rs[np.flatnonzero(fl & 1)], od, lambda wl, wc: cpu_widths(ox, wl, wc))
+            for c in sb["calls"]:
+                ox.match_gap(Opt.from_dict(dict(sb["opt"], seed_len=int(c["len"]))), n_stacks,
+                             sb["codes"][c["off"]:c["off"] + c["len"]], c["strand"],
+                             sb["widths"][c["wb_off"]:c["wb_off"] + c["len"] + 1], 2)
+            dt1 = time.perf_counter() - t0
+            result["cpu_baseline"] = {"value": round(n / dt1, 1), "unit": "reads/s", "cores": 1, "kind": "port",
+                                      "sample": f"{n} reads of the same workload: bwa_cal_sa_reg_gap restatement + "
+                                                f"the 6 seed searches of its {int((fl & 1).sum())} fallback reads, "
+                                                f"1 thread, in {dt1:.1f} s"}
+        elif a.cpu_sample:
             # 1 thread, then one thread per host core on disjoint chunks (independent
             # batches, as BASELINE.md §3 plans; ctypes releases the GIL in the C call)
             from concurrent.futures import ThreadPoolExecutor
             n = min(a.cpu_sample, a.batch)
             rs = batches[(a.warmup + 1) % nd][-n:]
             t0 = time.perf_counter()
-            ox.cal_sa_reg_gap(np.full(n, READ_LEN, np.uint32), rs.reshape(-1), Opt.from_dict(od))
+            ox.cal_sa_reg_gap(np.full(n, RL, np.uint32), rs.reshape(-1), Opt.from_dict(od))
             dt1 = time.perf_counter() - t0
             cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), len(os.sched_getaffinity(0))))
             per = max(1, min(n, a.batch // cores))
@@ -368,7 +458,7 @@ def main():
             chunks = [src[i * per:(i + 1) * per] for i in range(cores)]
 
             def one(ch):
-                ox.cal_sa_reg_gap(np.full(len(ch), READ_LEN, np.uint32), ch.reshape(-1), Opt.from_dict(od))
+                ox.cal_sa_reg_gap(np.full(len(ch), RL, np.uint32), ch.reshape(-1), Opt.from_dict(od))
 
             t0 = time.perf_counter()
             with ThreadPoolExecutor(cores) as ex:

@@ -192,6 +192,56 @@ def make_reads(genome: np.ndarray, records, n: int, L: int, seed: int,
     return reads, truth
 
 
+def make_spliced_reads(genome, records, n: int, L: int, seed: int, rc_frac: float = 0.5, tries: int = 64,
+                       chunk: int = 200_000):
+    """Spliced reads: exon A of 40-110 bases, an intron of
+    200-5000 bases that reads GT...AG on the + strand, then exon B up to L bases; 50 %
+    reverse-complemented.  Exon-A and intron lengths are drawn uniformly and rejected
+    until the motifs match (a read with no match among `tries` draws redraws its start).
+    Returns (reads (n, L) uint8, truth dict of start, exon_a, intron, strand)."""
+    reads = np.empty((n, L), dtype=np.uint8)
+    truth = {k: np.zeros(n, dtype=np.int64) for k in ("start", "exon_a", "intron", "strand")}
+    span = 110 + 5000 + L
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        sub = seed * 1_000_003 + c0
+        todo = np.arange(m)
+        st = np.zeros(m, np.int64)
+        ea = np.zeros(m, np.int64)
+        it = np.zeros(m, np.int64)
+        rnd = 0
+        while len(todo):
+            k = len(todo)
+            st[todo] = _starts(sub + 7919 * rnd, k, L, span, records, 0)
+            # donor: GT right after exon A
+            ca = 40 + (_u(sub + 7919 * rnd, k * tries, 1) % np.uint64(71)).astype(np.int64).reshape(k, tries)
+            d = st[todo][:, None] + ca
+            okd = (np.asarray(genome[d], np.uint8) == 2) & (np.asarray(genome[d + 1], np.uint8) == 3)
+            # acceptor: AG as the intron's last two bases
+            ci = 200 + (_u(sub + 7919 * rnd, k * tries, 2) % np.uint64(4801)).astype(np.int64).reshape(k, tries)
+            fd = np.argmax(okd, axis=1)
+            dd = st[todo] + ca[np.arange(k), fd]
+            a = dd[:, None] + ci
+            oka = (np.asarray(genome[a - 2], np.uint8) == 0) & (np.asarray(genome[a - 1], np.uint8) == 2)
+            fa = np.argmax(oka, axis=1)
+            good = okd.any(axis=1) & oka.any(axis=1)
+            ea[todo[good]] = ca[np.arange(k), fd][good]
+            it[todo[good]] = ci[np.arange(k), fa][good]
+            todo = todo[~good]
+            rnd += 1
+        pos = np.arange(L)[None, :]
+        src = np.where(pos < ea[:, None], st[:, None] + pos, st[:, None] + it[:, None] + pos)
+        r = np.asarray(genome[src], dtype=np.uint8)
+        strand = (_u(sub, m, 3) % np.uint64(1 << 20)).astype(np.float64) / float(1 << 20) < rc_frac
+        r = np.where(strand[:, None], revcomp_codes(r), r)
+        reads[c0:c0 + m] = r
+        truth["start"][c0:c0 + m] = st
+        truth["exon_a"][c0:c0 + m] = ea
+        truth["intron"][c0:c0 + m] = it
+        truth["strand"][c0:c0 + m] = strand
+    return reads, truth
+
+
 def write_fastq(path: str, reads: np.ndarray, prefix: str = "r") -> None:
     n, L = reads.shape
     qual = b"I" * L
