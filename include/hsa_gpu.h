@@ -7,8 +7,8 @@
  *
  * What each group replaces in the reference:
  *   hsa_index_*        -- BWTLoad2BWT's in-memory BWT + Occ tables (2BWT-Interface.c:13,
- *                         BWT.c:107): uploaded once to HBM and re-laid out into 64-byte
- *                         rank blocks (4 x u32 counts + 192 two-bit codes).
+ *                         BWT.c:107): uploaded once to HBM and re-laid out into 16-byte
+ *                         rank blocks (3 x u32 counts + 16 two-bit codes).
  *   hsa_occ4_batch     -- BWTAllOccValue (BWT.c:793) for a batch of positions.
  *   hsa_step_batch     -- BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235).
  *   hsa_width_batch    -- bwt_cal_width type 1 (bwtaln.c:73-98).
@@ -16,6 +16,13 @@
  *                         rc strand then forward strand, bwt_cal_width x2 and
  *                         bwt_match_gap (bwtgap.c:118-331) per strand (two kernels:
  *                         the widths of every read and strand, then the searches).
+ *   hsa_match_gap_batch -- bwt_match_gap (bwtgap.c:118-331) called directly with the
+ *                         caller's widths, as the splice path calls it (bwtgap.c:812,
+ *                         :919, :1192).
+ *   hsa_splice_seeds_device -- the six seed searches of bwt_splice_match
+ *                         (bwtgap.c:797-812) for every fallback read of a device batch.
+ *   hsa_sa_position_*  -- BWTSaValue (BWT.c:1195) + BWTRetrievePositionFromSAIndex
+ *                         (2BWT-Interface.c:329).
  *
  * Errors: every call returns 0 on success or a negative HSA_E* code and leaves a
  * message readable with hsa_last_error().  The library never falls back to a CPU
