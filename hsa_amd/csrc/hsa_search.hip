@@ -357,8 +357,10 @@ __device__ unsigned long long g_dctr[16];
 #define DC(i) ((void)0)
 #endif
 
-template <int MW, bool GAPS, typename WT>
-__global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
+// NT = lanes per workgroup: 256, or 64 when per-lane LDS (many buckets, long reads)
+// would leave fewer than 16 waves per CU in 256-lane workgroups (plan_launch)
+template <int MW, bool GAPS, typename WT, int NT>
+__global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 {
     using F = WFmt<WT>;
 #ifdef HSA_DIAG
@@ -369,9 +371,9 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 #endif
     extern __shared__ __align__(16) uint8_t s_lds[];
     const uint32_t tid = threadIdx.x;
-    const uint32_t gid = blockIdx.x * BLOCK + tid;
+    const uint32_t gid = blockIdx.x * NT + tid;
     const int lane = (int)(tid & 63);
-    for (uint32_t t = tid; t < 2 * MAXB; t += BLOCK) s_lds[t] = a.bmap[t];
+    for (uint32_t t = tid; t < 2 * MAXB; t += NT) s_lds[t] = a.bmap[t];
     static_assert(2 * sizeof(hsa_regime_t) <= 128, "regime LDS slot");
     hsa_regime_t *const s_reg = reinterpret_cast<hsa_regime_t *>(s_lds + 2 * MAXB);
     if (tid < 2 * sizeof(hsa_regime_t) / 4)
@@ -387,12 +389,12 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
 #define POOL(s) a.pool[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
 #define NXT(s) a.nxt[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
 #define HB(i) a.hbuf[(wv * a.hcap * 9 + (uint32_t)(i)) * 64 + lane]
-#define HEAD(b) s_heads[(uint32_t)(b) * BLOCK + tid]
+#define HEAD(b) s_heads[(uint32_t)(b) * NT + tid]
     // pruning elements in LDS, word-interleaved: the word holding elements
-    // [EPW*q, EPW*q + EPW) of a lane is word q * BLOCK + tid, so every lane reads its
+    // [EPW*q, EPW*q + EPW) of a lane is word q * NT + tid, so every lane reads its
     // own bank whatever position it is at, and a row copies in one store per word
-#define WB(p) s_wb[(((uint32_t)(p) / F::EPW) * BLOCK + tid) * F::EPW + (uint32_t)(p) % F::EPW]
-#define WS(p) s_ws[(((uint32_t)(p) / F::EPW) * BLOCK + tid) * F::EPW + (uint32_t)(p) % F::EPW]
+#define WB(p) s_wb[(((uint32_t)(p) / F::EPW) * NT + tid) * F::EPW + (uint32_t)(p) % F::EPW]
+#define WS(p) s_ws[(((uint32_t)(p) / F::EPW) * NT + tid) * F::EPW + (uint32_t)(p) % F::EPW]
 #define RG(f) (s_reg[C_REG(ctl)].f)
 
     // ---- persistent per-lane state
@@ -474,19 +476,19 @@ __global__ void __launch_bounds__(BLOCK, 4) k_search(SearchArgs a)
     // start bwt_match_gap (bwtgap.c:141-142)
     auto start_strand = [&]() {
         // LDS-DMA (global_load_lds_dword): word q of every active lane lands at
-        // word q * BLOCK + tid, which is exactly the wave's slice of the LDS layout, so
+        // word q * NT + tid, which is exactly the wave's slice of the LDS layout, so
         // the whole row is in flight at once and one wait covers it
         const uint32_t *src = reinterpret_cast<const uint32_t *>(a.wb) + row_base(a.rb / 4);
         uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + (tid & ~63u);
         const uint32_t nwb = a.rb / 4;                 // row capacity in words (uniform)
         for (uint32_t q = 0; q < nwb; ++q)
-            __builtin_amdgcn_global_load_lds(src + q * 64, db + q * BLOCK, 4, 0, 0);
+            __builtin_amdgcn_global_load_lds(src + q * 64, db + q * NT, 4, 0, 0);
         if (C_SEED(ctl) && !C_ALIAS(ctl)) {
             const uint32_t *ss = reinterpret_cast<const uint32_t *>(a.ws) + row_base(a.rs / 4);
             uint32_t *const ds = reinterpret_cast<uint32_t *>(s_ws) + (tid & ~63u);
             const uint32_t nws = a.rs / 4;
             for (uint32_t q = 0; q < nws; ++q)
-                __builtin_amdgcn_global_load_lds(ss + q * 64, ds + q * BLOCK, 4, 0, 0);
+                __builtin_amdgcn_global_load_lds(ss + q * 64, ds + q * NT, 4, 0, 0);
         }
         __builtin_amdgcn_s_waitcnt(0);                 // the DMA writes are visible to LDS reads
         DC(15);
@@ -1070,6 +1072,7 @@ static bool mm_buckets(const hsa_regime_t *rg, int n, const uint8_t *bmap)
 
 struct LaunchPlan {
     size_t lanes, blocks;
+    uint32_t nt;                     // lanes per workgroup of k_search (256 or 64)
     uint32_t pcap, hcap, nb;
     bool gaps, wide;                 // gap opens possible; 16-bit pruning elements (WFmt)
     uint32_t off_heads, off_wb, off_ws;
@@ -1083,39 +1086,56 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     P.gaps = gaps;
     P.wide = wide;
     const uint32_t esz = wide ? 2u : 1u;
-    P.off_heads = 2 * MAXB + 128;   // score tables, then the two regimes
-    P.off_wb = P.off_heads + (uint32_t)nb * BLOCK * 2;
     const uint32_t epw = 4u / esz;                       // elements per LDS word (WFmt::EPW)
-    P.off_ws = P.off_wb + ((uint32_t)max_len / epw + 1u) * BLOCK * 4u;
-    P.lds = ((size_t)P.off_ws + ((size_t)max_seed / epw + 1u) * BLOCK * 4u + 15) / 16 * 16;
-    if (P.lds > 160 * 1024) { hsa_set_error("reads too long for the LDS budget (%zu bytes)", P.lds); return HSA_E_ARG; }
-    // Resident workgroups per CU, from gfx950's own limits: 160 KiB of LDS per CU,
-    // and __launch_bounds__(BLOCK, 4) caps VGPRs so 4 workgroups of 4 waves fit.
+    // Resident workgroups per CU, from gfx950's own limits: 160 KiB of LDS per CU, at
+    // most 16 waves (__launch_bounds__(NT, 4) caps VGPRs at 4 waves per SIMD).  The
+    // per-lane LDS (bucket heads, pruning rows) decides between 256-lane workgroups
+    // and 64-lane ones, which pack the CU's LDS more finely: -n 4 -o 1 has 39 buckets
+    // and ~220 B per lane, i.e. 2 workgroups of 256 (8 waves) but 11 of 64 (11 waves).
     // (hipOccupancyMaxActiveBlocksPerMultiprocessor is not used: depending on which
     // HIP runtime the process loaded first it assumed 64 KiB of LDS and halved the
     // grid -- measured 512 instead of 1024 workgroups, 1.5x slower.)
-    int per_cu = (int)((160u * 1024u) / P.lds);
-    if (per_cu > 4) per_cu = 4;
-    const int want = g_waves_per_cu / (BLOCK / 64);
-    if (per_cu > want) per_cu = want > 0 ? want : 1;
+    auto layout = [&](uint32_t nt) {
+        P.nt = nt;
+        P.off_heads = 2 * MAXB + 128;   // score tables, then the two regimes
+        P.off_wb = P.off_heads + (uint32_t)nb * nt * 2;
+        P.off_ws = P.off_wb + ((uint32_t)max_len / epw + 1u) * nt * 4u;
+        P.lds = ((size_t)P.off_ws + ((size_t)max_seed / epw + 1u) * nt * 4u + 15) / 16 * 16;
+        int per_cu = (int)((160u * 1024u) / P.lds);
+        const int cap = 16 / (int)(nt / 64);                 // 16 waves per CU
+        const int want = g_waves_per_cu / (int)(nt / 64);
+        if (per_cu > cap) per_cu = cap;
+        if (per_cu > want) per_cu = want > 0 ? want : 1;
+        return per_cu;
+    };
+    static const int force256 = getenv("HSA_WG256") != nullptr;   // A/B runs only
+    int per_cu = layout(256);
+    if (per_cu < 4 && !force256) {
+        const int p64 = layout(64);
+        if (p64 > per_cu * 4) per_cu = p64;
+        else per_cu = layout(256);
+    }
+    if (P.lds > 160 * 1024) { hsa_set_error("reads too long for the LDS budget (%zu bytes)", P.lds); return HSA_E_ARG; }
     if (per_cu < 1) { hsa_set_error("search kernel does not fit (LDS %zu)", P.lds); return HSA_E_ARG; }
+    const uint32_t NTB = P.nt;
     size_t blocks = (size_t)ix->n_cu * per_cu;
-    size_t need_blocks = ((size_t)n_jobs + BLOCK - 1) / BLOCK;
+    size_t need_blocks = ((size_t)n_jobs + NTB - 1) / NTB;
     if (big) {
-        blocks = need_blocks < 16 ? need_blocks : 16;
+        const size_t big_blocks = 16 * (256 / NTB);         // 4096 lanes
+        blocks = need_blocks < big_blocks ? need_blocks : big_blocks;
     } else if (need_blocks < blocks) {
         blocks = need_blocks;
     }
     if (blocks < 1) blocks = 1;
     P.blocks = blocks;
-    P.lanes = blocks * BLOCK;
+    P.lanes = blocks * NTB;
     static int verbose = -1;
     if (verbose < 0) verbose = getenv("HSA_VERBOSE") != nullptr;
     if (verbose) {
         int occ = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_search<1, true, uint8_t>, BLOCK, P.lds);
-        fprintf(stderr, "[hsa] launch: %d CUs x %d workgroups (runtime occupancy query says %d), LDS %zu B, "
-                "%zu workgroups, %d buckets\n", ix->n_cu, per_cu, occ, P.lds, blocks, nb);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_search<1, true, uint8_t, 256>, 256, P.lds);
+        fprintf(stderr, "[hsa] launch: %d CUs x %d workgroups of %u lanes (runtime occupancy query says %d), "
+                "LDS %zu B, %zu workgroups, %d buckets\n", ix->n_cu, per_cu, P.nt, occ, P.lds, blocks, nb);
     }
     // pool slots are not reused within a search: gapped searches push many more
     P.pcap = big ? 65535u : (uint32_t)(g_pool_entries ? g_pool_entries : (gaps ? 16384 : 8192));
@@ -1123,20 +1143,27 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     return 0;
 }
 
+template <typename WT, int NT>
+static void launch_search_nt(const LaunchPlan &P, const SearchArgs &A, hipStream_t st)
+{
+    const dim3 g((unsigned)P.blocks), b(NT);
+    if (P.nb <= 32) {
+        if (P.gaps) hipLaunchKernelGGL((k_search<0, true, WT, NT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<0, false, WT, NT>), g, b, P.lds, st, A);
+    } else if (P.nb <= 64) {
+        if (P.gaps) hipLaunchKernelGGL((k_search<1, true, WT, NT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<1, false, WT, NT>), g, b, P.lds, st, A);
+    } else {
+        if (P.gaps) hipLaunchKernelGGL((k_search<2, true, WT, NT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<2, false, WT, NT>), g, b, P.lds, st, A);
+    }
+}
+
 template <typename WT>
 static void launch_search(const LaunchPlan &P, const SearchArgs &A, hipStream_t st)
 {
-    const dim3 g((unsigned)P.blocks), b(BLOCK);
-    if (P.nb <= 32) {
-        if (P.gaps) hipLaunchKernelGGL((k_search<0, true, WT>), g, b, P.lds, st, A);
-        else hipLaunchKernelGGL((k_search<0, false, WT>), g, b, P.lds, st, A);
-    } else if (P.nb <= 64) {
-        if (P.gaps) hipLaunchKernelGGL((k_search<1, true, WT>), g, b, P.lds, st, A);
-        else hipLaunchKernelGGL((k_search<1, false, WT>), g, b, P.lds, st, A);
-    } else {
-        if (P.gaps) hipLaunchKernelGGL((k_search<2, true, WT>), g, b, P.lds, st, A);
-        else hipLaunchKernelGGL((k_search<2, false, WT>), g, b, P.lds, st, A);
-    }
+    if (P.nt == 64) launch_search_nt<WT, 64>(P, A, st);
+    else launch_search_nt<WT, 256>(P, A, st);
 }
 
 // One search pass over jobs (or a job_list subset) with device pointers: k_widths
