@@ -84,15 +84,17 @@ def host_oracle_index(res, T):
     return OracleIndex(metas[0], metas[1])
 
 
-TRAFFIC_SRC = "profiles/r01_pmc_summary.json"
+# per-config PMC summaries (tools/profile_run.sh + tools/pmc_summary.py); config 4's
+# step mixes six kernels and has none yet
+TRAFFIC_SRCS = {2: "profiles/r01_pmc_summary.json", 3: "profiles/r01_pmc_summary_config3.json"}
 
 
-def traffic_per_launch():
+def traffic_per_launch(config):
     """HBM read+write bytes per step (k_widths + k_search) from the committed PMC pass
     (FETCH_SIZE calibrated on random 64-B gathers + WRITE_SIZE; tools/profile_run.sh,
     tools/pmc_summary.py) -- counters cannot be read in the timed run itself."""
     try:
-        with open(os.path.join(ROOT, TRAFFIC_SRC)) as f:
+        with open(os.path.join(ROOT, TRAFFIC_SRCS[config])) as f:
             d = json.load(f)
         return round(d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"])
     except (OSError, KeyError, ValueError):
@@ -364,7 +366,7 @@ def main():
                        "genome_bp": T, "reads_per_step": a.batch, "read_len": RL, "options": opt_str,
                        "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_per_launch() if a.config == 2 else None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_per_launch(a.config),
                          "kernel": "k_widths+k_search (one step)" if a.config != 4 else
                                    "main path (k_widths+k_search) + splice seeds (k_seed_prep+k_widths_import+k_search+"
                                    "k_widths_export)", "kernel_ms_mean": round(mean_kms, 3),
@@ -378,7 +380,7 @@ def main():
                          "peak_random_sector_measured": round(rand_gbs, 1),
                          "peak_random_sector_measured_64B_loads": round(rand64_gbs, 1),
                          "frac_of_random_sector": round(achieved / rand_gbs, 4),
-                         "traffic_source": TRAFFIC_SRC},
+                         "traffic_source": TRAFFIC_SRCS.get(a.config)},
             "mapped_frac": round(mapped_all / reads_all, 4), "fallback_frac": round(fallback_all / reads_all, 4),
             "pops_per_read": round(pops / reads_local, 1),
         }

@@ -23,10 +23,21 @@ def counters(d, kernel):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
     for r in rows:
-        if not r["Kernel_Name"].startswith(kernel) and (" " + kernel) not in r["Kernel_Name"]:
+        name = r["Kernel_Name"]
+        if name.startswith("void "):
+            name = name[5:]
+        # the kernel's own name only: k_widths must not match k_widths_import / _export
+        if not (name.startswith(kernel) and (kernel.endswith(">") or name[len(kernel):len(kernel) + 1] in ("<", "("))):
             continue
         agg[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
         dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    # one step = one full-batch launch; the overflow re-run launches of the same kernel
+    # (an empty or near-empty list, tens of microseconds) are not the step's launch
+    if dur:
+        top = max(dur.values())
+        keep = [d for d, ms in dur.items() if ms >= 0.5 * top]
+        agg = {d: agg[d] for d in keep}
+        dur = {d: dur[d] for d in keep}
     return agg, dur
 
 
