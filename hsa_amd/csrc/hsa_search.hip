@@ -1121,7 +1121,8 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     size_t blocks = (size_t)ix->n_cu * per_cu;
     size_t need_blocks = ((size_t)n_jobs + NTB - 1) / NTB;
     if (big) {
-        const size_t big_blocks = 16 * (256 / NTB);         // 4096 lanes
+        static const size_t big_lanes = getenv("HSA_BIG_LANES") ? strtoull(getenv("HSA_BIG_LANES"), nullptr, 10) : 4096;
+        const size_t big_blocks = big_lanes / NTB > 0 ? big_lanes / NTB : 1;
         blocks = need_blocks < big_blocks ? need_blocks : big_blocks;
     } else if (need_blocks < blocks) {
         blocks = need_blocks;

@@ -8,7 +8,11 @@ widths other than 16 B/lane streaming are uncalibrated): membench's k_indep
 issues a known number of random 64-byte block loads per dispatch; the ratio
 FETCH_SIZE*1024 / known bytes on that pattern is applied to k_search.
 
-usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>_pmc_summary.json
+usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>_pmc_summary.json [LAUNCHES]
+
+With LAUNCHES (warmup + timed steps of the profiled bench run), a step's traffic is
+the sum over EVERY dispatch of the step's kernels divided by LAUNCHES: config 4's
+step launches k_search twice (main path, splice seeds) plus the overflow re-runs.
 """
 import collections
 import csv
@@ -18,7 +22,10 @@ import statistics
 import sys
 
 
-def counters(d, kernel):
+STEP_KERNELS = ("k_widths", "k_search", "k_seed_prep", "k_widths_import", "k_widths_export")
+
+
+def counters(d, kernel, every=False):
     rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
@@ -33,7 +40,7 @@ def counters(d, kernel):
         dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     # one step = one full-batch launch; the overflow re-run launches of the same kernel
     # (an empty or near-empty list, tens of microseconds) are not the step's launch
-    if dur:
+    if dur and not every:
         top = max(dur.values())
         keep = [d for d, ms in dur.items() if ms >= 0.5 * top]
         agg = {d: agg[d] for d in keep}
@@ -53,9 +60,22 @@ def main():
     known = 256 * 16 // 4 * 256 * 2000 * 64
     cal = med(mb, "FETCH_SIZE") * 1024 / known
     out["fetch_calibration_random64"] = round(cal, 4)
-    # one step = k_widths + k_search launches: per-kernel medians, summed
-    out["per_kernel"] = {}
-    for k in ("k_widths", "k_search"):
+    launches = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    if launches:
+        out["per_kernel"] = {}
+        for k in STEP_KERNELS:
+            f, dur = counters(os.path.join(src, "pmc_fetch"), k, every=True)
+            w, _ = counters(os.path.join(src, "pmc_write"), k, every=True)
+            if not f:
+                continue
+            out["per_kernel"][k] = {"fetch_bytes": sum(v["FETCH_SIZE"] for v in f.values()) * 1024 / cal / launches,
+                                    "write_bytes": sum(v["WRITE_SIZE"] for v in w.values()) * 1024 / launches,
+                                    "dispatches_per_step": len(f) / launches,
+                                    "ms_per_step_pmc_pass": sum(dur.values()) / launches}
+    else:
+        # one step = k_widths + k_search launches: per-kernel medians, summed
+        out["per_kernel"] = {}
+    for k in (() if launches else ("k_widths", "k_search")):
         f, dur = counters(os.path.join(src, "pmc_fetch"), k)
         w, _ = counters(os.path.join(src, "pmc_write"), k)
         if not f:

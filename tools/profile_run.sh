@@ -15,7 +15,7 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $BENCH > $OUT/trace.json 2> $OUT/trace.err || exit 11
 pmc() {  # name, counters...
   local n=$1; shift
-  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc "$@" --kernel-include-regex "k_search|k_widths" --output-format csv -d $OUT/pmc_$n -o run -- python3 $BENCH > $OUT/pmc_$n.json 2> $OUT/pmc_$n.err || exit 12
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc "$@" --kernel-include-regex "${PMC_REGEX:-k_search|k_widths}" --output-format csv -d $OUT/pmc_$n -o run -- python3 $BENCH > $OUT/pmc_$n.json 2> $OUT/pmc_$n.err || exit 12
 }
 pmc fetch FETCH_SIZE
 pmc write WRITE_SIZE
