@@ -84,9 +84,10 @@ def host_oracle_index(res, T):
     return OracleIndex(metas[0], metas[1])
 
 
-# per-config PMC summaries (tools/profile_run.sh + tools/pmc_summary.py); config 4's
-# step mixes six kernels and has none yet
-TRAFFIC_SRCS = {2: "profiles/r01_pmc_summary.json", 3: "profiles/r01_pmc_summary_config3.json"}
+# per-config PMC summaries (tools/profile_run.sh + tools/pmc_summary.py; config 4's in
+# its "step" mode, which sums the main path's and the splice seeds' kernels)
+TRAFFIC_SRCS = {2: "profiles/r01_pmc_summary.json", 3: "profiles/r01_pmc_summary_config3.json",
+                4: "profiles/r01_pmc_summary_config4.json"}
 
 
 def traffic_per_launch(config):

@@ -8,11 +8,11 @@ widths other than 16 B/lane streaming are uncalibrated): membench's k_indep
 issues a known number of random 64-byte block loads per dispatch; the ratio
 FETCH_SIZE*1024 / known bytes on that pattern is applied to k_search.
 
-usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>_pmc_summary.json [LAUNCHES]
+usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>_pmc_summary.json [step]
 
-With LAUNCHES (warmup + timed steps of the profiled bench run), a step's traffic is
-the sum over EVERY dispatch of the step's kernels divided by LAUNCHES: config 4's
-step launches k_search twice (main path, splice seeds) plus the overflow re-runs.
+With "step", a step's traffic sums every kernel instantiation of the step, each as
+all its dispatches (overflow re-runs included) over its full-size launches: config
+4's step launches k_search twice (main path, splice seeds) plus the re-runs.
 """
 import collections
 import csv
@@ -29,6 +29,7 @@ def counters(d, kernel, every=False):
     rows = list(csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))))
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
+    names = {}
     for r in rows:
         name = r["Kernel_Name"]
         if name.startswith("void "):
@@ -37,10 +38,13 @@ def counters(d, kernel, every=False):
         if not (name.startswith(kernel) and (kernel.endswith(">") or name[len(kernel):len(kernel) + 1] in ("<", "("))):
             continue
         agg[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+        names[r["Dispatch_Id"]] = r["Kernel_Name"]
         dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     # one step = one full-batch launch; the overflow re-run launches of the same kernel
     # (an empty or near-empty list, tens of microseconds) are not the step's launch
-    if dur and not every:
+    if every:
+        return agg, dur, names
+    if dur:
         top = max(dur.values())
         keep = [d for d, ms in dur.items() if ms >= 0.5 * top]
         agg = {d: agg[d] for d in keep}
@@ -60,18 +64,25 @@ def main():
     known = 256 * 16 // 4 * 256 * 2000 * 64
     cal = med(mb, "FETCH_SIZE") * 1024 / known
     out["fetch_calibration_random64"] = round(cal, 4)
-    launches = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    launches = len(sys.argv) > 3 and sys.argv[3] == "step"
     if launches:
         out["per_kernel"] = {}
         for k in STEP_KERNELS:
-            f, dur = counters(os.path.join(src, "pmc_fetch"), k, every=True)
-            w, _ = counters(os.path.join(src, "pmc_write"), k, every=True)
+            f, dur, names = counters(os.path.join(src, "pmc_fetch"), k, every=True)
+            w, _, _ = counters(os.path.join(src, "pmc_write"), k, every=True)
             if not f:
                 continue
-            out["per_kernel"][k] = {"fetch_bytes": sum(v["FETCH_SIZE"] for v in f.values()) * 1024 / cal / launches,
-                                    "write_bytes": sum(v["WRITE_SIZE"] for v in w.values()) * 1024 / launches,
-                                    "dispatches_per_step": len(f) / launches,
-                                    "ms_per_step_pmc_pass": sum(dur.values()) / launches}
+            # per instantiation: all its dispatches (incl. overflow re-runs) over its
+            # full-size launches (>= half its longest dispatch)
+            fb = wb = ms = 0.0
+            for nm in set(names.values()):
+                ds = [d for d in names if names[d] == nm]
+                top = max(dur[d] for d in ds)
+                nl = sum(1 for d in ds if dur[d] >= 0.5 * top)
+                fb += sum(f[d]["FETCH_SIZE"] for d in ds) * 1024 / cal / nl
+                wb += sum(w[d]["WRITE_SIZE"] for d in ds if d in w) * 1024 / nl
+                ms += sum(dur[d] for d in ds) / nl
+            out["per_kernel"][k] = {"fetch_bytes": fb, "write_bytes": wb, "ms_per_step_pmc_pass": ms}
     else:
         # one step = k_widths + k_search launches: per-kernel medians, summed
         out["per_kernel"] = {}
