@@ -18,7 +18,7 @@
 
 static thread_local char g_err[1024] = "";
 int g_waves_per_cu = 16;
-int g_pool_entries = 0;      // 0: 8192 per lane, 16384 when gap opens are allowed
+int g_pool_entries = 0;      // 0: 8192 per lane, 32768 when gap opens are allowed
 int g_hit_cap = 64;
 
 void hsa_set_error(const char *fmt, ...)
@@ -76,19 +76,19 @@ void hsa_scratch_free(SearchScratch &s)
 
 int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap)
 {
-    if (lanes <= s.lanes && pcap <= s.pcap && hcap <= s.hcap && s.pool) return 0;
-    lanes = lanes > s.lanes ? lanes : s.lanes;
-    pcap = pcap > s.pcap ? pcap : s.pcap;
-    hcap = hcap > s.hcap ? hcap : s.hcap;
+    size_t pe = lanes * pcap, he = lanes * hcap;
+    if (pe <= s.pool_entries && he <= s.hit_entries && s.pool) return 0;
+    pe = pe > s.pool_entries ? pe : s.pool_entries;
+    he = he > s.hit_entries ? he : s.hit_entries;
     hsa_scratch_free(s);
-    if (hipMalloc(&s.pool, lanes * pcap * sizeof(uint4)) != hipSuccess ||
-        hipMalloc(&s.nxt, lanes * pcap * sizeof(uint16_t)) != hipSuccess ||
-        hipMalloc(&s.hbuf, lanes * hcap * 9 * sizeof(uint32_t)) != hipSuccess) {
+    if (hipMalloc(&s.pool, pe * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(&s.nxt, pe * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&s.hbuf, he * 9 * sizeof(uint32_t)) != hipSuccess) {
         hsa_set_error("scratch allocation failed (lanes %zu, pool %zu, hits %zu)", lanes, pcap, hcap);
         hsa_scratch_free(s);
         return HSA_E_MEM;
     }
-    s.lanes = lanes; s.pcap = pcap; s.hcap = hcap;
+    s.pool_entries = pe; s.hit_entries = he;
     return 0;
 }
 

@@ -18,11 +18,14 @@ void hsa_set_error(const char *fmt, ...);
     } while (0)
 
 // Per-launch scratch of the search kernel: grows, never shrinks.
+// Sized in entries (lanes x per-lane capacity): a launch indexes lane-interleaved
+// slots up to its own lanes * pcap, so a wide seed pass and a deep gapped pass share
+// one allocation instead of the product of their maxima.
 struct SearchScratch {
-    size_t lanes = 0, pcap = 0, hcap = 0;
-    uint4 *pool = nullptr;       // lanes * pcap
-    uint16_t *nxt = nullptr;     // lanes * pcap
-    uint32_t *hbuf = nullptr;    // lanes * hcap * 9
+    size_t pool_entries = 0, hit_entries = 0;
+    uint4 *pool = nullptr;       // pool_entries
+    uint16_t *nxt = nullptr;     // pool_entries
+    uint32_t *hbuf = nullptr;    // hit_entries * 9
 };
 
 struct hsa_index {
