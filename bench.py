@@ -90,16 +90,16 @@ TRAFFIC_SRCS = {2: "profiles/r01_pmc_summary.json", 3: "profiles/r01_pmc_summary
                 4: "profiles/r01_pmc_summary_config4.json"}
 
 
-def traffic_per_launch(config):
-    """HBM read+write bytes per step (k_widths + k_search) from the committed PMC pass
+def traffic_per_kernel(config):
+    """HBM read+write bytes per launch of each kernel from the committed PMC pass
     (FETCH_SIZE calibrated on random 64-B gathers + WRITE_SIZE; tools/profile_run.sh,
     tools/pmc_summary.py) -- counters cannot be read in the timed run itself."""
     try:
         with open(os.path.join(ROOT, TRAFFIC_SRCS[config])) as f:
             d = json.load(f)
-        return round(d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"])
-    except (OSError, KeyError, ValueError):
-        return None
+        return {k: round(v["fetch_bytes"] + v["write_bytes"]) for k, v in d["per_kernel"].items()}
+    except (OSError, KeyError, ValueError, TypeError):
+        return {}
 
 
 def diag_dump(path):
@@ -119,11 +119,12 @@ def diag_dump(path):
            "start_spread_ms": float((d[:, 1].max() - t0) / 100e3),
            "dur_ms_pct": [float(np.percentile(dur_ms, q)) for q in (0, 10, 50, 90, 99, 100)],
            "end_ms_pct": [float(np.percentile((d[:, 3] - t0) / 100e3, q)) for q in (0, 10, 50, 90, 99, 100)]}
-    ev = (C.c_ulonglong * 16)()
+    ev = (C.c_ulonglong * 32)()
     _lib.check(L.hsa_diag_counters(ev, 0))
     names = ["width_steps", "exact_steps", "expand_steps", "vt_pops", "pool_pops", "outer_iters_per_wave",
              "lanes_stepping", "control_iters_per_wave", "pool_flushes", "cyc_acquire", "cyc_control",
-             "cyc_rank_wait", "cyc_apply", "gap_shadows", "gap_shadow_ldp_sum", "strand_starts"]
+             "cyc_rank_wait", "cyc_apply", "gap_shadows", "gap_shadow_ldp_sum", "strand_starts",
+             "exact_steps_unique", "expand_steps_unique", "width_steps_unique", "width_steps_all"]
     out["events_total"] = {n: int(ev[i]) for i, n in enumerate(names)}
     log(f"[bench] diag: {json.dumps(out)}")
     with open(path, "w") as f:
@@ -139,6 +140,68 @@ def cpu_widths(ox, wl, wc):
     return np.concatenate(out).astype(np.uint32)
 
 
+
+def cpu_info():
+    """The host CPU the baseline ran on: model, physical cores visible, and the
+    threads used (the CPUs this process may run on, at most 16: the GPU box's share)."""
+    model, phys = "unknown", set()
+    try:
+        pid = cid = None
+        for ln in open("/proc/cpuinfo"):
+            k, _, v = ln.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name":
+                model = v
+            elif k == "physical id":
+                pid = v
+            elif k == "core id":
+                cid = v
+                phys.add((pid, cid))
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0))
+    return {"model": model, "physical_cores": len(phys) or None, "affinity": aff,
+            "threads": max(1, min(aff, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))}
+
+
+def oracle_threaded(ox, reads, RL, od, threads):
+    """bwa_cal_sa_reg_gap on the C restatement over disjoint chunks, one thread each
+    (ctypes releases the GIL; a steady-state batch: chunking does not change results).
+    Returns n_aln, flags, hits in read order, and the rank queries."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle_ctypes import Opt
+    n = len(reads)
+    edges = np.linspace(0, n, threads + 1).astype(np.int64)
+
+    def one(i):
+        ch = reads[edges[i]:edges[i + 1]]
+        return ox.cal_sa_reg_gap(np.full(len(ch), RL, np.uint32), np.ascontiguousarray(ch).reshape(-1),
+                                 Opt.from_dict(od))
+    with ThreadPoolExecutor(threads) as ex:
+        outs = list(ex.map(one, range(threads)))
+    return (np.concatenate([o[0] for o in outs]), np.concatenate([o[1] for o in outs]),
+            np.concatenate([o[2] for o in outs]), sum(int(o[3][0]) for o in outs))
+
+
+def compare_batch(g_n, g_f, g_o, g_h, o_n, o_f, o_h):
+    """Reads whose n_aln, fallback flag or hit records (every field, in order) differ."""
+    g_n = np.maximum(g_n.astype(np.int64), 0)
+    bad = (g_n != o_n) | ((g_f & 1) != (o_f & 1))
+    same = np.flatnonzero(~bad & (g_n > 0))
+    # GPU hits of those reads, gathered into read order
+    cnt = g_n[same]
+    idx = np.repeat(g_o[same].astype(np.int64) - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt) + \
+        np.arange(int(cnt.sum()))
+    o_off = np.concatenate([[0], np.cumsum(o_n.astype(np.int64))])
+    oidx = np.repeat(o_off[same] - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt) + np.arange(int(cnt.sum()))
+    diff = (g_h[idx] != o_h[oidx]).any(axis=1)
+    if diff.any():
+        owner = np.repeat(same, cnt)
+        bad[np.unique(owner[diff])] = True
+    nb = int(bad.sum())
+    return nb, (int(np.flatnonzero(bad)[0]) if nb else None)
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,7 +210,8 @@ def main():
     ap.add_argument("--genome", type=int, default=GENOME_T)
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--cpu-sample", type=int, default=20000, help="reads timed on the CPU restatement")
-    ap.add_argument("--parity-sample", type=int, default=4000, help="reads checked against the CPU restatement")
+    ap.add_argument("--parity-sample", type=int, default=-1,
+                    help="reads of the timed batch checked against the CPU restatement (-1: all of them; 0: none)")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
                     help="BASELINE.json config: 2 = 0-4 substitutions, -n 4 -o 0 (default, the metric's config); "
                          "3 = one 1-3 bp indel + 0-2 substitutions, -n 4 -o 1; "
@@ -214,7 +278,7 @@ def main():
     jobs["max_diff"] = opt.max_diff
     jobs["seed_len"] = opt.seed_len
     d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).cuda()
-    d_codes = [torch.from_numpy(b.reshape(-1)).cuda() for b in batches]
+    d_codes = [torch.from_numpy(_lib.pad_codes(b.reshape(-1))).cuda() for b in batches]
     hit_cap = a.batch * 8
     outs = []
     for j in range(nd):
@@ -252,8 +316,9 @@ def main():
     # table as large as the rank index (before the timed region, same process)
     rand_gbs = _lib.probe_gather(gi.nbytes(), 1, device)
     rand64_gbs = _lib.probe_gather(gi.nbytes(), 4, device)
+    coop_gbs = _lib.probe_gather(gi.nbytes(), 2, device)
     log(f"[bench] rank {rank}: random-sector gather probe over {gi.nbytes() / 2**30:.2f} GiB: {rand_gbs:.0f} GB/s "
-        f"(16-B loads), {rand64_gbs:.0f} GB/s (whole 64-B sectors)")
+        f"(16-B loads), {coop_gbs:.0f} GB/s (4 lanes x 16 B per sector), {rand64_gbs:.0f} GB/s (whole sectors per lane)")
 
     lib_stream = torch.cuda.ExternalStream(gi.stream_handle())
     for j in range(a.warmup):
@@ -264,7 +329,7 @@ def main():
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     if os.environ.get("HSA_DIAG_OUT"):
-        _lib.check(_lib.lib().hsa_diag_counters((C.c_ulonglong * 16)(), 1))
+        _lib.check(_lib.lib().hsa_diag_counters((C.c_ulonglong * 32)(), 1))
     t0 = time.perf_counter()
     for s in range(a.steps):
         ev[s][0].record(lib_stream)
@@ -275,26 +340,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kms = [e0.elapsed_time(e1) for e0, e1 in ev]
-    # per-kernel split of one more (untimed) step: k_widths, then k_search
-    if a.config == 4:   # main path, then the splice seeds
-        e3 = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        e3[0].record(lib_stream)
-        gi.search_device([rg], DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[0].data_ptr(),
-                                           d_n_aln=outs[0]["n"].data_ptr(), d_flags=outs[0]["f"].data_ptr(),
-                                           d_hit_off=outs[0]["o"].data_ptr(), d_hits=outs[0]["h"].data_ptr(),
-                                           hit_cap=hit_cap, d_counters=outs[0]["c"].data_ptr(), max_len=RL,
-                                           max_seed=opt.seed_len))
-        e3[1].record(lib_stream)
-        launch(0)
-        e3[2].record(lib_stream)
-        torch.cuda.synchronize()
-        split_ms = (e3[0].elapsed_time(e3[1]), e3[1].elapsed_time(e3[2]) - e3[0].elapsed_time(e3[1]))
-        log(f"[bench] rank {rank}: split of one step: main path {split_ms[0]:.2f} ms, splice seeds {split_ms[1]:.2f} ms")
-    else:
-        launch(a.warmup + a.steps)
-        split_ms = gi.last_pass_ms()
-        torch.cuda.synchronize()
-        log(f"[bench] rank {rank}: kernel split of one step: k_widths {split_ms[0]:.2f} ms, k_search {split_ms[1]:.2f} ms")
+    # per-kernel device time of every timed step: HIP events the library records on
+    # its stream around k_widths and k_search (+ its overflow re-run) of each pass
+    w_ms, s_ms = gi.pass_times(a.steps)
+    w_ms, s_ms = w_ms.astype(float), s_ms.astype(float)
+    seeds_ms = np.array(kms) - w_ms - s_ms if a.config == 4 else None
+    log(f"[bench] rank {rank}: per-step kernels: k_widths {np.mean(w_ms):.2f} ms, k_search {np.mean(s_ms):.2f} ms"
+        + (f", splice seeds {np.mean(seeds_ms):.2f} ms" if a.config == 4 else ""))
     if os.environ.get("HSA_DIAG_OUT"):
         diag_dump(os.environ["HSA_DIAG_OUT"])
     log(f"[bench] rank {rank}: per-step device ms {[round(x, 2) for x in kms]}, wall {elapsed * 1e3:.1f} ms")
@@ -307,7 +359,13 @@ def main():
     used = sorted({(a.warmup + s) % nd for s in range(a.steps)})
     per = {j: sum(1 for s in range(a.steps) if (a.warmup + s) % nd == j) for j in used}
     ctr = np.stack([outs[j]["c"].cpu().numpy() * per[j] for j in used])
-    queries = int(ctr[:, 2].sum())
+    queries = int(ctr[:, 2].sum())             # what the reference algorithm issues (include/hsa_gpu.h)
+    q_widths = int(ctr[:, 7].sum())            # ... of it in k_widths (strands the reference searches)
+    q_search = queries - q_widths              # ... of it in k_search
+    q_widths_issued = q_widths - int(ctr[:, 14].sum()) + int(ctr[:, 13].sum())   # + speculative fwd rows
+    unfinished = int(ctr[:, 11].sum())
+    if unfinished:
+        log(f"[bench] WARNING: {unfinished} reads unfinished (hit buffer too small)")
     seed_queries = 0
     if a.config == 4:   # the seed searches' rank queries and their prefix widths'
         sctr = np.stack([outs[j]["sc"].cpu().numpy() * per[j] for j in used])
@@ -352,7 +410,14 @@ def main():
         value = reads_all / elapsed
         mean_kms = float(np.mean(kms))
         q_per_launch = queries / a.steps
-        achieved = q_per_launch * BYTES_PER_QUERY / (mean_kms / 1e3) / 1e9
+        ms_search, ms_widths = float(np.mean(s_ms)), float(np.mean(w_ms))
+        # the dominant kernel: k_search, its algorithmic bytes per launch (the
+        # reference's rank queries it answers x one 64-byte sector) over its mean
+        # launch time from the per-pass HIP events
+        ach_search = q_search / a.steps * BYTES_PER_QUERY / (ms_search / 1e3) / 1e9
+        ach_widths = q_widths / a.steps * BYTES_PER_QUERY / (ms_widths / 1e3) / 1e9
+        ach_step = q_per_launch * BYTES_PER_QUERY / (mean_kms / 1e3) / 1e9
+        pk = traffic_per_kernel(a.config)
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True,
@@ -366,29 +431,41 @@ def main():
                                    f"(BASELINE configs[{a.config - 1}]); {a.steps} timed steps",
                        "genome_bp": T, "reads_per_step": a.batch, "read_len": RL, "options": opt_str,
                        "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_per_launch(a.config),
-                         "kernel": "k_widths+k_search (one step)" if a.config != 4 else
-                                   "main path (k_widths+k_search) + splice seeds (k_seed_prep+k_widths_import+k_search+"
-                                   "k_widths_export)", "kernel_ms_mean": round(mean_kms, 3),
-                         "kernel_split_ms": {"k_widths": round(split_ms[0], 3), "k_search": round(split_ms[1], 3)}
-                         if a.config != 4 else {"main_path": round(split_ms[0], 3),
-                                                "splice_seeds": round(split_ms[1], 3)},
-                         "algorithmic_bytes_per_launch": q_per_launch * BYTES_PER_QUERY,
+            "roofline": {"bound": "hbm", "kernel": "k_search", "achieved": round(ach_search, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(ach_search / HBM_PEAK_GBS, 4),
+                         "traffic": pk.get("k_search"),
+                         "k_search_ms": round(ms_search, 3),
+                         "k_search_algorithmic_bytes_per_launch": q_search / a.steps * BYTES_PER_QUERY,
+                         "k_search_frac_of_random_sector": round(ach_search / rand_gbs, 4),
+                         "k_search_frac_of_random_sector_coop": round(ach_search / coop_gbs, 4),
+                         "k_widths": {"ms": round(ms_widths, 3), "achieved": round(ach_widths, 1),
+                                      "frac": round(ach_widths / HBM_PEAK_GBS, 4),
+                                      "frac_of_random_sector": round(ach_widths / rand_gbs, 4),
+                                      "rank_queries_per_read": round(q_widths / reads_local, 1),
+                                      "issued_queries_per_read": round(q_widths_issued / reads_local, 1),
+                                      "traffic": pk.get("k_widths")},
+                         "step": {"ms": round(mean_kms, 3), "achieved": round(ach_step, 1),
+                                  "frac": round(ach_step / HBM_PEAK_GBS, 4),
+                                  "frac_of_random_sector": round(ach_step / rand_gbs, 4)},
                          "rank_queries_per_read": round(queries / reads_local, 1),
+                         "k_search_rank_queries_per_read": round(q_search / reads_local, 1),
                          "sectors_per_query": round(blocks / max(queries, 1), 4),
                          "bytes_per_query": BYTES_PER_QUERY,
                          "peak_random_sector_measured": round(rand_gbs, 1),
+                         "peak_random_sector_measured_coop4x16": round(coop_gbs, 1),
                          "peak_random_sector_measured_64B_loads": round(rand64_gbs, 1),
-                         "frac_of_random_sector": round(achieved / rand_gbs, 4),
                          "traffic_source": TRAFFIC_SRCS.get(a.config)},
             "mapped_frac": round(mapped_all / reads_all, 4), "fallback_frac": round(fallback_all / reads_all, 4),
             "pops_per_read": round(pops / reads_local, 1),
         }
         if a.config == 4:
             result["seed_rank_queries_per_read"] = round(seed_queries / reads_local, 1)
+            result["roofline"]["splice_seeds_ms"] = round(float(np.mean(seeds_ms)), 3)
 
-    # parity on a sample and the CPU baseline (rank 0 at N=1 only)
+    # parity and the CPU baseline (rank 0 at N=1 only): configs 2 and 3 compare the
+    # WHOLE timed batch with the C restatement run on the host's cores (that run is
+    # the CPU baseline); config 4 checks a sample (its seed calls are driven from
+    # Python one by one)
     if rank == 0 and world == 1 and (a.parity_sample or a.cpu_sample):
         t0 = time.time()
         ox = host_oracle_index(res, T)
@@ -396,15 +473,44 @@ def main():
         from oracle_ctypes import Opt, default_opt
         od = default_opt()
         od.update(max_diff=4, fnr=-1.0, max_gapo=max_gapo, mode=od["mode"] & ~0x01)
-        if a.parity_sample:
-            n = min(a.parity_sample, a.batch)
+        cpu = cpu_info()
+        j0 = a.warmup % nd
+        last = outs[j0]
+        g_n = last["n"].cpu().numpy()
+        g_f = last["f"].cpu().numpy().astype(np.uint32)
+        g_o = last["o"].cpu().numpy()
+        g_h = last["h"].cpu().numpy().view(np.uint32).reshape(-1, 9)
+        if a.config != 4 and a.parity_sample:
+            n = a.batch if a.parity_sample < 0 else min(a.parity_sample, a.batch)
+            threads = cpu["threads"]
+            t0 = time.perf_counter()
+            o_n, o_f, o_h, o_q = oracle_threaded(ox, batches[j0][:n], RL, od, threads)
+            dt = time.perf_counter() - t0
+            bad, first = compare_batch(g_n[:n], g_f[:n], g_o[:n], g_h, o_n, o_f, o_h)
+            gq = int(outs[j0]["c"][2].item())
+            result["parity_full" if n == a.batch else "parity_sample"] = {
+                "reads": n, "mismatching_reads": bad, "first_mismatch": first, "against": "oracle (C restatement)",
+                "fields": "n_aln, splice-fallback flag, every bwt_aln1_t field of every hit, hit order",
+                "rank_queries_gpu": gq if n == a.batch else None, "rank_queries_oracle": int(o_q)}
+            log(f"[bench] parity: {n} reads, {bad} differ from the CPU restatement; rank queries GPU "
+                f"{gq} vs oracle {int(o_q)} ({threads} threads, {dt:.1f} s)")
+            if a.cpu_sample:
+                n1 = min(a.cpu_sample, a.batch)
+                rs = batches[(a.warmup + 1) % nd][-n1:]
+                t1 = time.perf_counter()
+                ox.cal_sa_reg_gap(np.full(n1, RL, np.uint32), rs.reshape(-1), Opt.from_dict(od))
+                dt1 = time.perf_counter() - t1
+                result["cpu_baseline"] = {
+                    "value": round(n / dt, 1), "unit": "reads/s", "cores": threads, "kind": "port",
+                    "value_1core": round(n1 / dt1, 1), "cpu_model": cpu["model"],
+                    "physical_cores_visible": cpu["physical_cores"], "affinity_cpus": cpu["affinity"],
+                    "sample": f"the whole timed batch ({n} reads) on the bwa_cal_sa_reg_gap restatement, "
+                              f"{threads} threads on disjoint chunks, {dt:.1f} s (the parity run above); "
+                              f"1 thread: {n1} reads in {dt1:.1f} s"}
+        if a.config == 4 and a.parity_sample:
+            n = 4000 if a.parity_sample < 0 else min(a.parity_sample, a.batch)
             r0 = batches[a.warmup % nd][:n]
             o_n, o_f, o_h, _ = ox.cal_sa_reg_gap(np.full(n, RL, np.uint32), r0.reshape(-1), Opt.from_dict(od))
-            last = outs[a.warmup % nd]
-            g_n = last["n"].cpu().numpy()[:n]
-            g_f = last["f"].cpu().numpy()[:n].astype(np.uint32)
-            g_o = last["o"].cpu().numpy()[:n]
-            g_h = last["h"].cpu().numpy().view(np.uint32).reshape(-1, 9)
             oo = np.concatenate([[0], np.cumsum(o_n)])
             bad = 0
             for i in range(n):
@@ -446,32 +552,6 @@ def main():
                                       "sample": f"{n} reads of the same workload: bwa_cal_sa_reg_gap restatement + "
                                                 f"the 6 seed searches of its {int((fl & 1).sum())} fallback reads, "
                                                 f"1 thread, in {dt1:.1f} s"}
-        elif a.cpu_sample:
-            # 1 thread, then one thread per host core on disjoint chunks (independent
-            # batches, as BASELINE.md §3 plans; ctypes releases the GIL in the C call)
-            from concurrent.futures import ThreadPoolExecutor
-            n = min(a.cpu_sample, a.batch)
-            rs = batches[(a.warmup + 1) % nd][-n:]
-            t0 = time.perf_counter()
-            ox.cal_sa_reg_gap(np.full(n, RL, np.uint32), rs.reshape(-1), Opt.from_dict(od))
-            dt1 = time.perf_counter() - t0
-            cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), len(os.sched_getaffinity(0))))
-            per = max(1, min(n, a.batch // cores))
-            src = batches[(a.warmup + 1) % nd]
-            chunks = [src[i * per:(i + 1) * per] for i in range(cores)]
-
-            def one(ch):
-                ox.cal_sa_reg_gap(np.full(len(ch), RL, np.uint32), ch.reshape(-1), Opt.from_dict(od))
-
-            t0 = time.perf_counter()
-            with ThreadPoolExecutor(cores) as ex:
-                list(ex.map(one, chunks))
-            dtn = time.perf_counter() - t0
-            result["cpu_baseline"] = {"value": round(cores * per / dtn, 1), "unit": "reads/s", "cores": cores,
-                                      "kind": "port", "value_1core": round(n / dt1, 1),
-                                      "sample": f"{cores} threads x {per} reads of the same workload "
-                                                f"(bwa_cal_sa_reg_gap restatement, main path, disjoint chunks) in "
-                                                f"{dtn:.1f} s; 1 thread: {n} reads in {dt1:.1f} s"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -26,12 +26,22 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
     "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather", "hsa_last_pass_ms",
     "hsa_index_set_sa", "hsa_sa_position_batch", "hsa_sa_position_device", "hsa_match_gap_batch",
-    "bwt_match_gap", "bwt_match_gap_batch", "hsa_splice_seeds_device",
+    "bwt_match_gap", "bwt_match_gap_batch", "hsa_splice_seeds_device", "hsa_pass_times",
 ]
 
 
 class HsaError(RuntimeError):
     pass
+
+
+CODES_PAD = 16   # hsa_search_device reads a read's codes in aligned 16-byte loads
+
+
+def pad_codes(codes) -> np.ndarray:
+    """Read codes followed by the padding the device path may read past the last
+    read (include/hsa_gpu.h, hsa_device_batch_t.d_codes)."""
+    c = np.ascontiguousarray(codes, np.uint8).reshape(-1)
+    return np.concatenate([c, np.zeros(4 * CODES_PAD, np.uint8)])
 
 
 class GapOpt(C.Structure):
@@ -168,6 +178,8 @@ def lib():
     L.hsa_match_gap_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, vp, C.c_int, u8, C.c_size_t, i32, C.c_size_t,
                                       i32, i32, u64, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(Stats)]
     L.hsa_splice_seeds_device.argtypes = [vp, C.POINTER(Regime), C.POINTER(SeedBatch), vp]
+    f32 = np.ctypeslib.ndpointer(np.float32, flags="C")
+    L.hsa_pass_times.argtypes = [vp, C.c_int, f32, f32]
     L.hsa_cal_sa_reg_gap_flat.restype = C.c_long
     L.hsa_cal_sa_reg_gap_flat.argtypes = [vp, C.POINTER(GapOpt), C.c_int, u32, u64, u8, C.c_size_t, i32, u32, u64,
                                           C.POINTER(C.POINTER(C.c_uint32)), i32, C.POINTER(Stats)]
@@ -272,6 +284,13 @@ class GpuIndex:
         w, q = C.c_float(), C.c_float()
         check(lib().hsa_last_pass_ms(self.h, C.byref(w), C.byref(q)))
         return w.value, q.value
+
+    def pass_times(self, n):
+        """(k_widths ms, k_search ms) arrays of the last n hsa_search_device passes."""
+        w = np.zeros(n, np.float32)
+        s = np.zeros(n, np.float32)
+        check(lib().hsa_pass_times(self.h, n, w, s))
+        return w, s
 
     def nbytes(self) -> int:
         return int(lib().hsa_index_bytes(self.h))

@@ -179,6 +179,7 @@ static int index_init(int device, hsa_index **out)
     HSA_HIP(hipEventCreate(&ix->ev0));
     HSA_HIP(hipEventCreate(&ix->ev1));
     HSA_HIP(hipEventCreate(&ix->evm));
+    ix->ev_split = ix->evm;
     HSA_HIP(hipMalloc(&ix->d_ctr, 16 * sizeof(uint64_t)));
     *out = ix;
     return 0;
@@ -237,6 +238,9 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
     if (ix->evm) (void)hipEventDestroy(ix->evm);
+    for (int i = 0; i < hsa_index::PASS_RING; ++i)
+        for (int j = 0; j < 3; ++j)
+            if (ix->pev[i][j]) (void)hipEventDestroy(ix->pev[i][j]);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
     delete ix;
 }
@@ -411,17 +415,19 @@ extern "C" int hsa_synth_genome_device(int device, uint64_t T, uint64_t seed, ui
 // the 16-character layout issues; 4: the whole sector), 16 waves per CU.  Gives the
 // measured ceiling the search kernels' achieved bandwidth (one sector per query) is
 // compared with (tools/membench.hip is the stand-alone version).
+// PER = 2: four adjacent lanes share one random sector, each loading 16 bytes of it
+// (16 sectors per wave load instruction, every byte of each sector used).
 template <int PER>
 __global__ void __launch_bounds__(256) k_gather(const uint4 *__restrict__ buf, uint64_t nsec, int iters, uint32_t *out)
 {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t acc = 0;
-    uint64_t s = splitmix64(gid + 1);
+    uint64_t s = splitmix64((PER == 2 ? gid >> 2 : gid) + 1);
     for (int it = 0; it < iters; ++it) {
         s = splitmix64(s);
-        const uint4 *p = buf + (s % nsec) * 4 + (PER == 1 ? (s >> 62) : 0);
+        const uint4 *p = buf + (s % nsec) * 4 + (PER == 1 ? (s >> 62) : PER == 2 ? (gid & 3) : 0);
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
+        for (int k = 0; k < (PER == 2 ? 1 : PER); ++k) {
             const uint4 v = p[k];
             acc += v.x ^ v.y ^ v.z ^ v.w;
         }
@@ -437,7 +443,7 @@ __global__ void k_fill_words(uint32_t *buf, uint64_t n)
 
 extern "C" int hsa_probe_gather(int device, uint64_t table_bytes, int per_sector, double *gbps)
 {
-    if (per_sector != 1 && per_sector != 4) { hsa_set_error("per_sector must be 1 or 4"); return HSA_E_ARG; }
+    if (per_sector != 1 && per_sector != 2 && per_sector != 4) { hsa_set_error("per_sector must be 1, 2 or 4"); return HSA_E_ARG; }
     HSA_HIP(hipSetDevice(device));
     hipDeviceProp_t prop;
     HSA_HIP(hipGetDeviceProperties(&prop, device));
@@ -455,6 +461,7 @@ extern "C" int hsa_probe_gather(int device, uint64_t table_bytes, int per_sector
     const int iters = 1000;
     auto launch = [&](int it) {
         if (per_sector == 1) k_gather<1><<<blocks, 256>>>(buf, nsec, it, out);
+        else if (per_sector == 2) k_gather<2><<<blocks, 256>>>(buf, nsec, it, out);
         else k_gather<4><<<blocks, 256>>>(buf, nsec, it, out);
     };
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { rc = HSA_E_HIP; goto done; }
@@ -468,7 +475,7 @@ extern "C" int hsa_probe_gather(int device, uint64_t table_bytes, int per_sector
         rc = HSA_E_HIP;
         goto done;
     }
-    *gbps = (double)blocks * 256 * iters * 64 / (ms * 1e-3) / 1e9;    // sectors touched x 64 B
+    *gbps = (double)blocks * 256 * iters * 64 / (ms * 1e-3) / 1e9 / (per_sector == 2 ? 4 : 1);   // sectors x 64 B
 done:
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);

@@ -53,6 +53,12 @@ struct hsa_index {
     bool staged_mmb = false;            // staged regimes: bucket == n_mm (see mm_buckets)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evm = nullptr;           // between k_widths and k_search of the last pass (timing split)
+    // hsa_search_device passes: start / between k_widths and k_search / end, per pass, in a
+    // ring (hsa_pass_times), so a caller can time every launch of a back-to-back run
+    static constexpr int PASS_RING = 64;
+    hipEvent_t pev[PASS_RING][3] = {};
+    uint64_t pev_n = 0;
+    hipEvent_t ev_split = nullptr;      // recorded by launch_pass between k_widths and k_search
 };
 
 int hsa_grow(void **p, size_t *cap, size_t need);

@@ -95,6 +95,7 @@ struct SearchArgs {
     const hsa_mg_job_t *mg;
     int32_t *cw;
     int32_t *wbid;
+    uint32_t *wq;                  // k_widths: rank queries of each forward-strand width row
 };
 
 // entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
@@ -193,6 +194,24 @@ template <typename WT> struct WFmt {
     __device__ static uint32_t code(uint32_t v) { return (v >> CSH) & 7u; }   // 0..3, or 4..7 for N
 };
 
+#ifdef HSA_DIAG
+// Diagnostic build only (-DHSA_DIAG, never the product library): per-workgroup
+// start/end s_memtime and s_memrealtime of the last launch, for the in-kernel
+// clock and the workgroup-duration spread.
+__device__ unsigned long long g_diag[8192 * 4];
+// event counters: 0 width steps, 1 exact steps, 2 expand steps, 3 virtual-top pops,
+// 4 pool pops, 5 outer iterations (per wave), 6 lanes stepping summed over outer
+// iterations, 7 control-loop iterations (per wave), 8 entries flushed to the pool,
+// 9..12 shader cycles per wave in acquisition / control / rank-load wait / apply,
+// 13 gap_shadow calls with last_diff_pos > 0, 14 their summed last_diff_pos,
+// 15 strand starts, 16/17 exact/expand steps on a unique interval (l == k), 18/19
+// width steps on a unique interval / all width steps
+__device__ unsigned long long g_dctr[32];
+#define DC(i) (++dc[i])
+#else
+#define DC(i) ((void)0)
+#endif
+
 // ---------------------------------------------------------------- k_widths
 // bwt_cal_width type 1 (bwtaln.c:84-97) of every (read, strand): the whole read
 // (width_back) and its last seed_len bases (width_seed, bwtaln.c:344-348).  The
@@ -260,12 +279,19 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
     uint32_t *const wrow = a.wg + rb * a.rg * 64 + rl;
     WChain f{0, a.T, 0, 0, 0}, sd{0, a.T, 0, 0, 0};
     uint32_t st_q = 0, st_b = 0;
+#ifdef HSA_DIAG
+    uint32_t du = 0, dw = 0;
+#endif
     const uint32_t s0 = len - slen;
     auto base = [&](uint32_t sp) -> uint32_t {
         const uint32_t c = a.codes[off + (strand ? len - 1u - sp : sp)];
         return strand && c < 4 ? 3u - c : c;
     };
     for (uint32_t t = 0; t <= len; ++t) {
+#ifdef HSA_DIAG
+        if (t < len) { ++dw; du += f.k == f.l; }
+        if (has_seed && t < slen) { ++dw; du += sd.k == sd.l; }
+#endif
         const uint32_t cf = t < len ? base(t) : 4u;
         // the read's elements also carry the strand sequence's base (k_search's getc)
         width_step<WT>(a, f, t, len, cf, t < len ? F::code_bits(cf) : 0u, brow, wrow, st_q, st_b);
@@ -274,9 +300,21 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
             width_step<WT>(a, sd, t, slen, cs, 0u, srow, nullptr, st_q, st_b);
         }
     }
-    atomicAdd(&a.ctr[2], (unsigned long long)st_q);
+    // rank queries: the reverse-complement strand is always searched (bwtaln.c:343);
+    // the forward strand's widths are computed speculatively and count as the
+    // reference's work only when k_search searches that strand (ctr[13]: all of them)
+    if (strand) {
+        atomicAdd(&a.ctr[2], (unsigned long long)st_q);
+        atomicAdd(&a.ctr[7], (unsigned long long)st_q);
+    } else {
+        a.wq[q] = st_q;
+        atomicAdd(&a.ctr[13], (unsigned long long)st_q);
+    }
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
-    atomicAdd(&a.ctr[7], (unsigned long long)st_q);
+#ifdef HSA_DIAG
+    atomicAdd(&g_dctr[18], (unsigned long long)du);
+    atomicAdd(&g_dctr[19], (unsigned long long)dw);
+#endif
 }
 
 // Caller-width mode: the width rows of each call from the caller's bwt_width_t pairs
@@ -340,22 +378,6 @@ __global__ void __launch_bounds__(BLOCK) k_widths_export(SearchArgs a)
     }
 }
 
-#ifdef HSA_DIAG
-// Diagnostic build only (-DHSA_DIAG, never the product library): per-workgroup
-// start/end s_memtime and s_memrealtime of the last launch, for the in-kernel
-// clock and the workgroup-duration spread.
-__device__ unsigned long long g_diag[8192 * 4];
-// event counters: 0 width steps, 1 exact steps, 2 expand steps, 3 virtual-top pops,
-// 4 pool pops, 5 outer iterations (per wave), 6 lanes stepping summed over outer
-// iterations, 7 control-loop iterations (per wave), 8 entries flushed to the pool,
-// 9..12 shader cycles per wave in acquisition / control / rank-load wait / apply,
-// 13 gap_shadow calls with last_diff_pos > 0, 14 their summed last_diff_pos,
-// 15 strand starts
-__device__ unsigned long long g_dctr[16];
-#define DC(i) (++dc[i])
-#else
-#define DC(i) ((void)0)
-#endif
 
 // NT = lanes per workgroup: 256, or 64 when per-lane LDS (many buckets, long reads)
 // would leave fewer than 16 waves per CU in 256-lane workgroups (plan_launch)
@@ -416,11 +438,11 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     uint4 pf = make_uint4(0, 0, 0, 0);   // POOL(HEAD(lowest bucket)): the next pool pop, loaded ahead
     uint32_t pfl = NIL16;                //   and its NXT link
 #endif
-    uint32_t st_p = 0;
+    uint32_t st_p = 0, st_wq = 0;
     uint64_t st_q = 0, st_b = 0;          // wave-uniform (ballot counts)
     const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
 #ifdef HSA_DIAG
-    uint32_t dc[16] = {0};
+    uint32_t dc[18] = {0};
     uint64_t tsec[4] = {0, 0, 0, 0};
     uint64_t tt = 0;
 #define TMARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); tsec[k] += t_ - tt; tt = t_; } while (0)
@@ -496,7 +518,10 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     };
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
         const int job = a.job_list ? a.job_list[qpos] : (int)qpos;
-        if ((fl & HSA_F_OVERFLOW) && a.ovf_list) a.ovf_list[atomicAdd(&a.ctr[8], 1ull)] = job;
+        if (fl & HSA_F_OVERFLOW) {
+            if (a.ovf_list) a.ovf_list[atomicAdd(&a.ctr[8], 1ull)] = job;   // re-run by the next pass
+            else atomicAdd(&a.ctr[11], 1ull);                               // the last pass: stays unfinished
+        }
         a.n_aln[job] = na;
         a.flags[job] = fl;
         a.hit_off[job] = ho;
@@ -525,6 +550,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             finish_job(0, 0, 0);        // one call, one strand
         } else if (C_STRAND(ctl)) {
             ctl &= ~(1u << 3);          // strand 0
+            st_wq += a.wq[qpos];        // its widths are the reference's work now (bwtaln.c:344-348)
             start_strand();
         } else {
             finish_job(HSA_F_FALLBACK, 0, 0);
@@ -737,6 +763,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             if (lane == 0) dc[6] += (uint32_t)__popcll(rq);
             const uint32_t ph0 = C_PH(ctl);
             if (req) DC(ph0 == PH_EXACT ? 1 : 2);
+            if (req && rp2 == rp1 + 1u) DC(ph0 == PH_EXACT ? 16 : 17);
         }
 #endif
         uint32_t two = 0;
@@ -882,7 +909,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         g_diag[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memtime();
         g_diag[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
     }
-    for (int i = 0; i < 16; ++i)
+    for (int i = 0; i < 18; ++i)
         if (i < 9 || i > 12) atomicAdd(&g_dctr[i], (unsigned long long)dc[i]);
     if (lane == 0)
         for (int i = 0; i < 4; ++i) atomicAdd(&g_dctr[9 + i], (unsigned long long)tsec[i]);
@@ -893,6 +920,11 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     }
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);
+    if (st_wq) {
+        atomicAdd(&a.ctr[2], (unsigned long long)st_wq);
+        atomicAdd(&a.ctr[7], (unsigned long long)st_wq);
+        atomicAdd(&a.ctr[14], (unsigned long long)st_wq);
+    }
 #undef HEAD
 #undef WB
 #undef WS
@@ -1015,9 +1047,9 @@ extern "C" int hsa_diag_read(unsigned long long *out, int n_blocks)
 }
 extern "C" int hsa_diag_counters(unsigned long long *out, int reset)
 {
-    HSA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dctr), sizeof(unsigned long long) * 16));
+    HSA_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dctr), sizeof(unsigned long long) * 32));
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[32] = {0};
         HSA_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dctr), z, sizeof z));
     }
     return 0;
@@ -1205,6 +1237,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + 4 * (size_t)rg)) : nullptr;
+    A.wq = reinterpret_cast<uint32_t *>(wr + rows * (rb + rs + 4 * (size_t)rg + (mg ? 4 * (size_t)rg : 0)));
     return A;
 }
 
@@ -1222,7 +1255,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     const uint32_t rg = (uint32_t)max_len + 1u;
     const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
     const size_t row_bytes = rb + rs + 4 * (size_t)rg + (mg ? 4 * (size_t)rg : 0);   // + full bids (caller widths)
-    if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * row_bytes + 256))) return rc;
+    if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * row_bytes + 4 * (size_t)n + 256))) return rc;
     if (mg) {
         SearchArgs A = pass_args(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
                                  d_ho, d_hits, hit_cap, d_ctr, mg);
@@ -1232,7 +1265,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
         if (P.wide) hipLaunchKernelGGL(k_widths_import<uint16_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
         else hipLaunchKernelGGL(k_widths_import<uint8_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
         HSA_HIP(hipGetLastError());
-        if (ix->evm) HSA_HIP(hipEventRecord(ix->evm, st));
+        if (ix->ev_split) HSA_HIP(hipEventRecord(ix->ev_split, st));
         if (P.wide) launch_search<uint16_t>(P, A, st);
         else launch_search<uint8_t>(P, A, st);
         HSA_HIP(hipGetLastError());
@@ -1249,7 +1282,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     if (P.wide) hipLaunchKernelGGL(k_widths<uint16_t>, dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
     else hipLaunchKernelGGL(k_widths<uint8_t>, dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
     HSA_HIP(hipGetLastError());
-    if (ix->evm && !n_dev) HSA_HIP(hipEventRecord(ix->evm, st));
+    if (ix->ev_split && !n_dev) HSA_HIP(hipEventRecord(ix->ev_split, st));
     if (P.wide) launch_search<uint16_t>(P, A, st);
     else launch_search<uint8_t>(P, A, st);
     HSA_HIP(hipGetLastError());
@@ -1536,7 +1569,12 @@ extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, i
     unsigned long long *ctr = (unsigned long long *)b->d_counters;
     const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
     const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
-    HSA_HIP(hipEventRecord(ix->ev0, st));
+    hipEvent_t *pe = ix->pev[ix->pev_n % hsa_index::PASS_RING];
+    for (int j = 0; j < 3; ++j)
+        if (!pe[j]) HSA_HIP(hipEventCreate(&pe[j]));
+    ++ix->pev_n;
+    ix->ev_split = pe[1];
+    HSA_HIP(hipEventRecord(pe[0], st));
     if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, b->d_jobs, nullptr, b->n_jobs, b->max_len, b->max_seed,
                           b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st,
                           (int32_t *)ix->d_ovf)))
@@ -1552,7 +1590,8 @@ extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, i
                           b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
                           b->hit_cap, ctr, st, nullptr, ctr + 8, 9)))
         return rc;
-    HSA_HIP(hipEventRecord(ix->ev1, st));
+    HSA_HIP(hipEventRecord(pe[2], st));
+    ix->ev_split = ix->evm;
     return 0;
 }
 
@@ -1619,8 +1658,25 @@ extern "C" int hsa_splice_seeds_device(hsa_index_t *ix, const hsa_regime_t *seed
     return 0;
 }
 
+extern "C" int hsa_pass_times(hsa_index_t *ix, int n, float *widths_ms, float *search_ms)
+{
+    if (n < 1 || n > hsa_index::PASS_RING || (uint64_t)n > ix->pev_n) {
+        hsa_set_error("hsa_pass_times: %d passes requested, %llu recorded (ring %d)", n,
+                      (unsigned long long)ix->pev_n, hsa_index::PASS_RING);
+        return HSA_E_ARG;
+    }
+    for (int i = 0; i < n; ++i) {
+        hipEvent_t *pe = ix->pev[(ix->pev_n - (uint64_t)n + (uint64_t)i) % hsa_index::PASS_RING];
+        HSA_HIP(hipEventSynchronize(pe[2]));
+        HSA_HIP(hipEventElapsedTime(widths_ms + i, pe[0], pe[1]));
+        HSA_HIP(hipEventElapsedTime(search_ms + i, pe[1], pe[2]));
+    }
+    return 0;
+}
+
 extern "C" int hsa_last_pass_ms(hsa_index_t *ix, float *widths_ms, float *search_ms)
 {
+    if (ix->pev_n) return hsa_pass_times(ix, 1, widths_ms, search_ms);   // the newest hsa_search_device pass
     HSA_HIP(hipEventSynchronize(ix->ev1));
     HSA_HIP(hipEventElapsedTime(widths_ms, ix->ev0, ix->evm));
     HSA_HIP(hipEventElapsedTime(search_ms, ix->evm, ix->ev1));

@@ -10,7 +10,7 @@
  *   bwt_match_gap_batch  new: many bwt_match_gap calls in one GPU pass
  *   hsa_gpu_attach       new hook, called once after BWTLoad2BWT (bwtaln.c:467)
  *   hsa_gpu_detach       new hook, before BWTFree2BWT (bwtaln.c:527)
- *   hsa_gpu_set_devices  new hook (multi-GPU: reads of one call are split over devices)
+ *   hsa_gpu_set_devices  new hook: the number of devices one call may use (see below)
  *
  * The structs below are declared here only so that the library reads and writes
  * the host's objects at the right offsets; their layouts are those of the

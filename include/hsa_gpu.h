@@ -115,23 +115,43 @@ long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regime
 
 /* Device-resident variant for throughput runs: jobs/codes already on the device,
  * outputs stay on the device (d_hits capacity in records).  Launches on `stream`
- * (a hipStream_t; NULL = the library's stream) and does not synchronise. */
+ * (a hipStream_t; NULL = the library's stream) and does not synchronise: the
+ * caller reads d_counters after the stream completes.
+ *
+ * d_counters: >= 16 u64 of device scratch, zeroed by the call; the library writes
+ *   [1]  hit records allocated (may exceed hit_cap: see [11])
+ *   [2]  rank queries the reference algorithm issues for these reads: 2 per
+ *        bidirectional step, 2 per width step of every strand it searches
+ *        (bwtaln.c:343-359); a read re-run for capacity counts its work twice
+ *   [3]  64-byte rank sectors fetched    [4] gap_pop calls
+ *   [7]  the width queries among [2]
+ *   [8]  reads that overflowed their lane's capacity in the main pass (re-run on
+ *        the device with the large capacity)   [9] the re-run's queue head
+ *   [11] reads left UNFINISHED: still over capacity in the re-run, or their hits
+ *        did not fit in d_hits; such a read keeps HSA_F_OVERFLOW, n_aln 0, no hits.
+ *        Non-zero means: search those reads again with a larger hit_cap.
+ *   [13] width queries of every forward-strand row (computed speculatively)
+ *   [14] the part of [13] the reference issues (forward strands searched)
+ * d_codes: the read codes; the kernels read whole aligned 16-byte words, so the
+ *   buffer must stay readable 16 bytes past the last read's end. */
 typedef struct {
     const hsa_job_t *d_jobs; int n_jobs;
     const uint8_t *d_codes;
     int32_t *d_n_aln; uint32_t *d_flags; uint64_t *d_hit_off;
     uint32_t *d_hits; uint64_t hit_cap;
-    uint64_t *d_counters;         /* >= 8 u64 of device scratch, zeroed by the call: [1] hits, [2] rank
-                                     queries, [3] 64-B blocks fetched, [4] pops, [7] width rank queries */
+    uint64_t *d_counters;         /* >= 16 u64, see above */
     int32_t max_len, max_seed;    /* longest read, longest seed among the jobs */
 } hsa_device_batch_t;
 int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes,
                       const hsa_device_batch_t *b, void *stream);
 /* Device time of the two kernels of the last pass on this index (k_widths, then
- * k_search); waits for that pass to finish. */
+ * k_search with its overflow re-run); waits for that pass to finish. */
 int hsa_last_pass_ms(hsa_index_t *ix, float *widths_ms, float *search_ms);
+/* The same for each of the last n (<= 64) hsa_search_device passes, oldest first:
+ * HIP events recorded on the launch stream around each kernel of every pass. */
+int hsa_pass_times(hsa_index_t *ix, int n, float *widths_ms, float *search_ms);
 /* Kernel geometry/capacity knobs: 0 leaves a knob unchanged; pool_entries < 0 restores
- * its default (8192 entries per lane, 16384 when gap opens are allowed). */
+ * its default (8192 entries per lane, 32768 when gap opens are allowed). */
 int hsa_configure(int waves_per_cu, int pool_entries, int hit_cap);
 
 void hsa_free(void *p);
@@ -203,9 +223,11 @@ int hsa_sa_position_device(hsa_index_t *ix, size_t n, const uint32_t *d_sa_index
 /* Roofline probe: measured rate of uniformly random 64-byte-sector gathers over a
  * table of `table_bytes` (the access pattern of rank queries), in GB/s of sectors
  * touched (sectors/s x 64 B), all CUs at 16 waves each.  per_sector = 1: one 16-byte
- * load per sector (what a rank query issues); 4: the whole sector in four loads.
- * The denominator the search kernel's achieved bandwidth is compared with next to
- * the 8 TB/s spec peak. */
+ * load per sector (what a rank query issues); 2: four adjacent lanes load the four
+ * 16-byte quarters of one sector (16 sectors per wave instruction); 4: each lane
+ * loads its whole sector in four loads.  The denominator the search kernel's
+ * achieved bandwidth is compared with next to the 8 TB/s spec peak (SURVEY.md §8d;
+ * DESIGN.md "The random-access ceiling"). */
 int hsa_probe_gather(int device, uint64_t table_bytes, int per_sector, double *gbps);
 
 /* Suffix-array based BWT construction on the device for a text given as LSB-first

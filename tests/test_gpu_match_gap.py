@@ -139,7 +139,7 @@ def test_splice_seeds_device_match_oracle(tiny):
     reference's own seed calls)."""
     import torch
     from hsa_amd import splice
-    from hsa_amd._lib import JOB_DTYPE, DeviceBatch, SeedBatch, regime_of
+    from hsa_amd._lib import JOB_DTYPE, DeviceBatch, SeedBatch, pad_codes, regime_of
     from oracle_ctypes import Opt, OracleIndex, default_opt
     from test_splice_seeds import read_fastq
     lens, codes = read_fastq(os.path.join(GOLD, MAN["splice_reads"]))
@@ -159,7 +159,7 @@ def test_splice_seeds_device_match_oracle(tiny):
     def dev(a):
         return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
-    d_jobs, d_codes = dev(jobs.view(np.uint8)), dev(codes)
+    d_jobs, d_codes = dev(jobs.view(np.uint8)), dev(pad_codes(codes))
     cap = n * 64
     m = dict(n=torch.zeros(n, dtype=torch.int32, device="cuda"), f=torch.zeros(n, dtype=torch.int32, device="cuda"),
              o=torch.zeros(n, dtype=torch.int64, device="cuda"), h=torch.zeros(cap * 9, dtype=torch.int32, device="cuda"),

@@ -100,20 +100,20 @@ def test_overflow_rerun_is_exact(name):
     _compare(name, pool_entries=64)
 
 
-def test_device_path_rerun_is_exact():
-    """hsa_search_device (device-resident batch, bench.py's path) re-runs reads that
-    overflow their lane's capacity on the device: with a tiny pool most reads of a
-    gapped case take that route, and every hit must still equal the oracle's."""
+def _device_run(case, pool_entries=0, cap=None):
+    """One hsa_search_device call (device-resident batch, bench.py's path) on a golden
+    case as a steady-state batch (GAPE already cleared: both regimes coincide), and
+    the oracle's bwa_cal_sa_reg_gap on the same reads."""
     import torch
-    from hsa_amd._lib import JOB_DTYPE, DeviceBatch, GapOpt, Regime, configure
+    from hsa_amd._lib import JOB_DTYPE, DeviceBatch, GapOpt, Regime, configure, pad_codes
     from oracle_ctypes import Opt, OracleIndex, default_opt
-    g = load_case("tiny_gap100_n4o1")
+    g = load_case(case)
     fwd, rev = index_io.read_index(INDEX[g["index"]])
     ix = gpu_index(g["index"])
     od = parse_opts(g["args"], default_opt())
-    od["mode"] &= ~0x01                      # a steady-state batch: both regimes coincide
+    od["mode"] &= ~0x01
     n = len(g["lens"])
-    e_n, e_f, e_h, _ = OracleIndex(fwd, rev).cal_sa_reg_gap(g["lens"], g["codes"], Opt.from_dict(od))
+    exp = OracleIndex(fwd, rev).cal_sa_reg_gap(g["lens"], g["codes"], Opt.from_dict(od))
     o = GapOpt.from_dict(od)
     n_stacks = (o.max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape
     rg = Regime(s_mm=o.s_mm, s_gapo=o.s_gapo, s_gape=o.s_gape, mode=0, indel_end_skip=o.indel_end_skip,
@@ -125,29 +125,70 @@ def test_device_path_rerun_is_exact():
     jobs["max_diff"] = o.max_diff
     jobs["seed_len"] = np.where(g["lens"] > o.seed_len, o.seed_len, 0x7FFFFFFF)
     d_jobs = torch.from_numpy(jobs.view(np.uint8).copy()).cuda()
-    d_codes = torch.from_numpy(np.ascontiguousarray(g["codes"])).cuda()
-    cap = n * 16
+    d_codes = torch.from_numpy(pad_codes(g["codes"])).cuda()
+    cap = n * 16 if cap is None else cap
     t = dict(n=torch.zeros(n, dtype=torch.int32, device="cuda"), f=torch.zeros(n, dtype=torch.int32, device="cuda"),
-             o=torch.zeros(n, dtype=torch.int64, device="cuda"), h=torch.zeros(cap * 9, dtype=torch.int32, device="cuda"),
+             o=torch.zeros(n, dtype=torch.int64, device="cuda"),
+             h=torch.zeros(max(cap, 1) * 9, dtype=torch.int32, device="cuda"),
              c=torch.zeros(16, dtype=torch.int64, device="cuda"))
     b = DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=n, d_codes=d_codes.data_ptr(), d_n_aln=t["n"].data_ptr(),
                     d_flags=t["f"].data_ptr(), d_hit_off=t["o"].data_ptr(), d_hits=t["h"].data_ptr(), hit_cap=cap,
                     d_counters=t["c"].data_ptr(), max_len=int(g["lens"].max()), max_seed=o.seed_len)
-    configure(pool_entries=8)
+    if pool_entries:
+        configure(pool_entries=pool_entries)
     try:
         ix.search_device([rg], b)
         torch.cuda.synchronize()
     finally:
-        configure(pool_entries=-1)
-    reruns = int(t["c"][8].item())
-    assert reruns > 0, reruns
-    g_n = t["n"].cpu().numpy()
-    g_f = t["f"].cpu().numpy().astype(np.uint32)
-    g_o = t["o"].cpu().numpy()
-    g_h = t["h"].cpu().numpy().view(np.uint32).reshape(-1, 9)
-    assert not (g_f & 2).any(), "reads left overflowed after the re-run"
-    assert np.array_equal(g_f & 1, e_f & 1)
-    assert np.array_equal(g_n, e_n)
+        if pool_entries:
+            configure(pool_entries=-1)
+    got = dict(n=t["n"].cpu().numpy(), f=t["f"].cpu().numpy().astype(np.uint32), o=t["o"].cpu().numpy(),
+               h=t["h"].cpu().numpy().view(np.uint32).reshape(-1, 9), c=t["c"].cpu().numpy())
+    return got, exp
+
+
+def test_device_path_rerun_is_exact():
+    """hsa_search_device re-runs reads that overflow their lane's capacity on the
+    device: with a tiny pool most reads of a gapped case take that route, and every
+    hit must still equal the oracle's."""
+    got, (e_n, e_f, e_h, _) = _device_run("tiny_gap100_n4o1", pool_entries=8)
+    assert got["c"][8] > 0, got["c"][8]
+    assert got["c"][11] == 0, "reads left unfinished after the re-run"
+    assert not (got["f"] & 2).any(), "reads left overflowed after the re-run"
+    assert np.array_equal(got["f"] & 1, e_f & 1)
+    assert np.array_equal(got["n"], e_n)
     exp = split_hits(e_n, e_h)
-    bad = [i for i in range(n) if not np.array_equal(g_h[g_o[i]:g_o[i] + max(g_n[i], 0)], exp[i])]
+    bad = [i for i in range(len(exp)) if not np.array_equal(got["h"][got["o"][i]:got["o"][i] + max(got["n"][i], 0)],
+                                                             exp[i])]
     assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
+
+
+@pytest.mark.parametrize("case", ["tiny_mm100_n4o0", "tiny_gap100_n4o1", "rep_mm100_n4o1"])
+def test_rank_queries_match_oracle(case):
+    """The roofline numerator: the rank queries the kernels count (d_counters[2]) are
+    the ones the reference algorithm issues -- widths only for the strands it
+    searches (bwtaln.c:343-359), 2 per bidirectional step -- exactly the oracle's
+    count on the same reads (no read overflows at the default capacity)."""
+    got, (_, _, _, st) = _device_run(case)
+    assert got["c"][8] == 0
+    assert int(got["c"][2]) == int(st[0]), (int(got["c"][2]), int(st[0]))
+    assert int(got["c"][4]) == int(st[1]), "gap_pop count"
+    # the speculative forward-strand widths are counted apart: all >= searched ones
+    assert got["c"][13] >= got["c"][14]
+
+
+def test_device_path_hit_buffer_exhausted_is_reported():
+    """A caller hit buffer too small for the batch: the reads whose hits do not fit
+    stay flagged HSA_F_OVERFLOW with no hits and are counted in d_counters[11]
+    (include/hsa_gpu.h); every read that completed is exact."""
+    got, (e_n, e_f, e_h, _) = _device_run("tiny_mm100_n4o0", cap=40)
+    unfinished = (got["f"] & 2) != 0
+    assert unfinished.any()
+    assert int(got["c"][11]) == int(unfinished.sum())
+    exp = split_hits(e_n, e_h)
+    done = np.flatnonzero(~unfinished)
+    assert len(done) > 0
+    for i in done:
+        assert got["n"][i] == e_n[i]
+        assert np.array_equal(got["h"][got["o"][i]:got["o"][i] + max(got["n"][i], 0)], exp[i])
+    assert (got["n"][unfinished] == 0).all()
