@@ -79,10 +79,16 @@ __device__ __forceinline__ uint32_t hsa_occ_pair(const RankDir d, uint32_t p1, u
 {
     p1 -= (p1 > d.isa0);
     p2 -= (p2 > d.isa0);
-    // a narrow interval has both ends in one block: then one load serves both
-    const uint4 q1 = hsa_blk_load(d.blk, p1 >> 4);
-    uint4 q2 = q1;
-    if ((p2 >> 4) != (p1 >> 4)) q2 = hsa_blk_load(d.blk, p2 >> 4);
+    // a narrow interval has both ends in one block: then one load serves both.  The
+    // second load is issued before the first is waited for (q2 is chosen after both):
+    // with `q2 = q1; if (..) q2 = load` the compiler waits for q1 before the branch
+    // and the two sectors of a wide interval cost two serial memory latencies.
+    const uint32_t b1 = p1 >> 4, b2 = p2 >> 4;
+    const bool two = b2 != b1;
+    const uint4 q1 = hsa_blk_load(d.blk, b1);
+    uint4 q2r = make_uint4(0, 0, 0, 0);
+    if (two) q2r = hsa_blk_load(d.blk, b2);
+    const uint4 q2 = two ? q2r : q1;
     hsa_occ4_q(q1, p1, a);
     hsa_occ4_q(q2, p2, b);
     return 1u + ((p1 >> 6) != (p2 >> 6));
@@ -101,9 +107,12 @@ __device__ __forceinline__ uint32_t hsa_occ1_pair(const RankDir d, uint32_t p1, 
 {
     p1 -= (p1 > d.isa0);
     p2 -= (p2 > d.isa0);
-    const uint4 q1 = hsa_blk_load(d.blk, p1 >> 4);
-    uint4 q2 = q1;
-    if ((p2 >> 4) != (p1 >> 4)) q2 = hsa_blk_load(d.blk, p2 >> 4);
+    const uint32_t b1 = p1 >> 4, b2 = p2 >> 4;    // both loads in flight (hsa_occ_pair)
+    const bool two = b2 != b1;
+    const uint4 q1 = hsa_blk_load(d.blk, b1);
+    uint4 q2r = make_uint4(0, 0, 0, 0);
+    if (two) q2r = hsa_blk_load(d.blk, b2);
+    const uint4 q2 = two ? q2r : q1;
     a = hsa_occ1_q(q1, p1, c);
     b = hsa_occ1_q(q2, p2, c);
     return 1u + ((p1 >> 6) != (p2 >> 6));

@@ -19,6 +19,9 @@
 static thread_local char g_err[1024] = "";
 int g_waves_per_cu = 16;
 int g_pool_entries = 0;      // 0: 8192 per lane, 32768 when gap opens are allowed
+// k_search: waiting lanes per wave before the wave runs the strand-end / next-read
+// paths (HSA_BATCH_K overrides, for A/B runs)
+int g_batch_k = getenv("HSA_BATCH_K") ? atoi(getenv("HSA_BATCH_K")) : 16;
 int g_hit_cap = 64;
 
 void hsa_set_error(const char *fmt, ...)

@@ -68,4 +68,5 @@ void hsa_scratch_free(SearchScratch &s);
 // Knobs (hsa_configure).
 extern int g_waves_per_cu;
 extern int g_pool_entries;
+extern int g_batch_k;
 extern int g_hit_cap;

@@ -54,7 +54,7 @@
 #define HSA_PREFETCH 0    // keep the next pool pop loaded ahead (costs 5 VGPRs)
 #endif
 
-enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT };
+enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END };
 
 struct SearchArgs {
     RankDir fwd, rev;
@@ -96,6 +96,7 @@ struct SearchArgs {
     int32_t *cw;
     int32_t *wbid;
     uint32_t *wq;                  // k_widths: rank queries of each forward-strand width row
+    uint32_t batch_k;              // rare-event batching threshold (see (A) in k_search)
 };
 
 // entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
@@ -512,6 +513,18 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             for (uint32_t q = 0; q < nws; ++q)
                 __builtin_amdgcn_global_load_lds(ss + q * 64, ds + q * NT, 4, 0, 0);
         }
+#ifdef HSA_EXTRA_LOADS
+        // experiment only: HSA_EXTRA_LOADS random 16-byte rank-table loads per strand
+        // start, to test whether k_search's time follows its memory request count
+        {
+            uint32_t acc = 0, h = qpos * 2654435761u + C_STRAND(ctl);
+            for (int x = 0; x < HSA_EXTRA_LOADS; ++x) {
+                h = h * 1664525u + 1013904223u;
+                acc += a.fwd.blk[h % (a.T >> 4)].w;
+            }
+            if (acc == 0x9e3779b9u) a.ctr[15] = acc;
+        }
+#endif
         __builtin_amdgcn_s_waitcnt(0);                 // the DMA writes are visible to LDS reads
         DC(15);
         start_search();
@@ -534,16 +547,19 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             uint32_t *dst = a.hits + o * 9;
             const uint32_t s30 = C_STRAND(ctl) << 30;
             for (int h = 0; h < n_aln; ++h) {
-                dst[h * 9 + 0] = HB(h * 9 + 0);
-                dst[h * 9 + 1] = HB(h * 9 + 1);
-                dst[h * 9 + 2] = HB(h * 9 + 2);
-                dst[h * 9 + 3] = HB(h * 9 + 3);
-                dst[h * 9 + 4] = HB(h * 9 + 4);
+                // the six staged words first, then the record: one memory round trip per hit
+                const uint32_t v0 = HB(h * 9 + 0), v1 = HB(h * 9 + 1), v2 = HB(h * 9 + 2), v3 = HB(h * 9 + 3),
+                               v4 = HB(h * 9 + 4), v8 = HB(h * 9 + 8);
+                dst[h * 9 + 0] = v0;
+                dst[h * 9 + 1] = v1;
+                dst[h * 9 + 2] = v2;
+                dst[h * 9 + 3] = v3;
+                dst[h * 9 + 4] = v4;
                 dst[h * 9 + 5] = s30;
                 dst[h * 9 + 6] = 0;
                 // bwtaln.c:371-372 (a direct bwt_match_gap call leaves start/end 0)
                 dst[h * 9 + 7] = h == 0 && !a.mg ? (uint32_t)(C_LEN(ctl) - 1) : 0u;
-                dst[h * 9 + 8] = HB(h * 9 + 8);
+                dst[h * 9 + 8] = v8;
             }
             finish_job(0, n_aln, o);
         } else if (a.mg) {
@@ -622,8 +638,16 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     tt = __builtin_amdgcn_s_memtime();
 #endif
     for (;;) {
-        // ---------------- (A) read acquisition, wave aggregated
-        {
+        // ---------------- (A) strand ends and read acquisition, batched per wave.
+        // The rare steps of a read -- copying its hits out (end_strand), the switch to
+        // the forward strand with its row DMA, taking the next read -- are long code
+        // paths that the whole wave executes whenever one lane needs one.  A lane that
+        // reaches one waits (PH_END / PH_IDLE) until batch_k lanes of the wave wait, or
+        // no lane is searching, and the wave then runs each path once for all of them.
+        const uint64_t wm = __ballot(C_PH(ctl) == PH_IDLE || C_PH(ctl) == PH_END);
+        if (wm && ((uint32_t)__popcll(wm) >= a.batch_k ||
+                   __ballot(C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END) == 0)) {
+            if (C_PH(ctl) == PH_END) end_strand();
             const bool need = C_PH(ctl) == PH_IDLE;
             const uint64_t mb = __ballot(need);
             if (mb) {
@@ -678,9 +702,9 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         // rank step (pruned, hit, strand change) just skips this iteration's step
         // instead of making the whole wave run the control code again.
 #if HSA_CTL_LOOP
-        while (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && !req) {
+        while (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END && !req) {
 #else
-        if (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE) do {
+        if (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END) do {
 #endif
 #ifdef HSA_DIAG
             { const uint64_t em = __ballot(1); if (lane == __ffsll((unsigned long long)em) - 1) DC(7); }
@@ -698,7 +722,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 break;
             }
             // PH_POP: bwtgap.c:144-186
-            if (n_entries == 0 || n_entries > RG(max_entries)) { end_strand(); continue; }
+            if (n_entries == 0 || n_entries > RG(max_entries)) { SET_PH(ctl, PH_END); continue; }
             if (C_VT(ctl)) {
                 DC(3);
                 ctl &= ~(1u << 6);                                        // e already holds it
@@ -729,7 +753,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             ++st_p;
             const uint32_t m = e.w;
             if (!(R_MODE & MODE_NONSTOP) && SCORE(M_MM(m), M_GO(m), M_GE(m)) > best_score + S_MM) {
-                end_strand();
+                SET_PH(ctl, PH_END);
                 continue;
             }
             const int em = m_of(m);
@@ -737,7 +761,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             const int ei = M_I(m);
             if (ei > 0 && em < (int)(WB(ei - 1) & F::BIDM)) continue;
             if (ei == 0) {
-                if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) end_strand();
+                if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
                 continue;
             }
             if (em == 0 && (M_ST(m) == ST_M || (R_MODE & MODE_GAPE) || M_GE(m) == R_MAXGE)) {
@@ -794,7 +818,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 const uint32_t rk = aux - (il - ik), erl = e.z + (e.y - e.x);
                 const uint32_t hk = e.x ? ik : 0u, hl = e.y ? il : 0u, hrk = e.z ? rk : 0u, hrl = erl ? aux : 0u;
                 SET_PH(ctl, PH_POP);
-                if (!on_hit(hk, hl, hrk, hrl) && !C_OVF(ctl)) end_strand();
+                if (!on_hit(hk, hl, hrk, hrl) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
             }
         } else if (req && ph == PH_EXPAND) {
             // children of the bidirectional step (2BWT-Interface.c:235-272), in place:
@@ -1233,6 +1257,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.pcap = P.pcap; A.hcap = P.hcap;        // the planned capacities (the scratch may be larger)
     A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
     A.mm_buckets = ix->staged_mmb ? 1u : 0u;
+    A.batch_k = (uint32_t)g_batch_k;
     A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;

@@ -112,6 +112,17 @@ def _device_run(case, pool_entries=0, cap=None):
     ix = gpu_index(g["index"])
     od = parse_opts(g["args"], default_opt())
     od["mode"] &= ~0x01
+    # the device path searches every job it is given: keep the reads that pass
+    # bwa_cal_sa_reg_gap's filters (bwtaln.c:314-325; the drop-in applies them on the host)
+    offs = np.concatenate([[0], np.cumsum(g["lens"].astype(np.int64))])
+    keep = []
+    for r in range(len(g["lens"])):
+        sq = g["codes"][offs[r]:offs[r + 1]]
+        polyat = len(sq) >= 15 and ((sq[:15] == 0).all() or (sq[:15] == 3).all())
+        keep.append(int((sq > 3).sum()) <= od["max_diff"] and not polyat)
+    keep = np.array(keep)
+    g = dict(g, lens=g["lens"][keep], codes=np.concatenate([g["codes"][offs[r]:offs[r + 1]]
+                                                            for r in np.flatnonzero(keep)]))
     n = len(g["lens"])
     exp = OracleIndex(fwd, rev).cal_sa_reg_gap(g["lens"], g["codes"], Opt.from_dict(od))
     o = GapOpt.from_dict(od)

@@ -74,6 +74,49 @@ __global__ void __launch_bounds__(256) k_chain16(const uint4 *__restrict__ buf, 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// A wave-instruction with only `act` of its 64 lanes active: what a load costs the CU
+// when few lanes of a divergent persistent kernel need it (each active lane 16 B of
+// its own random sector).
+__global__ void __launch_bounds__(256) k_sparse(const uint4 *__restrict__ buf, uint64_t nsec, int iters, int act,
+                                                uint32_t *out)
+{
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t acc = 0;
+    uint64_t s = mix(gid + 1);
+    for (int it = 0; it < iters; ++it) {
+        s = mix(s);
+        if (lane < (uint32_t)act) {
+            const uint4 q = buf[(s % nsec) * 4 + (s >> 62)];
+            acc += q.x ^ q.w;
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// LDS-DMA rows: each active lane copies `words` dwords of its own random 128-byte row
+// into LDS (global_load_lds_dword, one instruction per word), as k_search's strand start
+__global__ void __launch_bounds__(256) k_dma(const uint32_t *__restrict__ buf, uint64_t nrows, int iters, int act,
+                                             int words, uint32_t *out)
+{
+    __shared__ uint32_t lds[32 * 256];
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t s = mix(gid + 1);
+    uint32_t acc = 0;
+    for (int it = 0; it < iters; ++it) {
+        s = mix(s);
+        if (lane < (uint32_t)act) {
+            const uint32_t *src = buf + (s % nrows) * 32;
+            uint32_t *dst = lds + (threadIdx.x & ~63u);
+            for (int q = 0; q < words; ++q) __builtin_amdgcn_global_load_lds(src + q, dst + q * 256, 4, 0, 0);
+            __builtin_amdgcn_s_waitcnt(0);
+            acc += lds[threadIdx.x];
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 __global__ void k_fill(uint32_t *buf, uint64_t n)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -94,6 +137,41 @@ int main(int argc, char **argv)
     CHECK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+    if (!strcmp(only, "sparse")) {
+        // loads per second by active lanes per wave instruction, 3 GB table, 16 waves/CU
+        const size_t bytes = (size_t)3 << 30;
+        const uint64_t nsec = bytes / 64;
+        for (int act : {1, 2, 4, 8, 16, 32, 64}) {
+            const int blocks = n_cu * 4, iters = 256;
+            k_sparse<<<blocks, 256>>>(buf, nsec, iters / 4, act, out);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipEventRecord(e0));
+            k_sparse<<<blocks, 256>>>(buf, nsec, iters, act, out);
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+            const double insts = (double)blocks * 4 * iters, lanes = insts * act;
+            printf("{\"mode\": \"sparse\", \"active_lanes\": %d, \"Ginst_per_s\": %.3f, \"Glane_loads_per_s\": %.2f, "
+                   "\"ns_per_inst_per_cu\": %.2f}\n", act, insts / (ms * 1e-3) / 1e9, lanes / (ms * 1e-3) / 1e9,
+                   ms * 1e6 / (insts / n_cu));
+        }
+        for (int act : {1, 4, 16, 64}) {
+            for (int words : {9, 26}) {
+                const int blocks = n_cu * 4, iters = 64;
+                k_dma<<<blocks, 256>>>((const uint32_t *)buf, bytes / 128, iters / 4, act, words, out);
+                CHECK(hipDeviceSynchronize());
+                CHECK(hipEventRecord(e0));
+                k_dma<<<blocks, 256>>>((const uint32_t *)buf, bytes / 128, iters, act, words, out);
+                CHECK(hipEventRecord(e1));
+                CHECK(hipEventSynchronize(e1));
+                float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+                const double rows = (double)blocks * 4 * iters * act, insts = (double)blocks * 4 * iters * words;
+                printf("{\"mode\": \"dma\", \"active_lanes\": %d, \"words\": %d, \"Grows_per_s\": %.3f, "
+                       "\"Ginst_per_s\": %.3f}\n", act, words, rows / (ms * 1e-3) / 1e9, insts / (ms * 1e-3) / 1e9);
+            }
+        }
+        return 0;
+    }
     const size_t sizes[] = {(size_t)128 << 20, (size_t)2 << 30, (size_t)6 << 30, (size_t)12 << 30};
     const int waves[] = {8, 16, 32};
     // lanes per sector and sectors per lane-load for the sector count
