@@ -74,18 +74,21 @@ int hsa_grow(void **p, size_t *cap, size_t need)
 void hsa_scratch_free(SearchScratch &s)
 {
     (void)hipFree(s.pool); (void)hipFree(s.nxt); (void)hipFree(s.hbuf);
+    const size_t lb = s.link_bytes;
     s = SearchScratch();
+    s.link_bytes = lb;
 }
 
-int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap)
+int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap, size_t link_bytes)
 {
     size_t pe = lanes * pcap, he = lanes * hcap;
-    if (pe <= s.pool_entries && he <= s.hit_entries && s.pool) return 0;
+    if (pe <= s.pool_entries && he <= s.hit_entries && s.pool && link_bytes == s.link_bytes) return 0;
     pe = pe > s.pool_entries ? pe : s.pool_entries;
     he = he > s.hit_entries ? he : s.hit_entries;
     hsa_scratch_free(s);
+    s.link_bytes = link_bytes;
     if (hipMalloc(&s.pool, pe * sizeof(uint4)) != hipSuccess ||
-        hipMalloc(&s.nxt, pe * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc(&s.nxt, pe * link_bytes) != hipSuccess ||
         hipMalloc(&s.hbuf, he * 9 * sizeof(uint32_t)) != hipSuccess) {
         hsa_set_error("scratch allocation failed (lanes %zu, pool %zu, hits %zu)", lanes, pcap, hcap);
         hsa_scratch_free(s);
@@ -235,7 +238,8 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (!ix) return;
     (void)hipSetDevice(ix->device);
     (void)hipFree(ix->blk[0]); (void)hipFree(ix->blk[1]);
-    hsa_scratch_free(ix->main); hsa_scratch_free(ix->big);
+    hsa_scratch_free(ix->main); hsa_scratch_free(ix->big); hsa_scratch_free(ix->huge);
+    if (ix->d_ovf2) (void)hipFree(ix->d_ovf2);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed);
     (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);

@@ -24,8 +24,9 @@ void hsa_set_error(const char *fmt, ...);
 struct SearchScratch {
     size_t pool_entries = 0, hit_entries = 0;
     uint4 *pool = nullptr;       // pool_entries
-    uint16_t *nxt = nullptr;     // pool_entries
+    void *nxt = nullptr;         // pool_entries links: uint16_t (main, big passes) or uint32_t (huge pass)
     uint32_t *hbuf = nullptr;    // hit_entries * 9
+    size_t link_bytes = 2;
 };
 
 struct hsa_index {
@@ -36,7 +37,8 @@ struct hsa_index {
     size_t nblk[2] = {0, 0};
     hipStream_t stream = nullptr;
     int n_cu = 0;
-    SearchScratch main, big;
+    SearchScratch main, big, huge;
+    void *d_ovf2 = nullptr; size_t d_ovf2_cap = 0; // device path: reads the big pass hands to the huge pass
     // staging for the host-pointer batch API
     void *d_in = nullptr; size_t d_in_cap = 0;
     void *d_out = nullptr; size_t d_out_cap = 0;
@@ -62,7 +64,7 @@ struct hsa_index {
 };
 
 int hsa_grow(void **p, size_t *cap, size_t need);
-int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap);
+int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap, size_t link_bytes = 2);
 void hsa_scratch_free(SearchScratch &s);
 
 // Knobs (hsa_configure).

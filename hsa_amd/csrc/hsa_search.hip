@@ -35,6 +35,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "hsa_device.h"
 #include "hsa_internal.h"
 
@@ -49,9 +51,6 @@
 #define MAXB 128          // buckets per regime (and score table length)
 #ifndef HSA_CTL_LOOP
 #define HSA_CTL_LOOP 0    // 1: loop the control code until every lane needs a rank step
-#endif
-#ifndef HSA_PREFETCH
-#define HSA_PREFETCH 0    // keep the next pool pop loaded ahead (costs 5 VGPRs)
 #endif
 
 enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END };
@@ -77,7 +76,7 @@ struct SearchArgs {
     uint32_t *wg;                  //   64 rows interleaved; wg: full w values (gap_shadow only)
     uint32_t rb, rs, rg;           //   row capacities: bytes, bytes, words
     uint4 *pool;
-    uint16_t *nxt;
+    void *nxt;                     // pool links: uint16_t, or uint32_t in the huge pass
     uint32_t *hbuf;
     uint32_t pcap, hcap, nb;
     uint32_t off_heads, off_wb, off_ws;   // LDS byte offsets
@@ -88,6 +87,7 @@ struct SearchArgs {
     int32_t *ovf_list;
     const unsigned long long *n_dev;
     uint32_t qctr;
+    uint32_t ovf_ctr;              // counter that numbers this pass's ovf_list entries
     // caller-width mode (hsa_match_gap_batch, bwt_match_gap called directly): per job
     // strand and width_seed kind; k_widths_import builds the rows from the caller's
     // bwt_width_t pairs (cw), the search takes that one strand, and gap_shadow keeps
@@ -382,10 +382,15 @@ __global__ void __launch_bounds__(BLOCK) k_widths_export(SearchArgs a)
 
 // NT = lanes per workgroup: 256, or 64 when per-lane LDS (many buckets, long reads)
 // would leave fewer than 16 waves per CU in 256-lane workgroups (plan_launch)
-template <int MW, bool GAPS, typename WT, int NT>
+// HUGE: the last capacity pass (reads that overflowed the big pass): 32-bit pool
+// links and popped slots reused through a free list, so a lane's pool holds any
+// stack the reference can build (n_entries <= max_entries + 9, bwtgap.c:150-151).
+template <int MW, bool GAPS, typename WT, int NT, bool HUGE = false>
 __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 {
     using F = WFmt<WT>;
+    using LT = typename std::conditional<HUGE, uint32_t, uint16_t>::type;   // pool link
+    constexpr uint32_t NIL = HUGE ? 0xFFFFFFFFu : (uint32_t)NIL16;
 #ifdef HSA_DIAG
     if (threadIdx.x == 0 && blockIdx.x < 8192) {
         g_diag[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime();
@@ -402,7 +407,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     if (tid < 2 * sizeof(hsa_regime_t) / 4)
         reinterpret_cast<uint32_t *>(s_reg)[tid] = reinterpret_cast<const uint32_t *>(a.regimes)[tid];
     __syncthreads();
-    uint16_t *const s_heads = reinterpret_cast<uint16_t *>(s_lds + a.off_heads);
+    LT *const s_heads = reinterpret_cast<LT *>(s_lds + a.off_heads);
     WT *const s_wb = reinterpret_cast<WT *>(s_lds + a.off_wb);
     WT *const s_ws = reinterpret_cast<WT *>(s_lds + a.off_ws);
     // per-lane HBM scratch, wave-interleaved: element e of lane l of wave w at
@@ -410,7 +415,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     // (few pages) and lanes at equal e coalesce
     const size_t wv = gid >> 6;
 #define POOL(s) a.pool[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
-#define NXT(s) a.nxt[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
+#define NXT(s) reinterpret_cast<LT *>(a.nxt)[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
 #define HB(i) a.hbuf[(wv * a.hcap * 9 + (uint32_t)(i)) * 64 + lane]
 #define HEAD(b) s_heads[(uint32_t)(b) * NT + tid]
     // pruning elements in LDS, word-interleaved: the word holding elements
@@ -430,15 +435,12 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     uint32_t aux = 0;              // exact tail: rev_l
     int opt_max_diff = 0, max_diff = 0, best_score = 0, best_cnt = 0, n_aln = 0, n_entries = 0;
     uint32_t pool_top = 0;
+    uint32_t free_head = NIL;      // HUGE: popped slots, linked through NXT
     BMask<MW> mask;
     // the current entry (k, l, rev_k, meta); between an expansion and the next pop
     // it holds the virtual top when C_VT is set (the last child pushed, when it is
     // the next pop: it never goes to the pool)
     uint4 e = make_uint4(0, 0, 0, 0);
-#if HSA_PREFETCH
-    uint4 pf = make_uint4(0, 0, 0, 0);   // POOL(HEAD(lowest bucket)): the next pool pop, loaded ahead
-    uint32_t pfl = NIL16;                //   and its NXT link
-#endif
     uint32_t st_p = 0, st_wq = 0;
     uint64_t st_q = 0, st_b = 0;          // wave-uniform (ballot counts)
     const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
@@ -465,26 +467,29 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         const int sc = SCORE(M_MM(m), M_GO(m), M_GE(m));
         return (uint32_t)sc < MAXB ? (int)s_lds[C_REG(ctl) * MAXB + sc] : 0xFF;
     };
-    // push to the pool (gap_push, bwtgap.c:46-75); pf/pfl keep the head entry of the
-    // lowest non-empty bucket (the next pool pop) so that pops never wait for a load
+    // push to the pool (gap_push, bwtgap.c:46-75)
     auto flush = [&](uint4 v, int b) {
-        if (pool_top >= a.pcap || (uint32_t)b >= a.nb) { ctl |= 1u << 8; return; }
+        if ((uint32_t)b >= a.nb) { ctl |= 1u << 8; return; }
+        uint32_t slot;
+        if (HUGE && free_head != NIL) {
+            slot = free_head;
+            free_head = NXT(slot);
+        } else {
+            if (pool_top >= a.pcap) { ctl |= 1u << 8; return; }
+            slot = pool_top++;
+        }
         DC(8);
-        const uint32_t slot = pool_top++;
         POOL(slot) = v;
-        const uint32_t old = mask.test(b) ? (uint32_t)HEAD(b) : NIL16;
-        NXT(slot) = (uint16_t)old;
-        HEAD(b) = (uint16_t)slot;
-#if HSA_PREFETCH
-        if (b <= mask.lowest()) { pf = v; pfl = old; }
-#endif
+        const uint32_t old = mask.test(b) ? (uint32_t)HEAD(b) : NIL;
+        NXT(slot) = (LT)old;
+        HEAD(b) = (LT)slot;
         mask.set(b);
     };
     auto start_search = [&]() {
         best_score = SCORE(opt_max_diff + 1, R_MAXGO + 1, R_MAXGE + 1);
         max_diff = opt_max_diff;
         best_cnt = 0; n_aln = 0;
-        mask.clear(); pool_top = 0;
+        mask.clear(); pool_top = 0; free_head = NIL;
         e = make_uint4(0, a.T, 0, meta_pack((uint32_t)C_LEN(ctl), ST_M, 0, 0, 0, 0));   // root (bwtgap.c:142)
         ctl |= 1u << 6;
         n_entries = 1;
@@ -532,7 +537,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
         const int job = a.job_list ? a.job_list[qpos] : (int)qpos;
         if (fl & HSA_F_OVERFLOW) {
-            if (a.ovf_list) a.ovf_list[atomicAdd(&a.ctr[8], 1ull)] = job;   // re-run by the next pass
+            if (a.ovf_list) a.ovf_list[atomicAdd(&a.ctr[a.ovf_ctr], 1ull)] = job;   // re-run by the next pass
             else atomicAdd(&a.ctr[11], 1ull);                               // the last pass: stays unfinished
         }
         a.n_aln[job] = na;
@@ -728,26 +733,14 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 ctl &= ~(1u << 6);                                        // e already holds it
             } else {
                 DC(4);
-                // pop the prefetched head of the lowest bucket, then prefetch the next
-                // one (used at the next pool pop, iterations later)
+                // pop the head of the lowest non-empty bucket
                 const int b = mask.lowest();
-#if HSA_PREFETCH
-                e = pf;
-                uint32_t nh = pfl;
-                if (nh == NIL16) {
-                    mask.reset(b);
-                    nh = mask.any() ? (uint32_t)HEAD(mask.lowest()) : NIL16;
-                } else {
-                    HEAD(b) = (uint16_t)nh;
-                }
-                if (nh != NIL16) { pf = POOL(nh); pfl = NXT(nh); }
-#else
                 const uint32_t slot = HEAD(b);
                 e = POOL(slot);
-                const uint16_t nx = NXT(slot);
-                if (nx == NIL16) mask.reset(b);
-                else HEAD(b) = nx;
-#endif
+                const uint32_t nx = NXT(slot);
+                if (nx == NIL) mask.reset(b);
+                else HEAD(b) = (LT)nx;
+                if (HUGE) { NXT(slot) = (LT)free_head; free_head = slot; }
             }
             --n_entries;
             ++st_p;
@@ -1133,11 +1126,19 @@ struct LaunchPlan {
     bool gaps, wide;                 // gap opens possible; 16-bit pruning elements (WFmt)
     uint32_t off_heads, off_wb, off_ws;
     size_t lds;
+    bool huge;                       // PASS_HUGE: 32-bit links, reused slots
 };
 
-static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int nb, bool gaps, bool wide, bool big,
-                       LaunchPlan &P)
+// The capacity passes of one search: MAIN (every read), BIG (the reads that overflowed
+// their main-pass lane: 65 535 pool slots, 16 384 hits), HUGE (the reads that overflowed
+// BIG: reused slots up to max_entries + 16 live entries, 262 144 hits).
+enum { PASS_MAIN = 0, PASS_BIG = 1, PASS_HUGE = 2 };
+
+static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int nb, bool gaps, bool wide, int mode,
+                       LaunchPlan &P, int max_entries = 0)
 {
+    const bool big = mode == PASS_BIG;
+    P.huge = mode == PASS_HUGE;
     P.nb = (uint32_t)nb;
     P.gaps = gaps;
     P.wide = wide;
@@ -1154,7 +1155,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     auto layout = [&](uint32_t nt) {
         P.nt = nt;
         P.off_heads = 2 * MAXB + 128;   // score tables, then the two regimes
-        P.off_wb = P.off_heads + (uint32_t)nb * nt * 2;
+        P.off_wb = P.off_heads + (uint32_t)nb * nt * (P.huge ? 4u : 2u);
         P.off_ws = P.off_wb + ((uint32_t)max_len / epw + 1u) * nt * 4u;
         P.lds = ((size_t)P.off_ws + ((size_t)max_seed / epw + 1u) * nt * 4u + 15) / 16 * 16;
         int per_cu = (int)((160u * 1024u) / P.lds);
@@ -1165,8 +1166,8 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
         return per_cu;
     };
     static const int force256 = getenv("HSA_WG256") != nullptr;   // A/B runs only
-    int per_cu = layout(256);
-    if (per_cu < 4 && !force256) {
+    int per_cu = layout(P.huge ? 64 : 256);
+    if (per_cu < 4 && !force256 && !P.huge) {
         const int p64 = layout(64);
         if (p64 > per_cu * 4) per_cu = p64;
         else per_cu = layout(256);
@@ -1176,7 +1177,9 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     const uint32_t NTB = P.nt;
     size_t blocks = (size_t)ix->n_cu * per_cu;
     size_t need_blocks = ((size_t)n_jobs + NTB - 1) / NTB;
-    if (big) {
+    if (P.huge) {
+        blocks = 1;                                          // 64 lanes: a handful of reads
+    } else if (big) {
         static const size_t big_lanes = getenv("HSA_BIG_LANES") ? strtoull(getenv("HSA_BIG_LANES"), nullptr, 10) : 4096;
         const size_t big_blocks = big_lanes / NTB > 0 ? big_lanes / NTB : 1;
         blocks = need_blocks < big_blocks ? need_blocks : big_blocks;
@@ -1200,6 +1203,13 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     // config 4 (150 bp, -o 1) 2.36 -> 2.07 s per 1M reads at 32768 (49152: same)
     P.pcap = big ? 65535u : (uint32_t)(g_pool_entries ? g_pool_entries : (gaps ? 32768 : 8192));
     P.hcap = big ? 16384u : (uint32_t)g_hit_cap;
+    if (P.huge) {
+        // live entries never exceed max_entries + 9 (bwtgap.c:150-151); the pool is
+        // capped at 4 Mi entries per lane (80 MB), beyond which a read stays unfinished
+        const uint64_t want = (uint64_t)(max_entries > 0 ? max_entries : 0) + 16u;
+        P.pcap = (uint32_t)(want < (4ull << 20) ? want : (4ull << 20));
+        P.hcap = 262144u;
+    }
     return 0;
 }
 
@@ -1222,6 +1232,12 @@ static void launch_search_nt(const LaunchPlan &P, const SearchArgs &A, hipStream
 template <typename WT>
 static void launch_search(const LaunchPlan &P, const SearchArgs &A, hipStream_t st)
 {
+    if (P.huge) {
+        const dim3 g((unsigned)P.blocks), b(64);
+        if (P.gaps) hipLaunchKernelGGL((k_search<2, true, WT, 64, true>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<2, false, WT, 64, true>), g, b, P.lds, st, A);
+        return;
+    }
     if (P.nt == 64) launch_search_nt<WT, 64>(P, A, st);
     else launch_search_nt<WT, 256>(P, A, st);
 }
@@ -1258,7 +1274,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
     A.mm_buckets = ix->staged_mmb ? 1u : 0u;
     A.batch_k = (uint32_t)g_batch_k;
-    A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0;
+    A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0; A.ovf_ctr = 8;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + 4 * (size_t)rg)) : nullptr;
@@ -1271,9 +1287,9 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
                        int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
                        uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st,
                        int32_t *ovf_list = nullptr, const unsigned long long *n_dev = nullptr, uint32_t qctr = 0,
-                       const MgPass *mg = nullptr)
+                       const MgPass *mg = nullptr, uint32_t ovf_ctr = 8)
 {
-    int rc = hsa_scratch_reserve(S, P.lanes, P.pcap, P.hcap);
+    int rc = hsa_scratch_reserve(S, P.lanes, P.pcap, P.hcap, P.huge ? 4 : 2);
     if (rc) return rc;
     const uint32_t esz = P.wide ? 2u : 1u;
     const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;
@@ -1284,7 +1300,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     if (mg) {
         SearchArgs A = pass_args(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
                                  d_ho, d_hits, hit_cap, d_ctr, mg);
-        A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr;
+        A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr; A.ovf_ctr = ovf_ctr;
         if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
         const unsigned nb = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
         if (P.wide) hipLaunchKernelGGL(k_widths_import<uint16_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
@@ -1300,7 +1316,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     }
     SearchArgs A = pass_args(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
                              d_ho, d_hits, hit_cap, d_ctr, nullptr);
-    A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr;
+    A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr; A.ovf_ctr = ovf_ctr;
     if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
     size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
     if (wblocks < 1) wblocks = 1;
@@ -1459,7 +1475,7 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     LaunchPlan P;
     const bool gaps = any_gaps(regimes, n_regimes);
     const bool wide = need_wide(regimes, n_regimes);
-    if ((rc = plan_launch(ix, n_jobs, max_len, max_seed, nb, gaps, wide, false, P))) return rc;
+    if ((rc = plan_launch(ix, n_jobs, max_len, max_seed, nb, gaps, wide, PASS_MAIN, P))) return rc;
     HSA_HIP(hipEventRecord(ix->ev0, st));
     if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs), nullptr, n_jobs,
                           max_len, max_seed, (const uint8_t *)(din + o_codes), d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, st,
@@ -1491,7 +1507,12 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
         if (n_over == 0) { free(list); break; }
         if (stats) stats->overflow_reruns += n_over;
         LaunchPlan B;
-        if ((rc = plan_launch(ix, n_over, max_len, max_seed, nb, gaps, wide, true, B))) { free(list); free(h); return rc; }
+        int max_entries = 0;
+        for (int r = 0; r < n_regimes; ++r) max_entries = regimes[r].max_entries > max_entries ? regimes[r].max_entries : max_entries;
+        const int mode = round == 0 ? PASS_BIG : PASS_HUGE;
+        if ((rc = plan_launch(ix, n_over, max_len, max_seed, nb, gaps, wide, mode, B, max_entries))) {
+            free(list); free(h); return rc;
+        }
         uint64_t cap2 = (uint64_t)n_over * 256 * (round + 1) + 65536;
         void *d2 = nullptr;
         size_t o2_fl = ((size_t)n_jobs * 4 + 255) / 256 * 256;
@@ -1500,7 +1521,7 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
         HSA_HIP(hipMemcpyAsync(din + o_list, list, sizeof(int32_t) * n_over, hipMemcpyHostToDevice, st));
         char *c2 = (char *)d2;
         HSA_HIP(hipEventRecord(ix->ev0, st));
-        if ((rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs),
+        if ((rc = launch_pass(ix, B, mode == PASS_BIG ? ix->big : ix->huge, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs),
                               (const int32_t *)(din + o_list), n_over, max_len, max_seed,
                               (const uint8_t *)(din + o_codes), (int32_t *)c2,
                               (uint32_t *)(c2 + o2_fl), (uint64_t *)(c2 + o2_ho), (uint32_t *)(c2 + o2_hits), cap2,
@@ -1586,11 +1607,17 @@ extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, i
     if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1024))) return rc;
     int nb = 0;
     if ((rc = stage_regimes(ix, regimes, n_regimes, (char *)ix->d_in, nb, st, before != ix->d_in))) return rc;
-    LaunchPlan P;
-    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, any_gaps(regimes, n_regimes),
-                          need_wide(regimes, n_regimes), false, P)))
+    LaunchPlan P, B, H;
+    const bool gaps = any_gaps(regimes, n_regimes), wide = need_wide(regimes, n_regimes);
+    int max_entries = 0;
+    for (int r = 0; r < n_regimes; ++r) max_entries = regimes[r].max_entries > max_entries ? regimes[r].max_entries : max_entries;
+    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_MAIN, P)) ||
+        (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_BIG, B)) ||
+        (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_HUGE, H, max_entries)))
         return rc;
-    if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, (size_t)b->n_jobs * 4 + 64))) return rc;
+    if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, (size_t)b->n_jobs * 4 + 64)) ||
+        (rc = hsa_grow(&ix->d_ovf2, &ix->d_ovf2_cap, (size_t)b->n_jobs * 4 + 64)))
+        return rc;
     unsigned long long *ctr = (unsigned long long *)b->d_counters;
     const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
     const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
@@ -1604,16 +1631,15 @@ extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, i
                           b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st,
                           (int32_t *)ix->d_ovf)))
         return rc;
-    // exact re-run of the reads that overflowed their lane's capacity, with the large
-    // per-lane capacity; the read count stays on the device (ctr[8]), so an empty
-    // re-run is a launch whose lanes exit at once
-    LaunchPlan B;
-    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, any_gaps(regimes, n_regimes),
-                          need_wide(regimes, n_regimes), true, B)))
-        return rc;
+    // exact re-runs of the reads that overflowed their lane's capacity: BIG for the
+    // main pass's (count ctr[8]), HUGE for BIG's (count ctr[12]); the read counts stay
+    // on the device, so an empty re-run is a launch whose lanes exit at once
     if ((rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, b->d_jobs, (const int32_t *)ix->d_ovf, b->n_jobs,
                           b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
-                          b->hit_cap, ctr, st, nullptr, ctr + 8, 9)))
+                          b->hit_cap, ctr, st, (int32_t *)ix->d_ovf2, ctr + 8, 9, nullptr, 12)) ||
+        (rc = launch_pass(ix, H, ix->huge, d_reg, d_bmap, b->d_jobs, (const int32_t *)ix->d_ovf2, b->n_jobs,
+                          b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
+                          b->hit_cap, ctr, st, nullptr, ctr + 12, 15)))
         return rc;
     HSA_HIP(hipEventRecord(pe[2], st));
     ix->ev_split = ix->evm;
@@ -1658,12 +1684,15 @@ extern "C" int hsa_splice_seeds_device(hsa_index_t *ix, const hsa_regime_t *seed
     const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
     const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
     const int seed_max = b->max_len / 3 + 2;
-    LaunchPlan P, B;
+    LaunchPlan P, B, H;
     const bool wide = need_wide(seed_regime, 1);
-    if ((rc = plan_launch(ix, (int)calls, seed_max, 0, nb, false, wide, false, P)) ||
-        (rc = plan_launch(ix, (int)calls, seed_max, 0, nb, false, wide, true, B)))
+    if ((rc = plan_launch(ix, (int)calls, seed_max, 0, nb, false, wide, PASS_MAIN, P)) ||
+        (rc = plan_launch(ix, (int)calls, seed_max, 0, nb, false, wide, PASS_BIG, B)) ||
+        (rc = plan_launch(ix, (int)calls, seed_max, 0, nb, false, wide, PASS_HUGE, H, seed_regime->max_entries)))
         return rc;
-    if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, calls * 4 + 64))) return rc;
+    if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, calls * 4 + 64)) ||
+        (rc = hsa_grow(&ix->d_ovf2, &ix->d_ovf2_cap, calls * 4 + 64)))
+        return rc;
     HSA_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_seed_prep, dim3((unsigned)((2 * n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, S);
     HSA_HIP(hipGetLastError());
@@ -1676,7 +1705,10 @@ extern "C" int hsa_splice_seeds_device(hsa_index_t *ix, const hsa_regime_t *seed
                           &mgp)))
         return rc;
     if ((rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, S.jobs, (const int32_t *)ix->d_ovf, (int)calls, seed_max, 0,
-                          S.codes, b->d_n_aln, sfl, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st, nullptr, ctr + 8, 9,
+                          S.codes, b->d_n_aln, sfl, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st, (int32_t *)ix->d_ovf2,
+                          ctr + 8, 9, &mgp, 12)) ||
+        (rc = launch_pass(ix, H, ix->huge, d_reg, d_bmap, S.jobs, (const int32_t *)ix->d_ovf2, (int)calls, seed_max, 0,
+                          S.codes, b->d_n_aln, sfl, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st, nullptr, ctr + 12, 15,
                           &mgp)))
         return rc;
     HSA_HIP(hipEventRecord(ix->ev1, st));

@@ -125,9 +125,14 @@ long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regime
  *        (bwtaln.c:343-359); a read re-run for capacity counts its work twice
  *   [3]  64-byte rank sectors fetched    [4] gap_pop calls
  *   [7]  the width queries among [2]
- *   [8]  reads that overflowed their lane's capacity in the main pass (re-run on
- *        the device with the large capacity)   [9] the re-run's queue head
- *   [11] reads left UNFINISHED: still over capacity in the re-run, or their hits
+ *   [8]  reads that overflowed their lane's capacity in the main pass (8 192 pool
+ *        slots, 32 768 with gap opens), re-run on the device in the BIG pass (65 535
+ *        slots, 16 384 hits per read)   [9] the big pass's queue head
+ *   [12] reads that overflowed the big pass too, re-run in the HUGE pass: popped
+ *        slots reused, so any stack up to max_entries + 16 live entries fits (the
+ *        reference's own bound, bwtgap.c:150-151; capped at 4 Mi), 262 144 hits
+ *        [15] the huge pass's queue head
+ *   [11] reads left UNFINISHED: still over capacity in the huge pass, or their hits
  *        did not fit in d_hits; such a read keeps HSA_F_OVERFLOW, n_aln 0, no hits.
  *        Non-zero means: search those reads again with a larger hit_cap.
  *   [13] width queries of every forward-strand row (computed speculatively)

@@ -105,7 +105,7 @@ def _device_run(case, pool_entries=0, cap=None):
     case as a steady-state batch (GAPE already cleared: both regimes coincide), and
     the oracle's bwa_cal_sa_reg_gap on the same reads."""
     import torch
-    from hsa_amd._lib import JOB_DTYPE, DeviceBatch, GapOpt, Regime, configure, pad_codes
+    from hsa_amd._lib import JOB_DTYPE, DeviceBatch, GapOpt, configure, pad_codes, regime_of
     from oracle_ctypes import Opt, OracleIndex, default_opt
     g = load_case(case)
     fwd, rev = index_io.read_index(INDEX[g["index"]])
@@ -127,9 +127,7 @@ def _device_run(case, pool_entries=0, cap=None):
     exp = OracleIndex(fwd, rev).cal_sa_reg_gap(g["lens"], g["codes"], Opt.from_dict(od))
     o = GapOpt.from_dict(od)
     n_stacks = (o.max_diff + 1) * o.s_mm + (o.max_gapo + 1) * o.s_gapo + (o.max_gape + 1) * o.s_gape
-    rg = Regime(s_mm=o.s_mm, s_gapo=o.s_gapo, s_gape=o.s_gape, mode=0, indel_end_skip=o.indel_end_skip,
-                max_del_occ=o.max_del_occ, max_entries=o.max_entries, max_gapo=o.max_gapo, max_gape=o.max_gape,
-                max_seed_diff=o.max_seed_diff, max_top2=o.max_top2, n_stacks=n_stacks, max_diff=o.max_diff)
+    rg = regime_of(od, n_stacks, o.max_diff)           # the option bits bwt_match_gap reads (NONSTOP, LOGGAP)
     jobs = np.zeros(n, JOB_DTYPE)
     jobs["off"] = np.concatenate([[0], np.cumsum(g["lens"].astype(np.uint64))[:-1]])
     jobs["len"] = g["lens"]
@@ -203,3 +201,18 @@ def test_device_path_hit_buffer_exhausted_is_reported():
         assert got["n"][i] == e_n[i]
         assert np.array_equal(got["h"][got["o"][i]:got["o"][i] + max(got["n"][i], 0)], exp[i])
     assert (got["n"][unfinished] == 0).all()
+
+
+def test_device_path_huge_pass_is_exact():
+    """Reads whose stacks take more than the big pass's 65 535 slots (NONSTOP, -n 6
+    -o 2 on the repeat-rich index: ~10^5-10^6 pushes per read) finish in the huge pass
+    (reused slots, bwtgap.c:150-151's bound) with the oracle's hits."""
+    got, (e_n, e_f, e_h, _) = _device_run("rep_deep_n6o2N")
+    assert got["c"][12] > 0, "no read reached the huge pass"
+    assert got["c"][11] == 0, "reads left unfinished"
+    assert np.array_equal(got["f"] & 1, e_f & 1)
+    assert np.array_equal(got["n"], e_n)
+    exp = split_hits(e_n, e_h)
+    bad = [i for i in range(len(exp)) if not np.array_equal(got["h"][got["o"][i]:got["o"][i] + max(got["n"][i], 0)],
+                                                             exp[i])]
+    assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
