@@ -27,6 +27,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather", "hsa_last_pass_ms",
     "hsa_index_set_sa", "hsa_sa_position_batch", "hsa_sa_position_device", "hsa_match_gap_batch",
     "bwt_match_gap", "bwt_match_gap_batch", "hsa_splice_seeds_device", "hsa_pass_times",
+    "hsa_cal_sa_reg_gap_multi",
 ]
 
 
@@ -180,6 +181,11 @@ def lib():
     L.hsa_splice_seeds_device.argtypes = [vp, C.POINTER(Regime), C.POINTER(SeedBatch), vp]
     f32 = np.ctypeslib.ndpointer(np.float32, flags="C")
     L.hsa_pass_times.argtypes = [vp, C.c_int, f32, f32]
+    if hasattr(L, "hsa_cal_sa_reg_gap_multi"):      # (older A/B builds lack it)
+        L.hsa_cal_sa_reg_gap_multi.restype = C.c_long
+        L.hsa_cal_sa_reg_gap_multi.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(GapOpt), C.c_int, u32, u64, u8,
+                                               C.c_size_t, i32, u32, u64, C.POINTER(C.POINTER(C.c_uint32)), i32,
+                                               C.POINTER(Stats)]
     L.hsa_cal_sa_reg_gap_flat.restype = C.c_long
     L.hsa_cal_sa_reg_gap_flat.argtypes = [vp, C.POINTER(GapOpt), C.c_int, u32, u64, u8, C.c_size_t, i32, u32, u64,
                                           C.POINTER(C.POINTER(C.c_uint32)), i32, C.POINTER(Stats)]
@@ -368,15 +374,39 @@ class GpuIndex:
         hits = _take_hits(hp, tot)
         return n_aln, flags, hoff, hits, st.as_dict()
 
-    def run_batches(self, lens, codes, opt_dict, batch):
-        """bwa_aln_core's batch loop (bwtaln.c:477-506); hits regrouped in read order."""
+    def cal_sa_reg_gap_slots(self, others, lens, codes, opt: GapOpt):
+        """cal_sa_reg_gap split over this index and `others` (device slots holding the
+        same BWT: hsa_cal_sa_reg_gap_multi)."""
+        ixs = [self] + list(others)
+        arr = (C.c_void_p * len(ixs))(*[i.h for i in ixs])
+        lens = np.ascontiguousarray(lens, np.uint32)
+        n = len(lens)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64) if n else \
+            np.zeros(0, np.uint64)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        n_aln = np.zeros(n, np.int32)
+        flags = np.zeros(n, np.uint32)
+        hoff = np.zeros(n, np.uint64)
+        sp = np.zeros(2 * n + 2, np.int32)
+        hp = C.POINTER(C.c_uint32)()
+        st = Stats()
+        tot = check(lib().hsa_cal_sa_reg_gap_multi(arr, len(ixs), C.byref(opt), n, lens, offs, codes, len(codes), n_aln,
+                                                   flags, hoff, C.byref(hp), sp, C.byref(st)))
+        return n_aln, flags, hoff, _take_hits(hp, tot), st.as_dict()
+
+    def run_batches(self, lens, codes, opt_dict, batch, others=()):
+        """bwa_aln_core's batch loop (bwtaln.c:477-506); hits regrouped in read order.
+        With `others`, each batch is split over the device slots self + others."""
         opt = GapOpt.from_dict(opt_dict)
         lens = np.asarray(lens, np.uint32)
         offs = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
         na_all, fl_all, per_read, stats = [], [], [], []
         for b0 in range(0, len(lens), batch):
             b1 = min(b0 + batch, len(lens))
-            na, fl, ho, hits, st = self.cal_sa_reg_gap(lens[b0:b1], codes[offs[b0]:offs[b1]], opt)
+            if others:
+                na, fl, ho, hits, st = self.cal_sa_reg_gap_slots(others, lens[b0:b1], codes[offs[b0]:offs[b1]], opt)
+            else:
+                na, fl, ho, hits, st = self.cal_sa_reg_gap(lens[b0:b1], codes[offs[b0]:offs[b1]], opt)
             for j in range(b1 - b0):
                 per_read.append(hits[int(ho[j]):int(ho[j]) + max(int(na[j]), 0)])
             na_all.append(na)

@@ -121,12 +121,42 @@ static int hb_append(hitbuf_t *b, const uint32_t *src, size_t n)
     return 0;
 }
 
-/* Search the reads [r0, r1) whose kind is K_JOB; results into the per-read outputs. */
-static int search_range(hsa_index_t *ix, const hsa_regime_t *rg, int r0, int r1, const int8_t *kind,
+/* One device slot's share of a search_range call (its own thread, its own index). */
+typedef struct {
+    hsa_index_t *ix;
+    const hsa_regime_t *rg;
+    hsa_job_t *jobs;
+    int n;
+    const uint8_t *codes;
+    size_t codes_len;
+    int32_t *na;
+    uint32_t *fl;
+    uint64_t *ho;
+    uint32_t *hits;
+    long tot;
+    hsa_stats_t st;
+    char err[256];
+} slot_part_t;
+
+static void *slot_run(void *arg)
+{
+    slot_part_t *p = (slot_part_t *)arg;
+    p->tot = hsa_search_batch(p->ix, p->rg, 1, p->jobs, p->n, p->codes, p->codes_len, p->na, p->fl, p->ho,
+                              &p->hits, &p->st);
+    if (p->tot < 0) snprintf(p->err, sizeof p->err, "%s", hsa_last_error());
+    return NULL;
+}
+
+/* Search the reads [r0, r1) whose kind is K_JOB; results into the per-read outputs.
+ * With several device slots the jobs are split into contiguous parts, one per slot,
+ * searched concurrently (one host thread per slot); reads are independent, so the
+ * parts' results are those of one search over all of them. */
+static int search_range(hsa_index_t *const *ixs, int n_ix, const hsa_regime_t *rg, int r0, int r1, const int8_t *kind,
                         const int32_t *jmd, const int32_t *jsl, int regime, const uint32_t *lens, const uint64_t *offs,
                         const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags, uint64_t *hit_off,
                         hitbuf_t *hb, hsa_stats_t *stats)
 {
+    (void)codes_len;
     int n = 0;
     for (int r = r0; r < r1; ++r) n += kind[r] == K_JOB;
     if (n == 0) return 0;
@@ -142,30 +172,63 @@ static int search_range(hsa_index_t *ix, const hsa_regime_t *rg, int r0, int r1,
         jobs[q].regime = 0;
         map[q++] = r;
     }
-    uint32_t *h = NULL;
-    hsa_stats_t s1;
-    long tot = hsa_search_batch(ix, rg + regime, 1, jobs, n, codes, codes_len, na, fl, ho, &h, &s1);
-    if (tot < 0) { free(jobs); free(map); free(na); free(fl); free(ho); return (int)tot; }
-    size_t base = hb->n;
-    if (hb_append(hb, h, (size_t)tot)) { hsa_free(h); free(jobs); free(map); free(na); free(fl); free(ho); return HSA_E_MEM; }
-    hsa_free(h);
-    for (int j = 0; j < n; ++j) {
-        int r = map[j];
-        n_aln[r] = na[j]; flags[r] = fl[j]; hit_off[r] = ho[j] + base;
+    if (n_ix < 1) n_ix = 1;
+    if (n_ix > n) n_ix = n;
+    slot_part_t part[HSA_MAX_SLOTS];
+    pthread_t th[HSA_MAX_SLOTS];
+    int started[HSA_MAX_SLOTS];
+    for (int k = 0; k < n_ix; ++k) {
+        const int j0 = (int)((long)n * k / n_ix), j1 = (int)((long)n * (k + 1) / n_ix);
+        slot_part_t *p = &part[k];
+        memset(p, 0, sizeof *p);
+        p->ix = ixs[k]; p->rg = rg + regime; p->jobs = jobs + j0; p->n = j1 - j0;
+        p->na = na + j0; p->fl = fl + j0; p->ho = ho + j0;
+        /* the part's codes only: offsets rebased to its first read */
+        const uint64_t c0 = jobs[j0].off, c1 = jobs[j1 - 1].off + jobs[j1 - 1].len;
+        for (int j = j0; j < j1; ++j) jobs[j].off -= c0;
+        p->codes = codes + c0; p->codes_len = (size_t)(c1 - c0);
+        started[k] = k > 0 && pthread_create(&th[k], NULL, slot_run, p) == 0;
+        if (k > 0 && !started[k]) slot_run(p);          /* no thread: run it here */
     }
-    if (stats) {
-        stats->rank_queries += s1.rank_queries; stats->blocks_loaded += s1.blocks_loaded; stats->pops += s1.pops;
-        stats->overflow_reruns += s1.overflow_reruns; stats->kernel_ms += s1.kernel_ms;
-        stats->main_kernel_ms += s1.main_kernel_ms; stats->main_launches += s1.main_launches;
+    slot_run(&part[0]);
+    for (int k = 1; k < n_ix; ++k) if (started[k]) pthread_join(th[k], NULL);
+    int rc = 0;
+    for (int k = 0; k < n_ix && rc == 0; ++k)
+        if (part[k].tot < 0) { rc = (int)part[k].tot; hsa_gpu_set_error_text(part[k].err); }
+    for (int k = 0; k < n_ix && rc == 0; ++k) {
+        slot_part_t *p = &part[k];
+        const size_t base = hb->n;
+        if (hb_append(hb, p->hits, (size_t)p->tot)) { rc = HSA_E_MEM; break; }
+        for (int j = 0; j < p->n; ++j) {
+            const int r = map[(p->jobs - jobs) + j];
+            n_aln[r] = p->na[j]; flags[r] = p->fl[j]; hit_off[r] = p->ho[j] + base;
+        }
+        if (stats) {
+            stats->rank_queries += p->st.rank_queries; stats->blocks_loaded += p->st.blocks_loaded;
+            stats->pops += p->st.pops; stats->overflow_reruns += p->st.overflow_reruns;
+            stats->kernel_ms += p->st.kernel_ms; stats->main_kernel_ms += p->st.main_kernel_ms;
+            stats->main_launches += p->st.main_launches;
+        }
     }
+    for (int k = 0; k < n_ix; ++k) if (part[k].hits) hsa_free(part[k].hits);
     free(jobs); free(map); free(na); free(fl); free(ho);
-    return 0;
+    return rc;
 }
 
 long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint32_t *lens, const uint64_t *offs,
                              const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
                              uint64_t *hit_off, uint32_t **hits, int32_t *splice_opt, hsa_stats_t *stats)
 {
+    return hsa_cal_sa_reg_gap_multi(&ix, 1, opt, n, lens, offs, codes, codes_len, n_aln, flags, hit_off, hits, splice_opt,
+                                    stats);
+}
+
+long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt, int n, const uint32_t *lens,
+                              const uint64_t *offs, const uint8_t *codes, size_t codes_len, int32_t *n_aln,
+                              uint32_t *flags, uint64_t *hit_off, uint32_t **hits, int32_t *splice_opt,
+                              hsa_stats_t *stats)
+{
+    if (n_ix < 1 || n_ix > HSA_MAX_SLOTS) { hsa_gpu_set_error_text("1 to 16 device slots"); return HSA_E_ARG; }
     *hits = NULL;
     if (stats) memset(stats, 0, sizeof *stats);
     gap_opt_t local = *opt;                                 /* :254 */
@@ -193,11 +256,12 @@ long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint3
 
     while (pos < n && rc == 0) {
         if (cur == 0) {
-            const int end = equivalent ? n : (pos + CHUNK0 < n ? pos + CHUNK0 : n);
+            const int chunk = CHUNK0 * n_ix;                /* regime A is searched in chunks (Q2) */
+            const int end = equivalent ? n : (pos + chunk < n ? pos + chunk : n);
             const optstate_t saved = st;
             for (int r = pos; r < end; ++r)
                 kind[r] = (int8_t)plan_read(opt, 0, &st, codes + offs[r], (int)lens[r], &jmd[r], &jsl[r]);
-            rc = search_range(ix, rg, pos, end, kind, jmd, jsl, 0, lens, offs, codes, codes_len, n_aln, flags,
+            rc = search_range(ixs, n_ix, rg, pos, end, kind, jmd, jsl, 0, lens, offs, codes, codes_len, n_aln, flags,
                               hit_off, &hb, stats);
             if (rc) break;
             int f = -1;
@@ -215,7 +279,7 @@ long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint3
         } else {
             for (int r = pos; r < n; ++r)
                 kind[r] = (int8_t)plan_read(opt, 1, &st, codes + offs[r], (int)lens[r], &jmd[r], &jsl[r]);
-            rc = search_range(ix, rg, pos, n, kind, jmd, jsl, 1, lens, offs, codes, codes_len, n_aln, flags,
+            rc = search_range(ixs, n_ix, rg, pos, n, kind, jmd, jsl, 1, lens, offs, codes, codes_len, n_aln, flags,
                               hit_off, &hb, stats);
             pos = n;
         }
@@ -246,41 +310,76 @@ long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint3
 /* ------------------------------------------------------------------ reference ABI */
 
 #define MAX_ATTACH 16
-static struct { const Idx2BWT *key; hsa_index_t *ix; } g_att[MAX_ATTACH];
+/* One attached Idx2BWT: its device index on every slot in use (slot k on device
+ * k % hsa_device_count()).  The table is guarded by g_att_mu; an entry's slots are
+ * only created, never replaced, while the Idx2BWT stays attached. */
+static struct { const Idx2BWT *key; hsa_index_t *ix[HSA_MAX_SLOTS]; int n; } g_att[MAX_ATTACH];
 static pthread_mutex_t g_att_mu = PTHREAD_MUTEX_INITIALIZER;
-static int g_device = 0;
+static int g_slots = 0;                 /* 0: not chosen yet (HSA_GPU_DEVICES, else 1) */
 
-static hsa_index_t *lookup(const Idx2BWT *bi)
+static int slots_in_use(void)
 {
-    for (int i = 0; i < MAX_ATTACH; ++i) if (g_att[i].key == bi) return g_att[i].ix;
-    return NULL;
+    if (g_slots == 0) {
+        const char *e = getenv("HSA_GPU_DEVICES");
+        const int v = e ? atoi(e) : 1;
+        g_slots = v >= 1 && v <= HSA_MAX_SLOTS ? v : 1;
+    }
+    return g_slots;
+}
+
+static int find_entry(const Idx2BWT *bi)
+{
+    for (int i = 0; i < MAX_ATTACH; ++i) if (g_att[i].key == bi) return i;
+    return -1;
 }
 
 int hsa_gpu_set_devices(int n)
 {
-    int have = hsa_device_count();
-    if (n < 1 || n > have) return HSA_E_ARG;
+    if (n < 1 || n > HSA_MAX_SLOTS || hsa_device_count() < 1) return HSA_E_ARG;
+    pthread_mutex_lock(&g_att_mu);
+    g_slots = n;
+    pthread_mutex_unlock(&g_att_mu);
     return 0;
 }
 
-/* Upload the bidirectional BWT of a loaded Idx2BWT once (hook after BWTLoad2BWT). */
-int hsa_gpu_attach(const Idx2BWT *bi)
+/* Upload one slot's copy of the bidirectional BWT (and SA, blocks). */
+static int attach_slot(const Idx2BWT *bi, int slot, hsa_index_t **out)
 {
-    pthread_mutex_lock(&g_att_mu);
-    if (lookup(bi)) { pthread_mutex_unlock(&g_att_mu); return 0; }
-    int slot = -1;
-    for (int i = 0; i < MAX_ATTACH; ++i) if (!g_att[i].key) { slot = i; break; }
-    if (slot < 0) { pthread_mutex_unlock(&g_att_mu); return HSA_E_ARG; }
     const BWT *f = bi->bwt, *r = bi->rev_bwt;
+    const int nd = hsa_device_count();
+    if (nd < 1) return HSA_E_NODEV;
     hsa_index_t *ix = NULL;
-    int rc = hsa_index_create(g_device, f->textLength, f->inverseSa0, f->cumulativeFreq, f->bwtCode,
+    int rc = hsa_index_create(slot % nd, f->textLength, f->inverseSa0, f->cumulativeFreq, f->bwtCode,
                               r->textLength, r->inverseSa0, r->cumulativeFreq, r->bwtCode, &ix);
     /* SA -> position on the device needs the sampled SA (BWT.c:206-223) and blocks */
     if (rc == 0 && f->saValue && bi->hsp)
         rc = hsa_index_set_sa(ix, f->saValue, f->saValueSizeInWord, f->saInterval,
                               (const uint32_t *)bi->hsp->blockList, bi->hsp->numOfBlock);
     if (rc != 0 && ix) { hsa_index_free(ix); ix = NULL; }
-    if (rc == 0) { g_att[slot].key = bi; g_att[slot].ix = ix; }
+    *out = ix;
+    return rc;
+}
+
+/* Upload the bidirectional BWT of a loaded Idx2BWT once per slot in use (hook after
+ * BWTLoad2BWT); slots added later by hsa_gpu_set_devices are attached on first use. */
+int hsa_gpu_attach(const Idx2BWT *bi)
+{
+    pthread_mutex_lock(&g_att_mu);
+    const int want = slots_in_use();
+    int e = find_entry(bi);
+    if (e < 0) {
+        for (int i = 0; i < MAX_ATTACH; ++i) if (!g_att[i].key) { e = i; break; }
+        if (e < 0) { pthread_mutex_unlock(&g_att_mu); return HSA_E_ARG; }
+        g_att[e].key = bi;
+        g_att[e].n = 0;
+    }
+    int rc = 0;
+    while (g_att[e].n < want && rc == 0) {
+        hsa_index_t *ix = NULL;
+        rc = attach_slot(bi, g_att[e].n, &ix);
+        if (rc == 0) g_att[e].ix[g_att[e].n++] = ix;
+    }
+    if (g_att[e].n == 0) g_att[e].key = NULL;
     pthread_mutex_unlock(&g_att_mu);
     return rc;
 }
@@ -288,21 +387,40 @@ int hsa_gpu_attach(const Idx2BWT *bi)
 void hsa_gpu_detach(const Idx2BWT *bi)
 {
     pthread_mutex_lock(&g_att_mu);
-    for (int i = 0; i < MAX_ATTACH; ++i)
-        if (g_att[i].key == bi) { hsa_index_free(g_att[i].ix); g_att[i].key = NULL; g_att[i].ix = NULL; }
+    const int e = find_entry(bi);
+    if (e >= 0) {
+        for (int k = 0; k < g_att[e].n; ++k) hsa_index_free(g_att[e].ix[k]);
+        memset(&g_att[e], 0, sizeof g_att[e]);
+    }
     pthread_mutex_unlock(&g_att_mu);
 }
 
-/* The device index of a loaded Idx2BWT, attached on first use (bwtaln_gpu.h). */
-hsa_index_t *hsa_gpu_index_of(const Idx2BWT *bi)
+/* The device indexes of a loaded Idx2BWT on the slots in use, attached on first use
+ * (bwtaln_gpu.h); *n receives the slot count. */
+hsa_index_t *const *hsa_gpu_slots_of(const Idx2BWT *bi, int *n)
 {
-    hsa_index_t *ix = lookup(bi);
-    if (!ix) {
+    pthread_mutex_lock(&g_att_mu);
+    const int want = slots_in_use();
+    const int e = find_entry(bi);
+    const int ok = e >= 0 && g_att[e].n >= want;
+    pthread_mutex_unlock(&g_att_mu);
+    if (!ok) {
         long rc = hsa_gpu_attach(bi);
         if (rc) hsa_gpu_fatal("hsa_gpu_attach", rc);
-        ix = lookup(bi);
     }
+    pthread_mutex_lock(&g_att_mu);
+    const int e2 = find_entry(bi);
+    hsa_index_t *const *ix = g_att[e2].ix;
+    *n = want;
+    pthread_mutex_unlock(&g_att_mu);
     return ix;
+}
+
+/* The device index of slot 0 (the splice path's direct bwt_match_gap calls). */
+hsa_index_t *hsa_gpu_index_of(const Idx2BWT *bi)
+{
+    int n = 0;
+    return hsa_gpu_slots_of(bi, &n)[0];
 }
 
 /* gap_init_stack layout (bwtgap.c:13-27), for the host's bwt_splice_match */
@@ -337,7 +455,8 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
 {
     (void)tid;
     gap_opt_t *opt = (gap_opt_t *)copt;     /* mutated, as the reference does through aux->opt */
-    hsa_index_t *ix = hsa_gpu_index_of(bi_bwt);
+    int n_slots = 1;
+    hsa_index_t *const *slots = hsa_gpu_slots_of(bi_bwt, &n_slots);
     uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)n_seqs + 1));
     uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)n_seqs + 1));
     size_t tot = 0;
@@ -354,7 +473,8 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     int32_t *sp = (int32_t *)malloc(sizeof(int32_t) * 2 * ((size_t)n_seqs + 1));
     gap_opt_t local = *opt;                 /* local_opt as of :254, before the call mutates *opt */
     uint32_t *hits = NULL;
-    long nh = hsa_cal_sa_reg_gap_flat(ix, opt, n_seqs, lens, offs, codes, tot, n_aln, flags, hoff, &hits, sp, NULL);
+    long nh = hsa_cal_sa_reg_gap_multi(slots, n_slots, opt, n_seqs, lens, offs, codes, tot, n_aln, flags, hoff, &hits, sp,
+                                       NULL);
     if (nh < 0) hsa_gpu_fatal("GPU search", nh);
     if (opt->fnr > 0.0) local.max_diff = cal_maxdiff(max_len, BWA_AVG_ERR, opt->fnr);
     if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;

@@ -4,8 +4,12 @@
 #define BWTALN_GPU_H
 #include "../../include/hsa_bwtaln.h"
 
-/* the device index of a loaded Idx2BWT, attached on first use */
+/* the device index of a loaded Idx2BWT (slot 0), attached on first use */
 hsa_index_t *hsa_gpu_index_of(const Idx2BWT *bi);
+/* its indexes on every device slot in use (hsa_gpu_set_devices); *n = slot count */
+hsa_index_t *const *hsa_gpu_slots_of(const Idx2BWT *bi, int *n);
+/* an error message for hsa_last_error() set from C (the library's buffer is per thread) */
+void hsa_gpu_set_error_text(const char *msg);
 /* the reference's convention for unrecoverable errors: message + exit(1) */
 void hsa_gpu_fatal(const char *what, long rc) __attribute__((noreturn));
 /* aln_score (bwtgap.h) */

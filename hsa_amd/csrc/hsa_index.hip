@@ -33,6 +33,7 @@ void hsa_set_error(const char *fmt, ...)
 }
 
 extern "C" const char *hsa_last_error(void) { return g_err; }
+extern "C" void hsa_gpu_set_error_text(const char *msg) { hsa_set_error("%s", msg); }
 
 extern "C" int hsa_device_count(void)
 {

@@ -50,9 +50,10 @@ struct hsa_index {
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;
     uint64_t *d_ctr = nullptr;
-    unsigned char staged[512];          // last regime block copied to d_in (skip identical re-copies)
+    unsigned char staged[1280];         // last regime block copied to d_in (skip identical re-copies)
     int staged_valid = 0;
     bool staged_mmb = false;            // staged regimes: bucket == n_mm (see mm_buckets)
+    int staged_ntab = 128;              // staged regimes: score table entries per regime (k_search LDS)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evm = nullptr;           // between k_widths and k_search of the last pass (timing split)
     // hsa_search_device passes: start / between k_widths and k_search / end, per pass, in a

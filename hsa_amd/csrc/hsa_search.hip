@@ -48,7 +48,8 @@
 #define ST_D 2
 #define NIL16 0xFFFFu
 #define BLOCK 256
-#define MAXB 128          // buckets per regime (and score table length)
+#define MAXB 128          // dense buckets per regime (BMask<2>)
+#define MAXS 512          // score table length per regime (n_stacks <= MAXS)
 #ifndef HSA_CTL_LOOP
 #define HSA_CTL_LOOP 0    // 1: loop the control code until every lane needs a rank step
 #endif
@@ -60,7 +61,8 @@ struct SearchArgs {
     uint32_t T;
     uint32_t C[5];
     const hsa_regime_t *regimes;
-    const uint8_t *bmap;           // [2][MAXB]: aln_score -> dense bucket (0xFF: unreachable)
+    const uint8_t *bmap;           // [2][MAXS]: aln_score -> dense bucket (0xFF: unreachable)
+    uint32_t ntab;                 // score table entries per regime kept in LDS (>= every n_stacks, multiple of 8)
     const hsa_job_t *jobs;
     const int32_t *job_list;       // optional indirection (re-runs); null = identity
     int n_jobs;
@@ -401,9 +403,10 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     const uint32_t tid = threadIdx.x;
     const uint32_t gid = blockIdx.x * NT + tid;
     const int lane = (int)(tid & 63);
-    for (uint32_t t = tid; t < 2 * MAXB; t += NT) s_lds[t] = a.bmap[t];
+    // the two regimes' score tables (ntab entries each), then the two regimes
+    for (uint32_t t = tid; t < 2 * a.ntab; t += NT) s_lds[t] = a.bmap[(t / a.ntab) * MAXS + t % a.ntab];
     static_assert(2 * sizeof(hsa_regime_t) <= 128, "regime LDS slot");
-    hsa_regime_t *const s_reg = reinterpret_cast<hsa_regime_t *>(s_lds + 2 * MAXB);
+    hsa_regime_t *const s_reg = reinterpret_cast<hsa_regime_t *>(s_lds + 2 * a.ntab);
     if (tid < 2 * sizeof(hsa_regime_t) / 4)
         reinterpret_cast<uint32_t *>(s_reg)[tid] = reinterpret_cast<const uint32_t *>(a.regimes)[tid];
     __syncthreads();
@@ -465,7 +468,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     auto bucket_of = [&](uint32_t m) -> int {
         if (!GAPS && a.mm_buckets) return M_MM(m);
         const int sc = SCORE(M_MM(m), M_GO(m), M_GE(m));
-        return (uint32_t)sc < MAXB ? (int)s_lds[C_REG(ctl) * MAXB + sc] : 0xFF;
+        return (uint32_t)sc < a.ntab ? (int)s_lds[C_REG(ctl) * a.ntab + sc] : 0xFF;
     };
     // push to the pool (gap_push, bwtgap.c:46-75)
     auto flush = [&](uint4 v, int b) {
@@ -1077,7 +1080,7 @@ static int check_regimes(const hsa_regime_t *rg, int n)
     for (int r = 0; r < n; ++r) {
         const hsa_regime_t &R = rg[r];
         if (R.s_mm < 0 || R.s_gapo < 0 || R.s_gape < 0) { hsa_set_error("negative penalty"); return HSA_E_ARG; }
-        if (R.n_stacks <= 0 || R.n_stacks > MAXB) { hsa_set_error("n_stacks %d outside 1..%d", R.n_stacks, MAXB); return HSA_E_ARG; }
+        if (R.n_stacks <= 0 || R.n_stacks > MAXS) { hsa_set_error("n_stacks %d outside 1..%d", R.n_stacks, MAXS); return HSA_E_ARG; }
         if (R.max_gapo > 14 || R.max_gape > 254) { hsa_set_error("max_gapo/max_gape out of range"); return HSA_E_ARG; }
         if (R.max_diff < -1 || R.max_diff > 125) { hsa_set_error("max_diff out of range"); return HSA_E_ARG; }
     }
@@ -1087,19 +1090,19 @@ static int check_regimes(const hsa_regime_t *rg, int n)
 // Dense bucket numbering of the scores a search of this regime can push
 // (bwtgap.c:46-75): n_mm <= max_diff+1, n_gapo <= min(max_gapo, max_diff), n_gape > 0
 // only after a gap open.  Returns the bucket count.
-static int bucket_map(const hsa_regime_t &R, uint8_t map[MAXB])
+static int bucket_map(const hsa_regime_t &R, uint8_t map[MAXS])
 {
-    bool used[MAXB] = {false};
+    bool used[MAXS] = {false};
     const int md = R.max_diff < 0 ? 0 : R.max_diff;
     const int go_max = R.max_gapo < md ? R.max_gapo : md;
     for (int mm = 0; mm <= md + 1; ++mm)
         for (int go = 0; go <= go_max; ++go)
             for (int ge = 0; ge <= (go > 0 ? R.max_gape : 0); ++ge) {
                 const int s = mm * R.s_mm + go * R.s_gapo + ge * R.s_gape;
-                if (s >= 0 && s < MAXB && s < R.n_stacks) used[s] = true;
+                if (s >= 0 && s < MAXS && s < R.n_stacks) used[s] = true;
             }
     int k = 0;
-    for (int s = 0; s < MAXB; ++s) map[s] = used[s] ? (uint8_t)k++ : (uint8_t)0xFF;
+    for (int s = 0; s < MAXS; ++s) map[s] = used[s] && k < 0xFF ? (uint8_t)k++ : (uint8_t)0xFF;
     return k;
 }
 
@@ -1113,7 +1116,7 @@ static bool mm_buckets(const hsa_regime_t *rg, int n, const uint8_t *bmap)
         const int md = R.max_diff < 0 ? 0 : R.max_diff;
         for (int mm = 0; mm <= md + 1; ++mm) {
             const int sc = mm * R.s_mm;
-            if (sc >= MAXB || bmap[r * MAXB + sc] != mm) return false;
+            if (sc >= MAXS || bmap[r * MAXS + sc] != mm) return false;
         }
     }
     return true;
@@ -1127,6 +1130,7 @@ struct LaunchPlan {
     uint32_t off_heads, off_wb, off_ws;
     size_t lds;
     bool huge;                       // PASS_HUGE: 32-bit links, reused slots
+    uint32_t ntab;                   // score table entries per regime in LDS
 };
 
 // The capacity passes of one search: MAIN (every read), BIG (the reads that overflowed
@@ -1139,6 +1143,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
 {
     const bool big = mode == PASS_BIG;
     P.huge = mode == PASS_HUGE;
+    P.ntab = (uint32_t)ix->staged_ntab;
     P.nb = (uint32_t)nb;
     P.gaps = gaps;
     P.wide = wide;
@@ -1154,7 +1159,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     // grid -- measured 512 instead of 1024 workgroups, 1.5x slower.)
     auto layout = [&](uint32_t nt) {
         P.nt = nt;
-        P.off_heads = 2 * MAXB + 128;   // score tables, then the two regimes
+        P.off_heads = 2 * P.ntab + 128;   // score tables, then the two regimes
         P.off_wb = P.off_heads + (uint32_t)nb * nt * (P.huge ? 4u : 2u);
         P.off_ws = P.off_wb + ((uint32_t)max_len / epw + 1u) * nt * 4u;
         P.lds = ((size_t)P.off_ws + ((size_t)max_seed / epw + 1u) * nt * 4u + 15) / 16 * 16;
@@ -1273,6 +1278,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.pcap = P.pcap; A.hcap = P.hcap;        // the planned capacities (the scratch may be larger)
     A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
     A.mm_buckets = ix->staged_mmb ? 1u : 0u;
+    A.ntab = P.ntab;
     A.batch_k = (uint32_t)g_batch_k;
     A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0; A.ovf_ctr = 8;
     A.mg = mg ? mg->d_mg : nullptr;
@@ -1357,21 +1363,25 @@ static int jobs_limits(const hsa_job_t *jobs, int n, int &max_len, int &max_seed
     return 0;
 }
 
-// regimes + bucket maps into the staging area: [regimes (256 B)][bmap 2*MAXB].
+// regimes + bucket maps into the staging area: [regimes (256 B)][bmap 2*MAXS].
 // Repeated launches with the same options skip the copy (a pageable H2D copy
 // would otherwise wait for the stream and stall the host between launches).
 static int stage_regimes(hsa_index *ix, const hsa_regime_t *regimes, int n_regimes, char *dst, int &nb,
                          hipStream_t st, bool force)
 {
-    static_assert(256 + 2 * MAXB <= sizeof(ix->staged), "staging copy");
-    uint8_t host[256 + 2 * MAXB];
+    static_assert(256 + 2 * MAXS <= sizeof(ix->staged), "staging copy");
+    uint8_t host[256 + 2 * MAXS];
     memset(host, 0xFF, sizeof host);
     memcpy(host, regimes, sizeof(hsa_regime_t) * n_regimes);
     nb = 1;
+    int ntab = 8;
     for (int r = 0; r < n_regimes; ++r) {
-        int k = bucket_map(regimes[r], host + 256 + r * MAXB);
+        int k = bucket_map(regimes[r], host + 256 + r * MAXS);
         nb = k > nb ? k : nb;
+        ntab = regimes[r].n_stacks > ntab ? regimes[r].n_stacks : ntab;
     }
+    if (nb > MAXB) { hsa_set_error("%d reachable scores: at most %d stack buckets", nb, MAXB); return HSA_E_ARG; }
+    ix->staged_ntab = (ntab + 7) / 8 * 8;
     ix->staged_mmb = mm_buckets(regimes, n_regimes, host + 256);
     if (!force && ix->staged_valid && memcmp(ix->staged, host, sizeof host) == 0) return 0;
     memcpy(ix->staged, host, sizeof host);
@@ -1439,7 +1449,7 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
 
     // device staging: regimes+bmap | jobs | list | codes [| mg jobs | caller widths]
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
-    const size_t o_reg = 0, o_jobs = 1024, o_list = o_jobs + al((size_t)n_jobs * sizeof(hsa_job_t));
+    const size_t o_reg = 0, o_jobs = 1536, o_list = o_jobs + al((size_t)n_jobs * sizeof(hsa_job_t));
     const size_t o_codes = o_list + al((size_t)n_jobs * 4);
     const size_t o_mg = o_codes + al(codes_len + 1);
     const size_t o_cw = o_mg + (mh ? al((size_t)n_jobs * sizeof(hsa_mg_job_t)) : 0);
@@ -1604,7 +1614,7 @@ extern "C" int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, i
     HSA_HIP(hipSetDevice(ix->device));
     hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
     void *before = ix->d_in;
-    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1024))) return rc;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1536))) return rc;
     int nb = 0;
     if ((rc = stage_regimes(ix, regimes, n_regimes, (char *)ix->d_in, nb, st, before != ix->d_in))) return rc;
     LaunchPlan P, B, H;
@@ -1678,7 +1688,7 @@ extern "C" int hsa_splice_seeds_device(hsa_index_t *ix, const hsa_regime_t *seed
     S.cw = (int32_t *)(d + o_cw); S.list = (int32_t *)(d + o_list); S.count = cnt; S.ctr = ctr;
     // the search pass zeroes the counters first; the width queries are added after it
     void *before = ix->d_in;
-    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1024))) return rc;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1536))) return rc;
     int nb = 0;
     if ((rc = stage_regimes(ix, seed_regime, 1, (char *)ix->d_in, nb, st, before != ix->d_in))) return rc;
     const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;

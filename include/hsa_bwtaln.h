@@ -10,7 +10,7 @@
  *   bwt_match_gap_batch  new: many bwt_match_gap calls in one GPU pass
  *   hsa_gpu_attach       new hook, called once after BWTLoad2BWT (bwtaln.c:467)
  *   hsa_gpu_detach       new hook, before BWTFree2BWT (bwtaln.c:527)
- *   hsa_gpu_set_devices  new hook: the number of devices one call may use (see below)
+ *   hsa_gpu_set_devices  new hook: device slots one call is split over (see below)
  *
  * The structs below are declared here only so that the library reads and writes
  * the host's objects at the right offsets; their layouts are those of the
@@ -155,6 +155,16 @@ bwt_aln1_t *bwt_match_gap(bwt_aux_t *aux, int *_n_aln);
 int  bwt_match_gap_batch(bwt_aux_t *const *aux, int n, bwt_aln1_t **out, int *n_out);
 int  hsa_gpu_attach(const Idx2BWT *bi_bwt);
 void hsa_gpu_detach(const Idx2BWT *bi_bwt);
+/* Device slots: each bwa_cal_sa_reg_gap call splits its reads into n contiguous parts,
+ * searched concurrently on slots 0..n-1 (slot k on device k % hsa_device_count(), one
+ * host thread and one uploaded index per slot; several slots may share a device).
+ * Reads are independent except for the option-regime switch after the first splice
+ * fallback read (bwtaln.c:254-363), which the split keeps: regime A is
+ * searched over all slots, the first fallback read is found over all of them, and the
+ * reads after it are searched again in regime B.  Results are those of one device.
+ * 1 <= n <= HSA_MAX_SLOTS; default 1, or the HSA_GPU_DEVICES environment variable.
+ * Returns 0, or HSA_E_ARG (n out of range or no device). */
+#define HSA_MAX_SLOTS 16
 int  hsa_gpu_set_devices(int n);
 
 /* The host's splice fallback (bwtgap.c:748).  Weak: when the host program does
@@ -175,6 +185,11 @@ bwt_aln1_t *bwt_splice_match(bwt_aux_t *aux, int *n_aln) __attribute__((weak));
 long hsa_cal_sa_reg_gap_flat(hsa_index_t *ix, gap_opt_t *opt, int n, const uint32_t *lens, const uint64_t *offs,
                              const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
                              uint64_t *hit_off, uint32_t **hits, int32_t *splice_opt, hsa_stats_t *stats);
+/* The same over n_ix device slots (indexes of the same BWT, see hsa_gpu_set_devices). */
+long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ix, int n_ix, gap_opt_t *opt, int n, const uint32_t *lens,
+                              const uint64_t *offs, const uint8_t *codes, size_t codes_len, int32_t *n_aln,
+                              uint32_t *flags, uint64_t *hit_off, uint32_t **hits, int32_t *splice_opt,
+                              hsa_stats_t *stats);
 
 #ifdef __cplusplus
 }

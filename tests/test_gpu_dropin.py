@@ -29,18 +29,23 @@ MAN = json.load(open(os.path.join(GOLD, "manifest_dropin.json")))
 needs_bin = pytest.mark.skipif(not os.path.exists(HSA_GPU), reason="oracle/_ref/HSA_gpu not built (make -C oracle)")
 
 
-def run_hsa_gpu(args, reads="reads"):
+def run_hsa_gpu(args, reads="reads", slots=1):
     idx = os.path.join(GOLD, "index", "tiny.fa")
     fq = os.path.join(GOLD, MAN[reads])
-    return subprocess.run([HSA_GPU, "aln", *args, idx, fq], capture_output=True, timeout=120)
+    env = dict(os.environ, HSA_GPU_DEVICES=str(slots))
+    return subprocess.run([HSA_GPU, "aln", *args, idx, fq], capture_output=True, timeout=120, env=env)
 
 
 @needs_bin
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,reads", [("default", "reads"), ("n4o0", "reads"), ("splice_default", "splice_reads"),
-                                        ("splice_n4o1", "splice_reads")])
-def test_dropin_sam_identical(name, reads):
-    r = run_hsa_gpu(MAN[name]["args"], reads)
+@pytest.mark.parametrize("name,reads,slots", [("default", "reads", 1), ("n4o0", "reads", 1),
+                                              ("splice_default", "splice_reads", 1), ("splice_n4o1", "splice_reads", 1),
+                                              ("default", "reads", 2), ("splice_n4o1", "splice_reads", 3)])
+def test_dropin_sam_identical(name, reads, slots):
+    """The reference HSA aln with our bwa_cal_sa_reg_gap / bwt_match_gap linked in prints
+    the reference's SAM byte for byte -- also with each call split over 2 or 3 device
+    slots (hsa_gpu_set_devices via HSA_GPU_DEVICES; slots share the one GPU here)."""
+    r = run_hsa_gpu(MAN[name]["args"], reads, slots)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     sam = r.stdout
     if hashlib.sha256(sam).hexdigest() != MAN[name]["sam_sha256"]:

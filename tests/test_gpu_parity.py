@@ -216,3 +216,66 @@ def test_device_path_huge_pass_is_exact():
     bad = [i for i in range(len(exp)) if not np.array_equal(got["h"][got["o"][i]:got["o"][i] + max(got["n"][i], 0)],
                                                              exp[i])]
     assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
+
+
+def _slot_indexes(name, n):
+    from hsa_amd._lib import GpuIndex
+    key = f"{name}#slots"
+    if key not in _GPU:
+        _GPU[key] = [GpuIndex(*index_io.read_index(INDEX[name])) for _ in range(3)]
+    return _GPU[key][:n]
+
+
+@pytest.mark.parametrize("name,slots", [("tiny_gap100_n4o1_b400", 2), ("tiny_edge_default", 3), ("rep_gap60_default", 2)])
+def test_device_slots_match_reference(name, slots):
+    """bwa_cal_sa_reg_gap split over device slots (hsa_cal_sa_reg_gap_multi: the
+    boundary's hsa_gpu_set_devices) gives the golden hits, the option-regime switch
+    after the first splice fallback read included (tiny_gap100_n4o1_b400)."""
+    from oracle_ctypes import default_opt
+    g = load_case(name)
+    ix = gpu_index(g["index"])
+    n_aln, flags, per_read, _ = ix.run_batches(g["lens"], g["codes"], parse_opts(g["args"], default_opt()), g["batch"],
+                                               others=_slot_indexes(g["index"], slots - 1))
+    exp_splice = (g["flags"] & 1).astype(bool)
+    assert np.array_equal((flags & 1).astype(bool), exp_splice)
+    exp = split_hits(g["n_aln"], g["hits"])
+    bad = [i for i in range(len(exp)) if not exp_splice[i] and not np.array_equal(per_read[i], exp[i])]
+    assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
+
+
+@pytest.mark.parametrize("slots", [1, 2])
+def test_regime_switch_after_first_chunk(slots):
+    """A gapped batch of 20 000 reads whose first splice-fallback read comes after the
+    first 8 192-read chunk (CHUNK0 in bwtaln_gpu.c) and after the first slot's part:
+    regime A up to and including that read, regime B after it (bwtaln.c:254-363),
+    against the oracle's bwa_cal_sa_reg_gap on the same batch."""
+    from hsa_amd._lib import GapOpt
+    from oracle_ctypes import Opt, OracleIndex, default_opt
+    g = load_case("tiny_gap100_n4o1")
+    fwd, rev = index_io.read_index(INDEX["tiny"])
+    L = int(g["lens"][0])
+    assert (g["lens"] == L).all()
+    base = g["codes"].reshape(-1, L)
+    reps = np.concatenate([base] * (20000 // len(base) + 1))[:20000].copy()
+    flags_seq = OracleIndex(fwd, rev).cal_sa_reg_gap(np.full(len(base), L, np.uint32), base.reshape(-1),
+                                                      Opt.from_dict(parse_opts(g["args"], default_opt())))[1]
+    # make every read before 12 345 mappable, and an unmappable read at 12 345
+    mappable = base[np.flatnonzero((flags_seq & 1) == 0)]
+    reps[:12345] = np.concatenate([mappable] * (12345 // len(mappable) + 1))[:12345]
+    rng = np.random.default_rng(9)
+    reps[12345] = rng.integers(0, 4, L)
+    lens = np.full(len(reps), L, np.uint32)
+    od = parse_opts(g["args"], default_opt())
+    e_n, e_f, e_h, _ = OracleIndex(fwd, rev).cal_sa_reg_gap(lens, reps.reshape(-1), Opt.from_dict(od))
+    assert (e_f[:12345] & 1).sum() == 0 and e_f[12345] & 1
+    ix = gpu_index("tiny")
+    others = _slot_indexes("tiny", slots - 1) if slots > 1 else []
+    if others:
+        n_aln, flags, hoff, hits, _ = ix.cal_sa_reg_gap_slots(others, lens, reps.reshape(-1), GapOpt.from_dict(od))
+    else:
+        n_aln, flags, hoff, hits, _ = ix.cal_sa_reg_gap(lens, reps.reshape(-1), GapOpt.from_dict(od))
+    assert np.array_equal(flags & 1, e_f & 1)
+    assert np.array_equal(n_aln, e_n)
+    exp = split_hits(e_n, e_h)
+    bad = [i for i in range(len(exp)) if not np.array_equal(hits[int(hoff[i]):int(hoff[i]) + max(int(n_aln[i]), 0)], exp[i])]
+    assert not bad, f"{len(bad)} reads differ; first {bad[0]}"

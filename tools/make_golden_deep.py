@@ -29,6 +29,12 @@ def main():
     r, _ = synth.make_reads(gr, recr, 60, 100, 31, max_mm=4)
     cases = [("rep_deep_n6o2N", list(r), ["-n", "6", "-o", "2", "-N"]),
              ("rep_deep_n6o2m", list(r), ["-n", "6", "-o", "2", "-m", "30000"])]
+    # more stack buckets than 128 (n_stacks = aln_score(7, 3, 21) = 138): the score
+    # table past the first 128 scores
+    g = synth.genome_codes(200003, 7)
+    rec = synth.record_layout(200003, 3)
+    rt, _ = synth.make_reads(g, rec, 200, 100, 41, indel=True, max_mm_indel=2)
+    tiny_cases = [("tiny_opts_bigstack", list(rt), ["-n", "6", "-o", "2", "-e", "20"])]
     man_path = os.path.join(mg.GOLD, "manifest_tiny.json")
     manifest = json.load(open(man_path))
     with tempfile.TemporaryDirectory() as work:
@@ -38,6 +44,13 @@ def main():
             manifest[name] = {"index": "rep", "args": args, "batch": 100000, "n": len(seqs),
                               "sha256": mg.hits_digest(n_aln, flags, hits), "ref_seconds": secs}
             print(f"  {name}: reference {secs:.2f} s, max hits per read {int(n_aln.max())}")
+        tprefix = os.path.join(ROOT, "tests", "golden", "index", "tiny.fa")
+        for name, seqs, args in tiny_cases:
+            n_aln, flags, hits, secs = mg.run_aln(tprefix, seqs, args, work)
+            mg.save_case(name, "tiny", seqs, args, 100000, n_aln, flags, hits)
+            manifest[name] = {"index": "tiny", "args": args, "batch": 100000, "n": len(seqs),
+                              "sha256": mg.hits_digest(n_aln, flags, hits), "ref_seconds": secs}
+            print(f"  {name}: reference {secs:.2f} s")
     with open(man_path, "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 
