@@ -216,6 +216,7 @@ def main():
                     help="BASELINE.json config: 2 = 0-4 substitutions, -n 4 -o 0 (default, the metric's config); "
                          "3 = one 1-3 bp indel + 0-2 substitutions, -n 4 -o 1; "
                          "4 = 150 bp spliced reads, -n 4 -o 1, main path + the splice path's seed searches")
+    ap.add_argument("--dropin", type=int, default=1, help="also time the host-array drop-in path (1) or not (0)")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0)
     a = ap.parse_args()
@@ -461,6 +462,30 @@ def main():
         if a.config == 4:
             result["seed_rank_queries_per_read"] = round(seed_queries / reads_local, 1)
             result["roofline"]["splice_seeds_ms"] = round(float(np.mean(seeds_ms)), 3)
+
+    # the drop-in path (rank 0, N=1, configs 2 and 3): the C-ABI bwa_cal_sa_reg_gap
+    # (flat form) on HOST arrays, the way a host HSA aln calls it -- reads copied in,
+    # hits copied out and unpacked per read -- at the reference's 100 000 reads per
+    # call (bwtaln.c:477) and at the whole 1 M-read batch per call
+    if rank == 0 and world == 1 and a.config != 4 and a.dropin:
+        src = batches[0]
+        dres = {}
+        for per_call in (100_000, a.batch):
+            per_call = min(per_call, a.batch)
+            o = GapOpt.from_dict(opt.as_dict())
+            gi.cal_sa_reg_gap(np.full(per_call, RL, np.uint32), src[:per_call].reshape(-1), o)   # warm
+            t0 = time.perf_counter()
+            done = 0
+            while done < a.batch:
+                m = min(per_call, a.batch - done)
+                gi.cal_sa_reg_gap(np.full(m, RL, np.uint32), src[done:done + m].reshape(-1), o)
+                done += m
+            dt = time.perf_counter() - t0
+            dres[str(per_call)] = round(a.batch / dt, 1)
+            log(f"[bench] drop-in path: {a.batch} reads in calls of {per_call}: {a.batch / dt:.0f} reads/s")
+        result["dropin"] = {"unit": "reads/s", "reads_per_call": dres,
+                            "what": "hsa_cal_sa_reg_gap_flat on host arrays: H2D reads, widths + search + "
+                                    "re-runs, D2H hits, per-read unpacking (PCIe and host work included)"}
 
     # parity and the CPU baseline (rank 0 at N=1 only): configs 2 and 3 compare the
     # WHOLE timed batch with the C restatement run on the host's cores (that run is

@@ -27,8 +27,10 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_cal_sa_reg_gap_flat", "hsa_index_stream", "hsa_probe_gather", "hsa_last_pass_ms",
     "hsa_index_set_sa", "hsa_sa_position_batch", "hsa_sa_position_device", "hsa_match_gap_batch",
     "bwt_match_gap", "bwt_match_gap_batch", "hsa_splice_seeds_device", "hsa_pass_times",
-    "hsa_cal_sa_reg_gap_multi",
+    "hsa_cal_sa_reg_gap_multi", "hsa_index_create_device64", "hsa_index_is64", "hsa_occ4_batch64",
+    "hsa_search_device64", "hsa_build_bwt_device64",
 ]
+ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
 
 class HsaError(RuntimeError):
@@ -179,6 +181,13 @@ def lib():
     L.hsa_match_gap_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, vp, C.c_int, u8, C.c_size_t, i32, C.c_size_t,
                                       i32, i32, u64, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(Stats)]
     L.hsa_splice_seeds_device.argtypes = [vp, C.POINTER(Regime), C.POINTER(SeedBatch), vp]
+    if hasattr(L, "hsa_search_device64"):           # (older A/B builds lack the 64-bit path)
+        L.hsa_index_create_device64.argtypes = [C.c_int, C.c_uint64, C.c_uint64, u64, vp, C.c_uint64, C.c_uint64,
+                                                u64, vp, C.POINTER(vp)]
+        L.hsa_index_is64.argtypes = [vp]
+        L.hsa_occ4_batch64.argtypes = [vp, C.c_int, C.c_size_t, u64, u64]
+        L.hsa_search_device64.argtypes = [vp, C.POINTER(Regime), C.c_int, C.POINTER(DeviceBatch), vp]
+        L.hsa_build_bwt_device64.argtypes = [C.c_int, C.c_uint64, vp, C.c_int, vp, C.POINTER(C.c_uint64), u64]
     f32 = np.ctypeslib.ndpointer(np.float32, flags="C")
     L.hsa_pass_times.argtypes = [vp, C.c_int, f32, f32]
     if hasattr(L, "hsa_cal_sa_reg_gap_multi"):      # (older A/B builds lack it)
@@ -245,6 +254,32 @@ class GpuIndex:
                                             np.ascontiguousarray(Cr, np.uint32), d_rcode, C.byref(h)))
         self.h = h
         return self
+
+    @classmethod
+    def from_device_codes64(cls, T, isa0, Cf, d_code, rT, risa0, Cr, d_rcode, device=0):
+        """A 64-bit interval index (hsa_index_create_device64): any text length; under
+        2^32 characters the 32-bit entry points serve it too."""
+        self = cls.__new__(cls)
+        self.T = T
+        h = C.c_void_p()
+        check(lib().hsa_index_create_device64(device, T, isa0, np.ascontiguousarray(Cf, np.uint64), d_code, rT, risa0,
+                                              np.ascontiguousarray(Cr, np.uint64), d_rcode, C.byref(h)))
+        self.h = h
+        return self
+
+    def is64(self) -> bool:
+        return bool(lib().hsa_index_is64(self.h))
+
+    def occ4_64(self, d, pos):
+        pos = np.ascontiguousarray(pos, np.uint64)
+        out = np.zeros((len(pos), 4), np.uint64)
+        check(lib().hsa_occ4_batch64(self.h, d, len(pos), pos, out))
+        return out
+
+    def search_device64(self, regimes, batch: "DeviceBatch"):
+        """hsa_search_device64: d_hits holds hsa_aln64_t records (14 u32)."""
+        rg = (Regime * len(regimes))(*regimes)
+        check(lib().hsa_search_device64(self.h, rg, len(regimes), C.byref(batch), None))
 
     def close(self):
         if getattr(self, "h", None):

@@ -15,6 +15,9 @@
 //      exactly the .bwt convention (BWT.c:156-181, BWT.h:61-83).
 // Random texts have essentially no 32-character ties; texts with long exact
 // repeats would spend their time in step 3 (documented in DESIGN.md).
+// Suffix positions are u32 for texts under 2^32 characters and u64 beyond (config 5:
+// the 64-bit index of hsa_index_create_device64); the selection of a batch's
+// positions scans the text in chunks of 2^31 positions.
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -85,17 +88,18 @@ __global__ void k_hist(const uint32_t *t, uint64_t T, unsigned long long *hist, 
     if (threadIdx.x < 4 && c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)c[threadIdx.x]);
 }
 
-struct InBuckets {
+template <typename P> struct InBuckets {
     const uint32_t *t;
     uint32_t lo, hi;
-    __device__ bool operator()(uint32_t p) const
+    __device__ bool operator()(P p) const
     {
         const uint32_t b = (uint32_t)(key32(t, p) >> 56);
         return b >= lo && b < hi;
     }
 };
 
-__global__ void k_keys(const uint32_t *t, const uint32_t *pos, size_t n, uint64_t *keys)
+template <typename P>
+__global__ void k_keys(const uint32_t *t, const P *pos, size_t n, uint64_t *keys)
 {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) keys[i] = key32(t, pos[i]);
@@ -110,12 +114,13 @@ __global__ void k_tie_flags(const uint64_t *keys, size_t n, uint8_t *flag)
 }
 
 // rows [row0, row0+n) of the full (T+1)-row BWT; row = 1 + sorted rank.
-__global__ void k_bwt_chars(const uint32_t *t, const uint32_t *sa, size_t n, uint64_t row0, uint8_t *bwt,
+template <typename P>
+__global__ void k_bwt_chars(const uint32_t *t, const P *sa, size_t n, uint64_t row0, uint8_t *bwt,
                             unsigned long long *isa0)
 {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t p = sa[i];
+    const P p = sa[i];
     if (p == 0) { *isa0 = row0 + i; bwt[row0 + i] = 0; }
     else bwt[row0 + i] = (uint8_t)char_at(t, p - 1);
 }
@@ -153,8 +158,9 @@ struct HostText {
     }
 };
 
-static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d_out, uint32_t *isa0_out,
-                     uint32_t C[5])
+template <typename P>
+static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d_out, uint64_t *isa0_out,
+                     uint64_t C[5])
 {
     (void)device;
     hipStream_t st = 0;
@@ -168,7 +174,7 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
     unsigned long long hist[260];
     HSA_HIP(hipMemcpy(hist, d_hist, sizeof hist, hipMemcpyDeviceToHost));
     C[0] = 0;
-    for (int c = 0; c < 4; ++c) C[c + 1] = C[c] + (uint32_t)hist[256 + c];
+    for (int c = 0; c < 4; ++c) C[c + 1] = C[c] + (uint64_t)hist[256 + c];
 
     uint8_t *d_bwt = nullptr;
     HSA_HIP(hipMalloc(&d_bwt, T + 16));
@@ -182,12 +188,12 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
     size_t maxb = 0;
     for (int b = 0; b < 256; ++b) maxb = std::max(maxb, (size_t)hist[b]);
     const size_t cap = std::max(std::min(kBatch, (size_t)T), maxb);
-    uint32_t *d_pos = nullptr, *d_pos2 = nullptr;
+    P *d_pos = nullptr, *d_pos2 = nullptr;
     uint64_t *d_key = nullptr, *d_key2 = nullptr;
     uint8_t *d_flag = nullptr;
     size_t *d_nsel = nullptr;
-    HSA_HIP(hipMalloc(&d_pos, cap * 4 + 64));
-    HSA_HIP(hipMalloc(&d_pos2, cap * 4 + 64));
+    HSA_HIP(hipMalloc(&d_pos, cap * sizeof(P) + 64));
+    HSA_HIP(hipMalloc(&d_pos2, cap * sizeof(P) + 64));
     HSA_HIP(hipMalloc(&d_key, cap * 8 + 64));
     HSA_HIP(hipMalloc(&d_key2, cap * 8 + 64));
     HSA_HIP(hipMalloc(&d_flag, cap + 64));
@@ -204,12 +210,21 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
         int e = b;
         while (e < 256 && (n + hist[e] <= cap || e == b)) n += hist[e++];
         if (n == 0) { b = e; continue; }
-        // 2. select positions with a bucket in [b, e)
-        InBuckets pred{d_text, (uint32_t)b, (uint32_t)e};
-        rocprim::counting_iterator<uint32_t> it(0u);
-        HSA_HIP(rocprim::select(nullptr, need, it, d_pos, d_nsel, (size_t)T, pred, st));
-        if (need > tmp_bytes) { (void)hipFree(tmp); tmp_bytes = need; HSA_HIP(hipMalloc(&tmp, tmp_bytes)); }
-        HSA_HIP(rocprim::select(tmp, need, it, d_pos, d_nsel, (size_t)T, pred, st));
+        // 2. select positions with a bucket in [b, e), 2^31 text positions at a time
+        InBuckets<P> pred{d_text, (uint32_t)b, (uint32_t)e};
+        size_t got = 0;
+        for (uint64_t c0 = 0; c0 < T; c0 += (uint64_t)1 << 31) {
+            const size_t cn = (size_t)std::min<uint64_t>(T - c0, (uint64_t)1 << 31);
+            rocprim::counting_iterator<P> it((P)c0);
+            HSA_HIP(rocprim::select(nullptr, need, it, d_pos + got, d_nsel, cn, pred, st));
+            if (need > tmp_bytes) { (void)hipFree(tmp); tmp_bytes = need; HSA_HIP(hipMalloc(&tmp, tmp_bytes)); }
+            HSA_HIP(rocprim::select(tmp, need, it, d_pos + got, d_nsel, cn, pred, st));
+            size_t k = 0;
+            HSA_HIP(hipMemcpyAsync(&k, d_nsel, sizeof k, hipMemcpyDeviceToHost, st));
+            HSA_HIP(hipStreamSynchronize(st));
+            got += k;
+        }
+        if (got != n) { hsa_set_error("bwt build: selected %zu of %zu suffixes", got, n); return HSA_E_HIP; }
         k_keys<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d_text, d_pos, n, d_key);
         HSA_HIP(hipGetLastError());
         HSA_HIP(rocprim::radix_sort_pairs(nullptr, need, d_key, d_key2, d_pos, d_pos2, n, 0, 64, st));
@@ -218,9 +233,11 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
         // 3. ties
         k_tie_flags<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d_key2, n, d_flag);
         HSA_HIP(hipGetLastError());
-        HSA_HIP(rocprim::select(nullptr, need, it, d_flag, d_pos, d_nsel, n, st));
+        uint32_t *const d_rank = reinterpret_cast<uint32_t *>(d_pos);              // d_pos := tied ranks
+        rocprim::counting_iterator<uint32_t> rit(0u);
+        HSA_HIP(rocprim::select(nullptr, need, rit, d_flag, d_rank, d_nsel, n, st));
         if (need > tmp_bytes) { (void)hipFree(tmp); tmp_bytes = need; HSA_HIP(hipMalloc(&tmp, tmp_bytes)); }
-        HSA_HIP(rocprim::select(tmp, need, it, d_flag, d_pos, d_nsel, n, st));   // d_pos := tied ranks
+        HSA_HIP(rocprim::select(tmp, need, rit, d_flag, d_rank, d_nsel, n, st));
         size_t nt = 0;
         HSA_HIP(hipMemcpy(&nt, d_nsel, sizeof nt, hipMemcpyDeviceToHost));
         if (nt) {
@@ -228,12 +245,11 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
                 host.w.resize(nwords + 4, 0);
                 HSA_HIP(hipMemcpy(host.w.data(), d_text, nwords * 4, hipMemcpyDeviceToHost));
             }
-            std::vector<uint32_t> rk(nt), ps(nt);
-            std::vector<uint64_t> ky(nt);
-            HSA_HIP(hipMemcpy(rk.data(), d_pos, nt * 4, hipMemcpyDeviceToHost));
+            std::vector<uint32_t> rk(nt);
+            HSA_HIP(hipMemcpy(rk.data(), d_rank, nt * 4, hipMemcpyDeviceToHost));
             // gather the tied keys/positions (ranks are sorted ascending)
             std::vector<uint64_t> kk;
-            std::vector<uint32_t> pp;
+            std::vector<P> pp;
             size_t i = 0;
             while (i < nt) {
                 size_t j = i;
@@ -241,17 +257,17 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
                 size_t len = j - i + 1;
                 kk.resize(len); pp.resize(len);
                 HSA_HIP(hipMemcpy(kk.data(), d_key2 + rk[i], len * 8, hipMemcpyDeviceToHost));
-                HSA_HIP(hipMemcpy(pp.data(), d_pos2 + rk[i], len * 4, hipMemcpyDeviceToHost));
+                HSA_HIP(hipMemcpy(pp.data(), d_pos2 + rk[i], len * sizeof(P), hipMemcpyDeviceToHost));
                 size_t g = 0;
                 while (g < len) {
                     size_t h = g;
                     while (h + 1 < len && kk[h + 1] == kk[g]) ++h;
                     if (h > g)
                         std::sort(pp.begin() + g, pp.begin() + h + 1,
-                                  [&](uint32_t x, uint32_t y) { return host.less(x, y); });
+                                  [&](P x, P y) { return host.less(x, y); });
                     g = h + 1;
                 }
-                HSA_HIP(hipMemcpy(d_pos2 + rk[i], pp.data(), len * 4, hipMemcpyHostToDevice));
+                HSA_HIP(hipMemcpy(d_pos2 + rk[i], pp.data(), len * sizeof(P), hipMemcpyHostToDevice));
                 i = j + 1;
             }
         }
@@ -267,16 +283,16 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
     k_pack<<<(unsigned)((nwords + 255) / 256), 256, 0, st>>>(d_bwt, T, isa0, d_out, nwords);
     HSA_HIP(hipGetLastError());
     HSA_HIP(hipDeviceSynchronize());
-    *isa0_out = (uint32_t)isa0;
+    *isa0_out = (uint64_t)isa0;
     (void)hipFree(tmp); (void)hipFree(d_pos); (void)hipFree(d_pos2); (void)hipFree(d_key); (void)hipFree(d_key2);
     (void)hipFree(d_flag); (void)hipFree(d_nsel); (void)hipFree(d_bwt); (void)hipFree(d_hist);
     return 0;
 }
 
-extern "C" int hsa_build_bwt_device(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse,
-                                    uint32_t *d_bwt_lsb, uint32_t *isa0, uint32_t C[5])
+static int build_bwt(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse, uint32_t *d_bwt_lsb,
+                     uint64_t *isa0, uint64_t C[5])
 {
-    if (T == 0 || T >= 0xFFFFFFFFull) { hsa_set_error("text length must be in [1, 2^32-1)"); return HSA_E_ARG; }
+    if (T == 0) { hsa_set_error("empty text"); return HSA_E_ARG; }
     HSA_HIP(hipSetDevice(device));
     const uint64_t nwords = (T + 15) / 16;
     uint32_t *t = nullptr;
@@ -294,7 +310,31 @@ extern "C" int hsa_build_bwt_device(int device, uint64_t T, const uint32_t *d_te
             HSA_HIP(hipMemcpy(t + nwords - 1, &last, 4, hipMemcpyHostToDevice));
         }
     }
-    int rc = build_one(device, T, t, d_bwt_lsb, isa0, C);
+    // u32 suffix positions while they fit (half the sort traffic of u64)
+    int rc = T < 0xFFFFFFFFull ? build_one<uint32_t>(device, T, t, d_bwt_lsb, isa0, C)
+                               : build_one<uint64_t>(device, T, t, d_bwt_lsb, isa0, C);
     (void)hipFree(t);
     return rc;
+}
+
+extern "C" int hsa_build_bwt_device64(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse,
+                                      uint32_t *d_bwt_lsb, uint64_t *isa0, uint64_t C[5])
+{
+    return build_bwt(device, T, d_text_lsb, reverse, d_bwt_lsb, isa0, C);
+}
+
+// The 32-bit entry point: the .bwt header fields are u32 (BWT.h:61-83)
+extern "C" int hsa_build_bwt_device(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse,
+                                    uint32_t *d_bwt_lsb, uint32_t *isa0, uint32_t C[5])
+{
+    if (T == 0 || T >= 0xFFFFFFFFull) {
+        hsa_set_error("text length must be in [1, 2^32-1) (hsa_build_bwt_device64 builds longer ones)");
+        return HSA_E_ARG;
+    }
+    uint64_t i64 = 0, c64[5] = {0, 0, 0, 0, 0};
+    const int rc = build_bwt(device, T, d_text_lsb, reverse, d_bwt_lsb, &i64, c64);
+    if (rc) return rc;
+    *isa0 = (uint32_t)i64;
+    for (int c = 0; c < 5; ++c) C[c] = (uint32_t)c64[c];
+    return 0;
 }

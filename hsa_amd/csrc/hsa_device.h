@@ -117,3 +117,86 @@ __device__ __forceinline__ uint32_t hsa_occ1_pair(const RankDir d, uint32_t p1, 
     b = hsa_occ1_q(q2, p2, c);
     return 1u + ((p1 >> 6) != (p2 >> 6));
 }
+
+// ---------------------------------------------------------------- 64-bit texts
+// Texts of 2^32 characters or more (config 5; the reference's bwtint_t is 32-bit,
+// 2BWT-Interface.h:26).  The blocks are the same 16-byte blocks, their counts kept
+// modulo 2^32; a superblock table holds the exact 64-bit Occ(A), Occ(C), Occ(G) at
+// every 2^24-character boundary (4 x u64 per entry, the 4th unused).  Counts inside
+// one superblock differ by less than 2^24, so Occ = sup + (u32)(block - (u32)sup).
+#define HSA_SUPER_SHIFT 24u
+
+struct RankDir64 {
+    const uint4 *blk;
+    const uint64_t *sup;
+    uint64_t isa0;
+};
+
+__device__ __forceinline__ void hsa_occ4_q64(const uint4 q, const uint64_t *__restrict__ sup, uint64_t p,
+                                             uint64_t o[4])
+{
+    const uint64_t *s = sup + (p >> HSA_SUPER_SHIFT) * 4u;
+    const uint64_t sa = s[0], sc = s[1], sg = s[2];
+    const uint32_t r = (uint32_t)p & 15u;
+    const uint32_t v = q.w & ((1u << (2u * r)) - 1u);
+    const uint32_t lo = v & 0x55555555u, hi = (v >> 1) & 0x55555555u;
+    const uint32_t n3 = __popc(lo & hi);
+    const uint32_t n1 = __popc(lo) - n3, n2 = __popc(hi) - n3;
+    o[0] = sa + (uint32_t)(q.x - (uint32_t)sa) + (r - n1 - n2 - n3);
+    o[1] = sc + (uint32_t)(q.y - (uint32_t)sc) + n1;
+    o[2] = sg + (uint32_t)(q.z - (uint32_t)sg) + n2;
+    o[3] = p - o[0] - o[1] - o[2];
+}
+
+__device__ __forceinline__ uint64_t hsa_occ1_q64(const uint4 q, const uint64_t *__restrict__ sup, uint64_t p,
+                                                 uint32_t c)
+{
+    uint64_t o[4];
+    hsa_occ4_q64(q, sup, p, o);
+    return c == 0 ? o[0] : c == 1 ? o[1] : c == 2 ? o[2] : o[3];
+}
+
+// The same interface as the 32-bit rank functions (k_search / k_widths are templated
+// on the interval type and call these by overload).
+__device__ __forceinline__ uint32_t occ_pair(const RankDir &d, uint32_t p1, uint32_t p2, uint32_t a[4], uint32_t b[4])
+{
+    return hsa_occ_pair(d, p1, p2, a, b);
+}
+
+__device__ __forceinline__ uint32_t occ1_pair(const RankDir &d, uint32_t p1, uint32_t p2, uint32_t c, uint32_t &a,
+                                              uint32_t &b)
+{
+    return hsa_occ1_pair(d, p1, p2, c, a, b);
+}
+
+__device__ __forceinline__ uint32_t occ_pair(const RankDir64 &d, uint64_t p1, uint64_t p2, uint64_t a[4],
+                                             uint64_t b[4])
+{
+    p1 -= (p1 > d.isa0);
+    p2 -= (p2 > d.isa0);
+    const uint64_t b1 = p1 >> 4, b2 = p2 >> 4;
+    const bool two = b2 != b1;
+    const uint4 q1 = d.blk[b1];
+    uint4 q2r = make_uint4(0, 0, 0, 0);
+    if (two) q2r = d.blk[b2];
+    const uint4 q2 = two ? q2r : q1;
+    hsa_occ4_q64(q1, d.sup, p1, a);
+    hsa_occ4_q64(q2, d.sup, p2, b);
+    return 1u + ((p1 >> 6) != (p2 >> 6));
+}
+
+__device__ __forceinline__ uint32_t occ1_pair(const RankDir64 &d, uint64_t p1, uint64_t p2, uint32_t c, uint64_t &a,
+                                              uint64_t &b)
+{
+    p1 -= (p1 > d.isa0);
+    p2 -= (p2 > d.isa0);
+    const uint64_t b1 = p1 >> 4, b2 = p2 >> 4;
+    const bool two = b2 != b1;
+    const uint4 q1 = d.blk[b1];
+    uint4 q2r = make_uint4(0, 0, 0, 0);
+    if (two) q2r = d.blk[b2];
+    const uint4 q2 = two ? q2r : q1;
+    a = hsa_occ1_q64(q1, d.sup, p1, c);
+    b = hsa_occ1_q64(q2, d.sup, p2, c);
+    return 1u + ((p1 >> 6) != (p2 >> 6));
+}

@@ -126,7 +126,7 @@ struct U4Plus {
 struct WordCounts {
     const uint32_t *code;
     size_t nwords;
-    uint32_t T;
+    uint64_t T;
     __host__ __device__ U4 operator()(size_t b) const
     {
         const uint32_t v = b < nwords ? code[b] : 0u;
@@ -138,7 +138,9 @@ struct WordCounts {
     }
 };
 
-// block b = (Occ A, C, G over [0, 16b) from the scan, code word b)
+// block b = (Occ A, C, G over [0, 16b) from the scan, code word b).  The scan's u32
+// sums wrap past 2^32 characters: the counts are then kept modulo 2^32 and the
+// superblock table (build_super) supplies the high part.
 __global__ void k_block_codes(const uint32_t *__restrict__ code, size_t nwords, size_t nblk, uint4 *__restrict__ blk)
 {
     const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -146,7 +148,7 @@ __global__ void k_block_codes(const uint32_t *__restrict__ code, size_t nwords, 
     blk[b].w = b < nwords ? code[b] : 0u;
 }
 
-static int build_blocks(hsa_index *ix, int dir, uint32_t T, const uint32_t *d_code_lsb, hipStream_t st)
+static int build_blocks(hsa_index *ix, int dir, uint64_t T, const uint32_t *d_code_lsb, hipStream_t st)
 {
     const size_t nwords = ((size_t)T + 15) / 16;
     const size_t nblk = (size_t)T / HSA_BLK_CHARS + 2;
@@ -166,6 +168,59 @@ static int build_blocks(hsa_index *ix, int dir, uint32_t T, const uint32_t *d_co
     HSA_HIP(hipStreamSynchronize(st));
     (void)hipFree(tmp);
     return 0;
+}
+
+// Superblock s (characters [s 2^24, (s+1) 2^24)): its A, C, G counts, one workgroup
+// per superblock; the host turns them into exact u64 prefix counts.
+__global__ void __launch_bounds__(256) k_super_counts(WordCounts wc, uint64_t words_per_sup, unsigned long long *out)
+{
+    __shared__ unsigned long long red[3][256];
+    const uint64_t s = blockIdx.x;
+    unsigned long long a = 0, c = 0, g = 0;
+    for (uint64_t w = s * words_per_sup + threadIdx.x; w < (s + 1) * words_per_sup && w < wc.nwords; w += 256) {
+        const U4 v = wc(w);
+        a += v.a; c += v.b; g += v.c;
+    }
+    red[0][threadIdx.x] = a; red[1][threadIdx.x] = c; red[2][threadIdx.x] = g;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h)
+            for (int j = 0; j < 3; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) out[s * 3 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// sup[s] = exact (Occ A, C, G, 0) at character s 2^24, s = 0 .. T >> 24 (RankDir64)
+static int build_super(hsa_index *ix, int dir, uint64_t T, const uint32_t *d_code_lsb, hipStream_t st)
+{
+    const uint64_t nwords = (T + 15) / 16, wps = (uint64_t)1 << (HSA_SUPER_SHIFT - 4);
+    const size_t nsup = (size_t)(T >> HSA_SUPER_SHIFT) + 2;
+    unsigned long long *d_cnt = nullptr;
+    HSA_HIP(hipMalloc(&d_cnt, nsup * 3 * sizeof(unsigned long long)));
+    HSA_HIP(hipMemsetAsync(d_cnt, 0, nsup * 3 * sizeof(unsigned long long), st));
+    k_super_counts<<<(unsigned)nsup, 256, 0, st>>>(WordCounts{d_code_lsb, (size_t)nwords, T}, wps, d_cnt);
+    HSA_HIP(hipGetLastError());
+    unsigned long long *cnt = (unsigned long long *)malloc(nsup * 3 * sizeof(unsigned long long));
+    uint64_t *sup = (uint64_t *)calloc(nsup * 4, sizeof(uint64_t));
+    if (!cnt || !sup) { free(cnt); free(sup); (void)hipFree(d_cnt); hsa_set_error("host allocation"); return HSA_E_MEM; }
+    HSA_HIP(hipMemcpyAsync(cnt, d_cnt, nsup * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HSA_HIP(hipStreamSynchronize(st));
+    for (size_t s = 1; s < nsup; ++s)
+        for (int j = 0; j < 3; ++j) sup[s * 4 + j] = sup[(s - 1) * 4 + j] + cnt[(s - 1) * 3 + j];
+    int rc = 0;
+    if (hipMalloc(&ix->sup[dir], nsup * 32) != hipSuccess) { hsa_set_error("hipMalloc(sup)"); rc = HSA_E_MEM; }
+    else if (hipMemcpy(ix->sup[dir], sup, nsup * 32, hipMemcpyHostToDevice) != hipSuccess) { hsa_set_error("sup copy"); rc = HSA_E_HIP; }
+    ix->nsup[dir] = nsup;
+    free(cnt); free(sup); (void)hipFree(d_cnt);
+    return rc;
+}
+
+int hsa_need32(const hsa_index *ix)
+{
+    if (!ix->is64) return 0;
+    hsa_set_error("the index text has 2^32 characters or more: use the 64-bit entry points (*64)");
+    return HSA_E_ARG;
 }
 
 static int index_init(int device, hsa_index **out)
@@ -210,6 +265,36 @@ extern "C" int hsa_index_create_device(int device, uint32_t T, uint32_t isa0, co
     return 0;
 }
 
+extern "C" int hsa_index_create_device64(int device, uint64_t T, uint64_t isa0, const uint64_t C[5],
+                                         const uint32_t *d_code_lsb, uint64_t rT, uint64_t risa0, const uint64_t rC[5],
+                                         const uint32_t *d_rcode_lsb, hsa_index_t **out)
+{
+    if (!C || !rC || !d_code_lsb || !d_rcode_lsb || !out) { hsa_set_error("null argument"); return HSA_E_ARG; }
+    if (T == 0 || rT == 0 || C[4] != T || rC[4] != rT || isa0 > T || risa0 > rT) {
+        hsa_set_error("inconsistent lengths (C[4] must equal T, isa0 <= T)");
+        return HSA_E_ARG;
+    }
+    if ((T >> 4) + 2 >= (1ull << 40)) { hsa_set_error("text too long"); return HSA_E_ARG; }
+    hsa_index *ix = nullptr;
+    int rc = index_init(device, &ix);
+    if (rc) return rc;
+    ix->has_sup = true;
+    ix->is64 = T > 0xFFFFFFFFull - 1 || rT > 0xFFFFFFFFull - 1;
+    ix->T64 = T; ix->isa0_64 = isa0; memcpy(ix->C64, C, sizeof ix->C64);
+    ix->rT64 = rT; ix->risa0_64 = risa0; memcpy(ix->rC64, rC, sizeof ix->rC64);
+    if (!ix->is64) {       // the 32-bit entry points serve the same index
+        ix->T = (uint32_t)T; ix->isa0 = (uint32_t)isa0; ix->rT = (uint32_t)rT; ix->risa0 = (uint32_t)risa0;
+        for (int c = 0; c < 5; ++c) { ix->C[c] = (uint32_t)C[c]; ix->rC[c] = (uint32_t)rC[c]; }
+    }
+    if ((rc = build_blocks(ix, 0, T, d_code_lsb, ix->stream)) || (rc = build_blocks(ix, 1, rT, d_rcode_lsb, ix->stream)) ||
+        (rc = build_super(ix, 0, T, d_code_lsb, ix->stream)) || (rc = build_super(ix, 1, rT, d_rcode_lsb, ix->stream))) {
+        hsa_index_free(ix);
+        return rc;
+    }
+    *out = ix;
+    return 0;
+}
+
 extern "C" int hsa_index_create(int device, uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code,
                                 uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *rcode,
                                 hsa_index_t **out)
@@ -239,6 +324,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (!ix) return;
     (void)hipSetDevice(ix->device);
     (void)hipFree(ix->blk[0]); (void)hipFree(ix->blk[1]);
+    (void)hipFree(ix->sup[0]); (void)hipFree(ix->sup[1]);
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big); hsa_scratch_free(ix->huge);
     if (ix->d_ovf2) (void)hipFree(ix->d_ovf2);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed);
@@ -253,7 +339,11 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     delete ix;
 }
 
-extern "C" size_t hsa_index_bytes(const hsa_index_t *ix) { return (ix->nblk[0] + ix->nblk[1]) * 16; }
+extern "C" size_t hsa_index_bytes(const hsa_index_t *ix)
+{
+    return (ix->nblk[0] + ix->nblk[1]) * 16 + (ix->nsup[0] + ix->nsup[1]) * 32;
+}
+extern "C" int hsa_index_is64(const hsa_index_t *ix) { return ix->is64 ? 1 : 0; }
 extern "C" int hsa_index_device(const hsa_index_t *ix) { return ix->device; }
 extern "C" void *hsa_index_stream(const hsa_index_t *ix) { return (void *)ix->stream; }
 
@@ -267,9 +357,40 @@ __global__ void k_occ4(RankDir d, const uint32_t *pos, size_t n, uint32_t *out)
     out[4 * i] = o[0]; out[4 * i + 1] = o[1]; out[4 * i + 2] = o[2]; out[4 * i + 3] = o[3];
 }
 
+__global__ void k_occ4_64(RankDir64 d, const uint64_t *pos, size_t n, uint64_t *out)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t a[4], b[4];
+    occ_pair(d, pos[i], pos[i], a, b);
+    out[4 * i] = a[0]; out[4 * i + 1] = a[1]; out[4 * i + 2] = a[2]; out[4 * i + 3] = a[3];
+}
+
+extern "C" int hsa_occ4_batch64(hsa_index_t *ix, int dir, size_t n, const uint64_t *pos, uint64_t *occ)
+{
+    if (dir < 0 || dir > 1) { hsa_set_error("dir"); return HSA_E_ARG; }
+    if (!ix->has_sup) { hsa_set_error("not a 64-bit index (hsa_index_create_device64)"); return HSA_E_ARG; }
+    const uint64_t T = dir ? ix->rT64 : ix->T64;
+    for (size_t i = 0; i < n; ++i)
+        if (pos[i] > T + 1) { hsa_set_error("position %llu > T + 1", (unsigned long long)pos[i]); return HSA_E_ARG; }
+    HSA_HIP(hipSetDevice(ix->device));
+    ix->staged_valid = 0;
+    int rc;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, n * 8 + 16)) || (rc = hsa_grow(&ix->d_out, &ix->d_out_cap, n * 32 + 16)))
+        return rc;
+    HSA_HIP(hipMemcpyAsync(ix->d_in, pos, n * 8, hipMemcpyHostToDevice, ix->stream));
+    RankDir64 d{ix->blk[dir], ix->sup[dir], dir ? ix->risa0_64 : ix->isa0_64};
+    if (n) k_occ4_64<<<(unsigned)((n + 255) / 256), 256, 0, ix->stream>>>(d, (const uint64_t *)ix->d_in, n, (uint64_t *)ix->d_out);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipMemcpyAsync(occ, ix->d_out, n * 32, hipMemcpyDeviceToHost, ix->stream));
+    HSA_HIP(hipStreamSynchronize(ix->stream));
+    return 0;
+}
+
 extern "C" int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t *pos, uint32_t *occ)
 {
     if (dir < 0 || dir > 1) { hsa_set_error("dir"); return HSA_E_ARG; }
+    if (int rc0 = hsa_need32(ix)) return rc0;
     HSA_HIP(hipSetDevice(ix->device));
     ix->staged_valid = 0;                      // d_in is reused below
     int rc;
@@ -305,6 +426,7 @@ __global__ void k_step(RankDir d, const uint32_t *C, const uint32_t *in, size_t 
 
 extern "C" int hsa_step_batch(hsa_index_t *ix, size_t n, const uint32_t *klrr, uint32_t *out16)
 {
+    if (int rc0 = hsa_need32(ix)) return rc0;
     HSA_HIP(hipSetDevice(ix->device));
     ix->staged_valid = 0;                      // d_in is reused below
     int rc;
@@ -351,6 +473,7 @@ __global__ void k_width(RankDir rev, uint32_t T, const uint32_t *C, const uint64
 extern "C" int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
                                const uint8_t *codes, size_t codes_len, uint32_t *width_out)
 {
+    if (int rc0 = hsa_need32(ix)) return rc0;
     HSA_HIP(hipSetDevice(ix->device));
     ix->staged_valid = 0;                      // d_in is reused below
     uint64_t *woff = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));

@@ -35,6 +35,14 @@ struct hsa_index {
     uint32_t rT = 0, risa0 = 0, rC[5] = {0, 0, 0, 0, 0};
     uint4 *blk[2] = {nullptr, nullptr};
     size_t nblk[2] = {0, 0};
+    // 64-bit interval index (hsa_index_create_device64): exact lengths / counts and the
+    // superblock tables of RankDir64 (hsa_device.h).  is64: a text of 2^32 characters
+    // or more, which only the *64 entry points accept.
+    bool has_sup = false, is64 = false;
+    uint64_t T64 = 0, isa0_64 = 0, C64[5] = {0, 0, 0, 0, 0};
+    uint64_t rT64 = 0, risa0_64 = 0, rC64[5] = {0, 0, 0, 0, 0};
+    uint64_t *sup[2] = {nullptr, nullptr};
+    size_t nsup[2] = {0, 0};
     hipStream_t stream = nullptr;
     int n_cu = 0;
     SearchScratch main, big, huge;
@@ -67,6 +75,8 @@ struct hsa_index {
 int hsa_grow(void **p, size_t *cap, size_t need);
 int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap, size_t link_bytes = 2);
 void hsa_scratch_free(SearchScratch &s);
+// HSA_E_ARG unless the index fits the 32-bit entry points (bwtint_t, 2BWT-Interface.h:26)
+int hsa_need32(const hsa_index *ix);
 
 // Knobs (hsa_configure).
 extern int g_waves_per_cu;

@@ -79,6 +79,7 @@ extern "C" int hsa_index_set_sa(hsa_index_t *ix, const uint32_t *sa_values, uint
         hsa_set_error("hsa_index_set_sa: bad arguments");
         return HSA_E_ARG;
     }
+    if (int rc0 = hsa_need32(ix)) return rc0;
     if (n_values < ((uint64_t)ix->T + interval) / interval) {
         hsa_set_error("hsa_index_set_sa: %llu values < (T + s) / s", (unsigned long long)n_values);
         return HSA_E_ARG;

@@ -1,0 +1,1468 @@
+#pragma once
+// hsa_search_kernels.h -- the bwa_cal_sa_reg_gap per-read loop as two persistent kernels
+// (templated on the interval type: 32-bit, the reference's bwtint_t, and 64-bit for
+// texts of 2^32 characters or more), and the host helpers that plan and launch them.
+// Included by hsa_search.hip (32-bit API) and hsa_search64.hip (64-bit API).
+//
+// k_widths: bwt_cal_width (bwtaln.c:73-98) for every (read, strand) of the batch --
+//   the seed width and the whole-read width of the rc and the fwd strand, one work
+//   item per lane, pulled from a global queue.  All lanes run the same short step
+//   (one single-character rank pair on the reverse BWT), so the waves stay
+//   converged.  Output: per (read, strand) a row of pruning bytes
+//   min(bid,127) | (w[p] == w[p+1]) << 7 for the read and for the seed, and the
+//   full w values (only gap_shadow reads them).
+// k_search: per read, rc strand then fwd strand (bwtaln.c:343-359): copy the
+//   strand's pruning bytes into LDS and run bwt_match_gap (bwtgap.c:118-331); the
+//   first strand with hits wins; no hit on either -> HSA_F_FALLBACK (splice).
+//
+// One lane owns one read at a time (reads are pulled from a global queue with a
+// wave-aggregated atomic, so a lane that finishes a cheap read immediately takes
+// the next one: work-stealing at read granularity).  Every loop iteration of
+// k_search performs at most ONE bidirectional rank step per lane (two Occ queries
+// on the forward BWT, usually one 64-byte block), whatever the lane is doing --
+// exact tail (bwt_match_exact) or expansion -- so all lanes issue their HBM loads
+// together and the state machine in between is register/LDS work.  Control that
+// needs no rank (pruned pops, hits) loops without touching the BWT.
+//
+// Per-lane state in LDS (160 KiB per CU): the pruning bytes of the current strand
+// (everything bwt_match_gap's pruning reads: bwtgap.c:170, :256-263) and the
+// stack's bucket heads.  Buckets are the REACHABLE scores only (a score table per
+// regime maps aln_score -> dense bucket, order preserved), so `-n 4 -o 0` needs 6
+// heads instead of the reference's 54 (bwtgap.c:18).  Stack entries (16 bytes + a
+// 16-bit link) live in a per-lane pool in HBM; a bit mask in registers gives the
+// lowest non-empty bucket (== gap_stack_t.best).  The child pushed LAST by an
+// expansion is always the next pop when its bucket is the lowest, so it stays in
+// registers ("virtual top").  A regime set without gap opens (max_gapo == 0: every
+// entry stays in state M) runs a specialisation without the indel code.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <type_traits>
+
+#include "hsa_device.h"
+#include "hsa_internal.h"
+
+#define MODE_GAPE 0x01
+#define MODE_LOGGAP 0x04
+#define MODE_NONSTOP 0x10
+#define ST_M 0
+#define ST_I 1
+#define ST_D 2
+#define NIL16 0xFFFFu
+#define BLOCK 256
+#define MAXB 128          // dense buckets per regime (BMask<2>)
+#define MAXS 512          // score table length per regime (n_stacks <= MAXS)
+#ifndef HSA_CTL_LOOP
+#define HSA_CTL_LOOP 0    // 1: loop the control code until every lane needs a rank step
+#endif
+
+enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END };
+
+struct SearchArgs {
+    RankDir fwd, rev;
+    uint32_t T;
+    uint32_t C[5];
+    // 64-bit texts (IT = uint64_t kernels): the same, with superblock tables
+    RankDir64 fwd64, rev64;
+    uint64_t T64;
+    uint64_t C64[5];
+    const hsa_regime_t *regimes;
+    const uint8_t *bmap;           // [2][MAXS]: aln_score -> dense bucket (0xFF: unreachable)
+    uint32_t ntab;                 // score table entries per regime kept in LDS (>= every n_stacks, multiple of 8)
+    const hsa_job_t *jobs;
+    const int32_t *job_list;       // optional indirection (re-runs); null = identity
+    int n_jobs;
+    const uint8_t *codes;
+    int32_t *n_aln;
+    uint32_t *flags;
+    uint64_t *hit_off;
+    uint32_t *hits;
+    uint64_t hit_cap;
+    unsigned long long *ctr;       // [0] queue head [1] hit alloc [2] rank queries [3] blocks [4] pops [5] errors
+                                   // [6] width item queue head
+    const uint8_t *wb, *ws;        // width rows of k_widths (row = list position * 2 + strand),
+    uint32_t *wg;                  //   64 rows interleaved; wg: full w values (gap_shadow only)
+    uint32_t rb, rs, rg;           //   row capacities: bytes, bytes, words
+    uint4 *pool;
+    void *nxt;                     // pool links: uint16_t, or uint32_t in the huge pass
+    uint32_t *hbuf;
+    uint32_t pcap, hcap, nb;
+    uint32_t off_heads, off_wb, off_ws;   // LDS byte offsets
+    uint32_t mm_buckets;           // 1: the bucket of every score is its n_mm (no gap opens, s_mm > 0)
+    // device-side overflow re-run: the main pass appends reads that exceeded their
+    // lane's capacity to ovf_list (count in ctr[8]); the re-run pass takes its read
+    // count from n_dev and its queue head from ctr[qctr]
+    int32_t *ovf_list;
+    const unsigned long long *n_dev;
+    uint32_t qctr;
+    uint32_t ovf_ctr;              // counter that numbers this pass's ovf_list entries
+    // caller-width mode (hsa_match_gap_batch, bwt_match_gap called directly): per job
+    // strand and width_seed kind; k_widths_import builds the rows from the caller's
+    // bwt_width_t pairs (cw), the search takes that one strand, and gap_shadow keeps
+    // the full bid values (wbid) so the mutated widths can be handed back
+    const hsa_mg_job_t *mg;
+    int32_t *cw;
+    int32_t *wbid;
+    uint32_t *wq;                  // k_widths: rank queries of each forward-strand width row
+    uint32_t batch_k;              // rare-event batching threshold (see (A) in k_search)
+};
+
+// entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
+__device__ __forceinline__ uint32_t meta_pack(uint32_t i, uint32_t st, uint32_t isd, uint32_t mm, uint32_t go,
+                                              uint32_t ge)
+{
+    return i | st << 10 | isd << 12 | mm << 13 | go << 20 | ge << 24;
+}
+#define M_I(m) ((int)((m) & 1023u))
+#define M_ST(m) ((int)(((m) >> 10) & 3u))
+#define M_ISD(m) ((int)(((m) >> 12) & 1u))
+#define M_MM(m) ((int)(((m) >> 13) & 127u))
+#define M_GO(m) ((int)(((m) >> 20) & 15u))
+#define M_GE(m) ((int)((m) >> 24))
+
+// control word: ph:3 | strand:1 | has_seed:1 | reg:1 | has_vt:1 | seed_alias:1 | ovf:2 | len:10 | seed_len:10
+#define C_PH(c) ((c) & 7u)
+#define C_STRAND(c) (((c) >> 3) & 1u)
+#define C_SEED(c) (((c) >> 4) & 1u)
+#define C_REG(c) (((c) >> 5) & 1u)
+#define C_VT(c) (((c) >> 6) & 1u)
+#define C_ALIAS(c) (((c) >> 7) & 1u)
+#define C_OVF(c) (((c) >> 8) & 3u)
+#define C_LEN(c) ((int)(((c) >> 10) & 1023u))
+#define C_SLEN(c) ((int)(((c) >> 20) & 1023u))
+#define SET_PH(c, p) ((c) = ((c) & ~7u) | (p))
+
+// v[c] for a runtime c in 0..3 as selects: a dynamically indexed register array
+// would be lowered through the private segment (scratch) of the dispatch.
+template <typename V>
+__device__ __forceinline__ V pick4(const V v[4], uint32_t c)
+{
+    return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3];
+}
+
+// The interval type of a kernel instantiation: uint32_t (the reference's bwtint_t,
+// 2BWT-Interface.h:26) or uint64_t (texts of 2^32 characters or more).
+template <typename IT> struct Ix;
+template <> struct Ix<uint32_t> {
+    __device__ static const RankDir &fwd(const SearchArgs &a) { return a.fwd; }
+    __device__ static const RankDir &rev(const SearchArgs &a) { return a.rev; }
+    __device__ static uint32_t T(const SearchArgs &a) { return a.T; }
+    __device__ static const uint32_t *C(const SearchArgs &a) { return a.C; }
+};
+template <> struct Ix<uint64_t> {
+    __device__ static const RankDir64 &fwd(const SearchArgs &a) { return a.fwd64; }
+    __device__ static const RankDir64 &rev(const SearchArgs &a) { return a.rev64; }
+    __device__ static uint64_t T(const SearchArgs &a) { return a.T64; }
+    __device__ static const uint64_t *C(const SearchArgs &a) { return a.C64; }
+};
+
+// A stack entry (gap_entry_t, bwtaln.h:52-58): k, l, rev_k and the meta word
+// (rev_l = rev_k + (l - k)).  32-bit: one uint4 in the pool; 64-bit: two.
+template <typename IT> struct Ent {
+    IT x, y, z;
+    uint32_t w;
+};
+template <typename IT>
+__device__ __forceinline__ Ent<IT> ent_load(const uint4 *pool, size_t idx, int lane)
+{
+    if constexpr (sizeof(IT) == 4) {
+        const uint4 v = pool[idx * 64 + lane];
+        return Ent<IT>{v.x, v.y, v.z, v.w};
+    } else {
+        const uint4 u = pool[(2 * idx) * 64 + lane], v = pool[(2 * idx + 1) * 64 + lane];
+        return Ent<IT>{(uint64_t)u.x | (uint64_t)u.y << 32, (uint64_t)u.z | (uint64_t)u.w << 32,
+                       (uint64_t)v.x | (uint64_t)v.y << 32, v.z};
+    }
+}
+template <typename IT>
+__device__ __forceinline__ void ent_store(uint4 *pool, size_t idx, int lane, const Ent<IT> &e)
+{
+    if constexpr (sizeof(IT) == 4) {
+        pool[idx * 64 + lane] = make_uint4(e.x, e.y, e.z, e.w);
+    } else {
+        pool[(2 * idx) * 64 + lane] = make_uint4((uint32_t)e.x, (uint32_t)(e.x >> 32), (uint32_t)e.y, (uint32_t)(e.y >> 32));
+        pool[(2 * idx + 1) * 64 + lane] = make_uint4((uint32_t)e.z, (uint32_t)(e.z >> 32), e.w, 0u);
+    }
+}
+// staged words per hit (HB) and words per output hit record: bwt_aln1_t (bwtaln.h:41-50)
+// for 32-bit intervals; hsa_aln64_t (include/hsa_gpu.h) for 64-bit ones
+template <typename IT> struct HitW { static constexpr uint32_t STAGE = sizeof(IT) == 4 ? 9u : 10u;
+                                     static constexpr uint32_t OUT = sizeof(IT) == 4 ? 9u : 14u; };
+
+__device__ __forceinline__ int int_log2(uint32_t v)   // bwtgap.c:107-116
+{
+    int c = 0;
+    if (v & 0xffff0000u) { v >>= 16; c |= 16; }
+    if (v & 0xff00) { v >>= 8; c |= 8; }
+    if (v & 0xf0) { v >>= 4; c |= 4; }
+    if (v & 0xc) { v >>= 2; c |= 2; }
+    if (v & 0x2) c |= 1;
+    return c;
+}
+
+template <int MW> struct BMask;
+template <> struct BMask<0> {        // <= 32 buckets: one 32-bit word
+    uint32_t m0 = 0;
+    __device__ __forceinline__ void clear() { m0 = 0; }
+    __device__ __forceinline__ bool any() const { return m0 != 0; }
+    __device__ __forceinline__ int lowest() const { return m0 ? __ffs(m0) - 1 : (1 << 30); }
+    __device__ __forceinline__ bool test(int b) const { return (m0 >> b) & 1u; }
+    __device__ __forceinline__ void set(int b) { m0 |= 1u << b; }
+    __device__ __forceinline__ void reset(int b) { m0 &= ~(1u << b); }
+};
+template <> struct BMask<1> {
+    uint64_t m0 = 0;
+    __device__ __forceinline__ void clear() { m0 = 0; }
+    __device__ __forceinline__ bool any() const { return m0 != 0; }
+    __device__ __forceinline__ int lowest() const { return m0 ? __ffsll((unsigned long long)m0) - 1 : (1 << 30); }
+    __device__ __forceinline__ bool test(int b) const { return (m0 >> b) & 1ull; }
+    __device__ __forceinline__ void set(int b) { m0 |= 1ull << b; }
+    __device__ __forceinline__ void reset(int b) { m0 &= ~(1ull << b); }
+};
+template <> struct BMask<2> {
+    uint64_t m0 = 0, m1 = 0;
+    __device__ __forceinline__ void clear() { m0 = m1 = 0; }
+    __device__ __forceinline__ bool any() const { return (m0 | m1) != 0; }
+    __device__ __forceinline__ int lowest() const
+    {
+        if (m0) return __ffsll((unsigned long long)m0) - 1;
+        if (m1) return 64 + __ffsll((unsigned long long)m1) - 1;
+        return 1 << 30;
+    }
+    __device__ __forceinline__ bool test(int b) const { return b < 64 ? ((m0 >> b) & 1ull) : ((m1 >> (b - 64)) & 1ull); }
+    __device__ __forceinline__ void set(int b) { if (b < 64) m0 |= 1ull << b; else m1 |= 1ull << (b - 64); }
+    __device__ __forceinline__ void reset(int b) { if (b < 64) m0 &= ~(1ull << b); else m1 &= ~(1ull << (b - 64)); }
+};
+
+// Pruning element of one read position, as k_widths writes it and k_search keeps it
+// in LDS: min(bid, BIDM) | (w[p] == w[p+1]) << BIDB | (code & 3) << CSH |
+// (code > 3) << (CSH + 2), code being the strand sequence's base at p.  A bid is
+// only ever compared with m, m - 1 or m_seed - 1 (bwtgap.c:170, :256-263), all
+// <= max(max_diff, max_seed_diff), so capping it at BIDM is exact while that bound
+// is < BIDM: 8-bit elements (4-bit bid) for bounds <= 14, else 16-bit (8-bit bid).
+// The base code keeps exactly what bwt_match_gap derives from it: c > 3 (N) and
+// (c + j) & 3 (bwtgap.c:305-306).
+template <typename WT> struct WFmt {
+    static constexpr uint32_t BIDB = sizeof(WT) == 1 ? 4u : 8u;
+    static constexpr uint32_t BIDM = (1u << BIDB) - 1u;
+    static constexpr uint32_t EQ = 1u << BIDB;
+    static constexpr uint32_t CSH = BIDB + 1u;
+    static constexpr uint32_t EB = 8u * sizeof(WT);           // bits per element
+    static constexpr uint32_t EPW = 4u / sizeof(WT);          // elements per u32
+    __device__ static uint32_t code_bits(uint32_t c) { return (c & 3u) << CSH | (c > 3 ? 4u : 0u) << CSH; }
+    __device__ static uint32_t code(uint32_t v) { return (v >> CSH) & 7u; }   // 0..3, or 4..7 for N
+};
+
+#ifdef HSA_DIAG
+// Diagnostic build only (-DHSA_DIAG, never the product library): per-workgroup
+// start/end s_memtime and s_memrealtime of the last launch, for the in-kernel
+// clock and the workgroup-duration spread.
+static __device__ unsigned long long g_diag[8192 * 4];
+// event counters: 0 width steps, 1 exact steps, 2 expand steps, 3 virtual-top pops,
+// 4 pool pops, 5 outer iterations (per wave), 6 lanes stepping summed over outer
+// iterations, 7 control-loop iterations (per wave), 8 entries flushed to the pool,
+// 9..12 shader cycles per wave in acquisition / control / rank-load wait / apply,
+// 13 gap_shadow calls with last_diff_pos > 0, 14 their summed last_diff_pos,
+// 15 strand starts, 16/17 exact/expand steps on a unique interval (l == k), 18/19
+// width steps on a unique interval / all width steps
+static __device__ unsigned long long g_dctr[32];
+#define DC(i) (++dc[i])
+#else
+#define DC(i) ((void)0)
+#endif
+
+// ---------------------------------------------------------------- k_widths
+// bwt_cal_width type 1 (bwtaln.c:84-97) of every (read, strand): the whole read
+// (width_back) and its last seed_len bases (width_seed, bwtaln.c:344-348).  The
+// strand-1 sequence is the reverse complement (seq_reverse(.., 1), bwtaln.c:337).
+// Forward extension on the reverse BWT with the forward C table
+// (BWTSARangeForeward, 2BWT-Interface.c:121-131).
+//
+// One lane per (read, strand) row, rows in order, so a wave's 64 rows are stored
+// interleaved -- element e of row R at (R / 64 * cap + e) * 64 + R % 64 -- and every
+// store of a step is one coalesced 256-byte wave store.  The two chains of a row
+// (read and seed) are independent, so each iteration advances both: two rank pairs
+// in flight per lane.  All reads of a batch have similar lengths, so the lanes stay
+// converged without a work queue.
+template <typename IT> struct WChain {
+    IT k, l;
+    uint32_t bid;
+    IT prevw;
+    uint32_t acc;
+};
+
+template <typename WT, typename IT>
+__device__ __forceinline__ void width_step(const SearchArgs &a, WChain<IT> &ch, uint32_t t, uint32_t n, uint32_t c,
+                                           uint32_t cbits, uint32_t *__restrict__ brow, IT *__restrict__ wrow,
+                                           uint32_t &st_q, uint32_t &st_b)
+{
+    using F = WFmt<WT>;
+    IT w;
+    if (t < n) {
+        if (c < 4) {
+            IT ok, ol;
+            st_b += occ1_pair(Ix<IT>::rev(a), ch.k, ch.l + 1u, c, ok, ol);
+            st_q += 2;
+            const IT cc = pick4(Ix<IT>::C(a), c);
+            ch.k = cc + ok + 1u;
+            ch.l = cc + ol;
+        }
+        if (ch.k > ch.l || c > 3) { ch.k = 0; ch.l = Ix<IT>::T(a); ++ch.bid; }
+        w = ch.l - ch.k + 1u;
+    } else {
+        w = 0; ++ch.bid;                                         // width[len] = {0, ++bid}
+    }
+    // element t-1 is final now (its eq bit needs w[t]); elements go out a word at a time
+    if (t > 0) {
+        if (ch.prevw == w) ch.acc |= F::EQ << (((t - 1) % F::EPW) * F::EB);
+        if ((t - 1) % F::EPW == F::EPW - 1) { brow[((t - 1) / F::EPW) * 64] = ch.acc; ch.acc = 0; }
+    }
+    ch.acc |= ((ch.bid < F::BIDM ? ch.bid : F::BIDM) | cbits) << ((t % F::EPW) * F::EB);
+    if (wrow) wrow[t * 64] = w;
+    ch.prevw = w;
+    if (t == n) brow[(t / F::EPW) * 64] = ch.acc;
+}
+
+template <typename WT, typename IT = uint32_t>
+__global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
+{
+    using F = WFmt<WT>;
+    const uint32_t R = blockIdx.x * BLOCK + threadIdx.x;     // row = list position * 2 + strand
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    if (R >= 2u * n_jobs) return;
+    const uint32_t q = R >> 1, strand = R & 1u;
+    const hsa_job_t J = a.jobs[a.job_list ? a.job_list[q] : (int)q];
+    const uint32_t len = J.len;
+    const uint64_t off = J.off;
+    const bool has_seed = (int)len > J.seed_len;
+    const uint32_t slen = has_seed ? (uint32_t)J.seed_len : 0u;
+    const size_t rb = R >> 6, rl = R & 63u;
+    uint32_t *const brow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.wb)) + rb * (a.rb / 4) * 64 + rl;
+    uint32_t *const srow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.ws)) + rb * (a.rs / 4) * 64 + rl;
+    IT *const wrow = reinterpret_cast<IT *>(a.wg) + rb * a.rg * 64 + rl;
+    WChain<IT> f{0, Ix<IT>::T(a), 0, 0, 0}, sd{0, Ix<IT>::T(a), 0, 0, 0};
+    uint32_t st_q = 0, st_b = 0;
+#ifdef HSA_DIAG
+    uint32_t du = 0, dw = 0;
+#endif
+    const uint32_t s0 = len - slen;
+    auto base = [&](uint32_t sp) -> uint32_t {
+        const uint32_t c = a.codes[off + (strand ? len - 1u - sp : sp)];
+        return strand && c < 4 ? 3u - c : c;
+    };
+    for (uint32_t t = 0; t <= len; ++t) {
+#ifdef HSA_DIAG
+        if (t < len) { ++dw; du += f.k == f.l; }
+        if (has_seed && t < slen) { ++dw; du += sd.k == sd.l; }
+#endif
+        const uint32_t cf = t < len ? base(t) : 4u;
+        // the read's elements also carry the strand sequence's base (k_search's getc)
+        width_step<WT, IT>(a, f, t, len, cf, t < len ? F::code_bits(cf) : 0u, brow, wrow, st_q, st_b);
+        if (has_seed && t <= slen) {
+            const uint32_t cs = t < slen ? base(s0 + t) : 4u;
+            width_step<WT, IT>(a, sd, t, slen, cs, 0u, srow, nullptr, st_q, st_b);
+        }
+    }
+    // rank queries: the reverse-complement strand is always searched (bwtaln.c:343);
+    // the forward strand's widths are computed speculatively and count as the
+    // reference's work only when k_search searches that strand (ctr[13]: all of them)
+    if (strand) {
+        atomicAdd(&a.ctr[2], (unsigned long long)st_q);
+        atomicAdd(&a.ctr[7], (unsigned long long)st_q);
+    } else {
+        a.wq[q] = st_q;
+        atomicAdd(&a.ctr[13], (unsigned long long)st_q);
+    }
+    atomicAdd(&a.ctr[3], (unsigned long long)st_b);
+#ifdef HSA_DIAG
+    atomicAdd(&g_dctr[18], (unsigned long long)du);
+    atomicAdd(&g_dctr[19], (unsigned long long)dw);
+#endif
+}
+
+// Caller-width mode: the width rows of each call from the caller's bwt_width_t pairs
+// (hsa_match_gap_batch) -- the same element format and row layout k_widths writes;
+// the row of list position q is q * 2 + strand.  Besides the pruning elements and the
+// full w values, the full bids go to wbid: gap_shadow rewrites them (bwtgap.c:101).
+template <typename WT>
+__global__ void __launch_bounds__(BLOCK) k_widths_import(SearchArgs a)
+{
+    using F = WFmt<WT>;
+    const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    if (q >= n_jobs) return;
+    const int job = a.job_list ? a.job_list[q] : (int)q;
+    const hsa_job_t J = a.jobs[job];
+    const hsa_mg_job_t M = a.mg[job];
+    const uint32_t R = q * 2u + (uint32_t)(M.strand & 1);
+    const size_t rb = R >> 6, rl = R & 63u;
+    uint32_t *const brow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.wb)) + rb * (a.rb / 4) * 64 + rl;
+    uint32_t *const srow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.ws)) + rb * (a.rs / 4) * 64 + rl;
+    uint32_t *const wrow = a.wg + rb * a.rg * 64 + rl;
+    int32_t *const drow = a.wbid + rb * a.rg * 64 + rl;
+    // elements 0..n of one row; element t: min(bid, BIDM) | (w[t] == w[t+1]) | base code
+    auto emit = [&](uint32_t *row, const int32_t *w, uint32_t n, bool read_row) {
+        uint32_t acc = 0;
+        uint32_t wt = (uint32_t)w[0];
+        for (uint32_t t = 0; t <= n; ++t) {
+            const uint32_t bid = (uint32_t)w[2 * t + 1];
+            const uint32_t wn = t < n ? (uint32_t)w[2 * t + 2] : 0u;
+            uint32_t e = bid < F::BIDM ? bid : F::BIDM;
+            if (t < n && wt == wn) e |= F::EQ;
+            if (read_row && t < n) e |= F::code_bits(a.codes[J.off + t]);
+            acc |= e << ((t % F::EPW) * F::EB);
+            if (t % F::EPW == F::EPW - 1 || t == n) { row[(t / F::EPW) * 64] = acc; acc = 0; }
+            if (read_row) { wrow[t * 64] = wt; drow[t * 64] = (int32_t)bid; }
+            wt = wn;
+        }
+    };
+    emit(brow, a.cw + 2 * M.wb_off, J.len, true);
+    if (M.seed == HSA_SEED_OWN) emit(srow, a.cw + 2 * M.ws_off, (uint32_t)J.seed_len, false);
+}
+
+// Caller-width mode: width_back after the search (gap_shadow rewrote it in the rows)
+// back into the caller's pairs.  Reads that overflowed this pass are skipped: the
+// re-run that completes them exports them.
+static __global__ void __launch_bounds__(BLOCK) k_widths_export(SearchArgs a)
+{
+    const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    if (q >= n_jobs) return;
+    const int job = a.job_list ? a.job_list[q] : (int)q;
+    if (a.flags[job] & HSA_F_OVERFLOW) return;
+    const hsa_job_t J = a.jobs[job];
+    const hsa_mg_job_t M = a.mg[job];
+    const uint32_t R = q * 2u + (uint32_t)(M.strand & 1);
+    const size_t base = (R >> 6) * (size_t)a.rg * 64 + (R & 63u);
+    int32_t *const o = a.cw + 2 * M.wb_off;
+    for (uint32_t t = 0; t <= J.len; ++t) {
+        o[2 * t] = (int32_t)a.wg[base + t * 64];
+        o[2 * t + 1] = a.wbid[base + t * 64];
+    }
+}
+
+
+// NT = lanes per workgroup: 256, or 64 when per-lane LDS (many buckets, long reads)
+// would leave fewer than 16 waves per CU in 256-lane workgroups (plan_launch)
+// HUGE: the last capacity pass (reads that overflowed the big pass): 32-bit pool
+// links and popped slots reused through a free list, so a lane's pool holds any
+// stack the reference can build (n_entries <= max_entries + 9, bwtgap.c:150-151).
+template <int MW, bool GAPS, typename WT, int NT, bool HUGE = false, typename IT = uint32_t>
+__global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
+{
+    using F = WFmt<WT>;
+    using E = Ent<IT>;
+    using CT = typename std::conditional<sizeof(IT) == 8, int64_t, int>::type;   // best_cnt (int in bwtgap.c:127)
+    constexpr uint32_t HW = HitW<IT>::STAGE, OW = HitW<IT>::OUT;
+    const IT TT = Ix<IT>::T(a);
+    const IT *const CC = Ix<IT>::C(a);
+    using LT = typename std::conditional<HUGE, uint32_t, uint16_t>::type;   // pool link
+    constexpr uint32_t NIL = HUGE ? 0xFFFFFFFFu : (uint32_t)NIL16;
+#ifdef HSA_DIAG
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {
+        g_diag[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memtime();
+        g_diag[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+    extern __shared__ __align__(16) uint8_t s_lds[];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gid = blockIdx.x * NT + tid;
+    const int lane = (int)(tid & 63);
+    // the two regimes' score tables (ntab entries each), then the two regimes
+    for (uint32_t t = tid; t < 2 * a.ntab; t += NT) s_lds[t] = a.bmap[(t / a.ntab) * MAXS + t % a.ntab];
+    static_assert(2 * sizeof(hsa_regime_t) <= 128, "regime LDS slot");
+    hsa_regime_t *const s_reg = reinterpret_cast<hsa_regime_t *>(s_lds + 2 * a.ntab);
+    if (tid < 2 * sizeof(hsa_regime_t) / 4)
+        reinterpret_cast<uint32_t *>(s_reg)[tid] = reinterpret_cast<const uint32_t *>(a.regimes)[tid];
+    __syncthreads();
+    LT *const s_heads = reinterpret_cast<LT *>(s_lds + a.off_heads);
+    WT *const s_wb = reinterpret_cast<WT *>(s_lds + a.off_wb);
+    WT *const s_ws = reinterpret_cast<WT *>(s_lds + a.off_ws);
+    // per-lane HBM scratch, wave-interleaved: element e of lane l of wave w at
+    // (w * cap + e) * 64 + l, so one wave's accesses stay inside one small region
+    // (few pages) and lanes at equal e coalesce
+    const size_t wv = gid >> 6;
+#define NXT(s) reinterpret_cast<LT *>(a.nxt)[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
+#define HB(i) a.hbuf[(wv * a.hcap * HW + (uint32_t)(i)) * 64 + lane]
+#define HEAD(b) s_heads[(uint32_t)(b) * NT + tid]
+    // pruning elements in LDS, word-interleaved: the word holding elements
+    // [EPW*q, EPW*q + EPW) of a lane is word q * NT + tid, so every lane reads its
+    // own bank whatever position it is at, and a row copies in one store per word
+#define WB(p) s_wb[(((uint32_t)(p) / F::EPW) * NT + tid) * F::EPW + (uint32_t)(p) % F::EPW]
+#define WS(p) s_ws[(((uint32_t)(p) / F::EPW) * NT + tid) * F::EPW + (uint32_t)(p) % F::EPW]
+#define RG(f) (s_reg[C_REG(ctl)].f)
+
+    // ---- persistent per-lane state
+    uint32_t ctl = PH_IDLE;        // control word (C_* accessors)
+    uint32_t qpos = 0;             // position of the read in the job list (width row = qpos * 2 + strand)
+    uint32_t pen = 0;              // s_mm | s_gapo << 10 | s_gape << 20
+    uint32_t rmode = 0;            // mode | max_gapo << 8 | max_gape << 16
+    uint32_t pos = 0;              // exact tail: next position
+    IT ik = 0, il = 0;             // exact-tail interval
+    IT aux = 0;                    // exact tail: rev_l
+    int opt_max_diff = 0, max_diff = 0, best_score = 0, n_aln = 0, n_entries = 0;
+    CT best_cnt = 0;
+    uint32_t pool_top = 0;
+    uint32_t free_head = NIL;      // HUGE: popped slots, linked through NXT
+    BMask<MW> mask;
+    // the current entry (k, l, rev_k, meta); between an expansion and the next pop
+    // it holds the virtual top when C_VT is set (the last child pushed, when it is
+    // the next pop: it never goes to the pool)
+    E e{0, 0, 0, 0};
+    uint32_t st_p = 0, st_wq = 0;
+    uint64_t st_q = 0, st_b = 0;          // wave-uniform (ballot counts)
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+#ifdef HSA_DIAG
+    uint32_t dc[18] = {0};
+    uint64_t tsec[4] = {0, 0, 0, 0};
+    uint64_t tt = 0;
+#define TMARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); tsec[k] += t_ - tt; tt = t_; } while (0)
+#endif
+
+#define S_MM ((int)(pen & 1023u))
+#define S_GO ((int)((pen >> 10) & 1023u))
+#define S_GE ((int)(pen >> 20))
+#define R_MODE ((int)(rmode & 255u))
+#define R_MAXGO ((int)((rmode >> 8) & 255u))
+#define R_MAXGE ((int)(rmode >> 16))
+#define SCORE(mm, go, ge) ((mm) * S_MM + (go) * S_GO + (ge) * S_GE)
+
+    // base of the current strand's sequence at p (from the LDS element, see WFmt)
+    auto getc = [&](int p) -> uint32_t { return F::code(WB(p)); };
+    // stack bucket of an entry: dense index of its score (bwtgap.c:46-75)
+    auto bucket_of = [&](uint32_t m) -> int {
+        if (!GAPS && a.mm_buckets) return M_MM(m);
+        const int sc = SCORE(M_MM(m), M_GO(m), M_GE(m));
+        return (uint32_t)sc < a.ntab ? (int)s_lds[C_REG(ctl) * a.ntab + sc] : 0xFF;
+    };
+    // push to the pool (gap_push, bwtgap.c:46-75)
+    auto flush = [&](const E &v, int b) {
+        if ((uint32_t)b >= a.nb) { ctl |= 1u << 8; return; }
+        uint32_t slot;
+        if (HUGE && free_head != NIL) {
+            slot = free_head;
+            free_head = NXT(slot);
+        } else {
+            if (pool_top >= a.pcap) { ctl |= 1u << 8; return; }
+            slot = pool_top++;
+        }
+        DC(8);
+        ent_store<IT>(a.pool, wv * a.pcap + slot, lane, v);
+        const uint32_t old = mask.test(b) ? (uint32_t)HEAD(b) : NIL;
+        NXT(slot) = (LT)old;
+        HEAD(b) = (LT)slot;
+        mask.set(b);
+    };
+    auto start_search = [&]() {
+        best_score = SCORE(opt_max_diff + 1, R_MAXGO + 1, R_MAXGE + 1);
+        max_diff = opt_max_diff;
+        best_cnt = 0; n_aln = 0;
+        mask.clear(); pool_top = 0; free_head = NIL;
+        e = E{0, TT, 0, meta_pack((uint32_t)C_LEN(ctl), ST_M, 0, 0, 0, 0)};   // root (bwtgap.c:142)
+        ctl |= 1u << 6;
+        n_entries = 1;
+        SET_PH(ctl, PH_POP);
+    };
+    // width row of the current strand: row qpos * 2 + strand, 64 rows interleaved
+    auto row_base = [&](uint32_t cap_words) -> size_t {
+        const uint32_t r = qpos * 2u + C_STRAND(ctl);
+        return (size_t)(r >> 6) * cap_words * 64 + (r & 63u);
+    };
+    // copy the strand's pruning elements (k_widths) into the lane's LDS columns, then
+    // start bwt_match_gap (bwtgap.c:141-142)
+    auto start_strand = [&]() {
+        // LDS-DMA (global_load_lds_dword): word q of every active lane lands at
+        // word q * NT + tid, which is exactly the wave's slice of the LDS layout, so
+        // the whole row is in flight at once and one wait covers it
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.wb) + row_base(a.rb / 4);
+        uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + (tid & ~63u);
+        const uint32_t nwb = a.rb / 4;                 // row capacity in words (uniform)
+        for (uint32_t q = 0; q < nwb; ++q)
+            __builtin_amdgcn_global_load_lds(src + q * 64, db + q * NT, 4, 0, 0);
+        if (C_SEED(ctl) && !C_ALIAS(ctl)) {
+            const uint32_t *ss = reinterpret_cast<const uint32_t *>(a.ws) + row_base(a.rs / 4);
+            uint32_t *const ds = reinterpret_cast<uint32_t *>(s_ws) + (tid & ~63u);
+            const uint32_t nws = a.rs / 4;
+            for (uint32_t q = 0; q < nws; ++q)
+                __builtin_amdgcn_global_load_lds(ss + q * 64, ds + q * NT, 4, 0, 0);
+        }
+#ifdef HSA_EXTRA_LOADS
+        // experiment only: HSA_EXTRA_LOADS random 16-byte rank-table loads per strand
+        // start, to test whether k_search's time follows its memory request count
+        {
+            uint32_t acc = 0, h = qpos * 2654435761u + C_STRAND(ctl);
+            for (int x = 0; x < HSA_EXTRA_LOADS; ++x) {
+                h = h * 1664525u + 1013904223u;
+                acc += a.fwd.blk[h % (a.T >> 4)].w;
+            }
+            if (acc == 0x9e3779b9u) a.ctr[15] = acc;
+        }
+#endif
+        __builtin_amdgcn_s_waitcnt(0);                 // the DMA writes are visible to LDS reads
+        DC(15);
+        start_search();
+    };
+    auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
+        const int job = a.job_list ? a.job_list[qpos] : (int)qpos;
+        if (fl & HSA_F_OVERFLOW) {
+            if (a.ovf_list) a.ovf_list[atomicAdd(&a.ctr[a.ovf_ctr], 1ull)] = job;   // re-run by the next pass
+            else atomicAdd(&a.ctr[11], 1ull);                               // the last pass: stays unfinished
+        }
+        a.n_aln[job] = na;
+        a.flags[job] = fl;
+        a.hit_off[job] = ho;
+        SET_PH(ctl, PH_IDLE);
+    };
+    auto end_strand = [&]() {
+        if (n_aln > 0) {
+            const unsigned long long o = atomicAdd(&a.ctr[1], (unsigned long long)n_aln);
+            if (o + (uint64_t)n_aln > a.hit_cap) { finish_job(HSA_F_OVERFLOW, 0, 0); return; }
+            uint32_t *dst = a.hits + o * OW;
+            const uint32_t s30 = C_STRAND(ctl) << 30;
+            for (int h = 0; h < n_aln; ++h) {
+                // bwtaln.c:371-372 (a direct bwt_match_gap call leaves start/end 0)
+                const uint32_t end = h == 0 && !a.mg ? (uint32_t)(C_LEN(ctl) - 1) : 0u;
+                if constexpr (sizeof(IT) == 4) {
+                    // the six staged words first, then the record: one memory round trip per hit
+                    const uint32_t v0 = HB(h * 9 + 0), v1 = HB(h * 9 + 1), v2 = HB(h * 9 + 2), v3 = HB(h * 9 + 3),
+                                   v4 = HB(h * 9 + 4), v8 = HB(h * 9 + 8);
+                    dst[h * 9 + 0] = v0;
+                    dst[h * 9 + 1] = v1;
+                    dst[h * 9 + 2] = v2;
+                    dst[h * 9 + 3] = v3;
+                    dst[h * 9 + 4] = v4;
+                    dst[h * 9 + 5] = s30;
+                    dst[h * 9 + 6] = 0;
+                    dst[h * 9 + 7] = end;
+                    dst[h * 9 + 8] = v8;
+                } else {
+                    // hsa_aln64_t (include/hsa_gpu.h): 14 words
+                    uint32_t v[10];
+#pragma unroll
+                    for (int j = 0; j < 10; ++j) v[j] = HB(h * 10 + j);
+                    dst[h * 14 + 0] = v[0];
+                    dst[h * 14 + 1] = s30;
+#pragma unroll
+                    for (int j = 1; j < 9; ++j) dst[h * 14 + 1 + j] = v[j];
+                    dst[h * 14 + 10] = 0;
+                    dst[h * 14 + 11] = end;
+                    dst[h * 14 + 12] = v[9];
+                    dst[h * 14 + 13] = 0;
+                }
+            }
+            finish_job(0, n_aln, o);
+        } else if (a.mg) {
+            finish_job(0, 0, 0);        // one call, one strand
+        } else if (C_STRAND(ctl)) {
+            ctl &= ~(1u << 3);          // strand 0
+            st_wq += a.wq[qpos];        // its widths are the reference's work now (bwtaln.c:344-348)
+            start_strand();
+        } else {
+            finish_job(HSA_F_FALLBACK, 0, 0);
+        }
+    };
+    // hit handling (bwtgap.c:188-243) for entry e with final interval (k,l,rk,rl);
+    // returns false when the search must stop
+    auto on_hit = [&](IT k, IT l, IT rk, IT rl) -> bool {
+        const uint32_t m = e.w;
+        const int score = SCORE(M_MM(m), M_GO(m), M_GE(m));
+        if (n_aln == 0) {
+            best_score = score;
+            const int best_diff = M_MM(m) + M_GO(m) + ((R_MODE & MODE_GAPE) ? M_GE(m) : 0);
+            if (!(R_MODE & MODE_NONSTOP)) max_diff = (best_diff + 1 > opt_max_diff) ? opt_max_diff : best_diff + 1;
+        }
+        if (score == best_score) {
+            if constexpr (sizeof(IT) == 4) best_cnt = (int)((uint32_t)best_cnt + (l - k + 1u));
+            else best_cnt += (CT)(l - k + 1u);
+        } else if (best_cnt > RG(max_top2)) {
+            return false;
+        }
+        bool add = true;
+        if (M_GO(m)) {
+            for (int j = 0; j < n_aln; ++j) {
+                if constexpr (sizeof(IT) == 4) {
+                    if (HB(j * 9 + 1) == k && HB(j * 9 + 2) == l) { add = false; break; }
+                } else {
+                    const uint64_t hk = (uint64_t)HB(j * 10 + 1) | (uint64_t)HB(j * 10 + 2) << 32;
+                    const uint64_t hl = (uint64_t)HB(j * 10 + 3) | (uint64_t)HB(j * 10 + 4) << 32;
+                    if (hk == k && hl == l) { add = false; break; }
+                }
+            }
+        }
+        if (add) {
+            if ((uint32_t)n_aln >= a.hcap) { ctl |= 1u << 8; return false; }
+            // gap_shadow (bwtgap.c:94-105) on width_back[0, last_diff_pos), then the
+            // pruning elements of those positions (eq bit of p needs w[p+1])
+            const IT x = l - k + 1u;
+            const int ldp = M_ISD(m) ? M_I(m) : 0;
+            if (ldp > 0) {
+#ifdef HSA_DIAG
+                DC(13); dc[14] += (uint32_t)ldp;
+#endif
+                IT *const wg = reinterpret_cast<IT *>(a.wg) + row_base(a.rg);
+                int32_t *const wd = a.wbid ? a.wbid + row_base(a.rg) : nullptr;
+#define WG(p) wg[(uint32_t)(p) * 64]
+                IT jj = 0;
+                for (int p = 0; p < ldp; ++p) {
+                    IT w = WG(p);
+                    if (w > x) { w -= x; WG(p) = w; }
+                    else if (w == x) {
+                        WB(p) = (WT)((WB(p) & ~F::BIDM) | 1u);
+                        WG(p) = TT - (++jj);
+                        if (wd) wd[(uint32_t)p * 64] = 1;
+                    }
+                }
+                IT wnext = WG(ldp);
+                for (int p = ldp - 1; p >= 0; --p) {
+                    const IT w = WG(p);
+                    WB(p) = (WT)((WB(p) & ~F::EQ) | (w == wnext ? F::EQ : 0u));
+                    wnext = w;
+                }
+#undef WG
+            }
+            const uint32_t mw = (uint32_t)M_MM(m) | (uint32_t)M_GO(m) << 16 | (uint32_t)M_GE(m) << 24;
+            if constexpr (sizeof(IT) == 4) {
+                HB(n_aln * 9 + 0) = mw;
+                HB(n_aln * 9 + 1) = k; HB(n_aln * 9 + 2) = l; HB(n_aln * 9 + 3) = rk; HB(n_aln * 9 + 4) = rl;
+                HB(n_aln * 9 + 8) = (uint32_t)score;
+            } else {
+                HB(n_aln * 10 + 0) = mw;
+                HB(n_aln * 10 + 1) = (uint32_t)k; HB(n_aln * 10 + 2) = (uint32_t)(k >> 32);
+                HB(n_aln * 10 + 3) = (uint32_t)l; HB(n_aln * 10 + 4) = (uint32_t)(l >> 32);
+                HB(n_aln * 10 + 5) = (uint32_t)rk; HB(n_aln * 10 + 6) = (uint32_t)(rk >> 32);
+                HB(n_aln * 10 + 7) = (uint32_t)rl; HB(n_aln * 10 + 8) = (uint32_t)(rl >> 32);
+                HB(n_aln * 10 + 9) = (uint32_t)score;
+            }
+            ++n_aln;
+        }
+        return true;
+    };
+    // m (available differences) of entry e (bwtgap.c:160-163)
+    auto m_of = [&](uint32_t m) -> int {
+        int mm = max_diff - (M_MM(m) + M_GO(m));
+        if (R_MODE & MODE_GAPE) mm -= M_GE(m);
+        return mm;
+    };
+
+#ifdef HSA_DIAG
+    tt = __builtin_amdgcn_s_memtime();
+#endif
+    for (;;) {
+        // ---------------- (A) strand ends and read acquisition, batched per wave.
+        // The rare steps of a read -- copying its hits out (end_strand), the switch to
+        // the forward strand with its row DMA, taking the next read -- are long code
+        // paths that the whole wave executes whenever one lane needs one.  A lane that
+        // reaches one waits (PH_END / PH_IDLE) until batch_k lanes of the wave wait, or
+        // no lane is searching, and the wave then runs each path once for all of them.
+        const uint64_t wm = __ballot(C_PH(ctl) == PH_IDLE || C_PH(ctl) == PH_END);
+        if (wm && ((uint32_t)__popcll(wm) >= a.batch_k ||
+                   __ballot(C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END) == 0)) {
+            if (C_PH(ctl) == PH_END) end_strand();
+            const bool need = C_PH(ctl) == PH_IDLE;
+            const uint64_t mb = __ballot(need);
+            if (mb) {
+                const int leader = __ffsll((unsigned long long)mb) - 1;
+                unsigned long long base = 0;
+                if (lane == leader) base = atomicAdd(&a.ctr[a.qctr], (unsigned long long)__popcll(mb));
+                base = __shfl(base, leader);
+                if (need) {
+                    const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
+                    if (j < (unsigned long long)n_jobs) {
+                        qpos = (uint32_t)j;
+                        const int job = a.job_list ? a.job_list[j] : (int)j;
+                        const hsa_job_t J = a.jobs[job];
+                        opt_max_diff = J.max_diff;
+                        const uint32_t len = J.len;
+                        if (a.mg) {
+                            // one direct bwt_match_gap call: its strand, its width_seed kind
+                            // (host-checked: 0 <= seed_len <= len when width_seed is given)
+                            const hsa_mg_job_t M = a.mg[job];
+                            const uint32_t has_seed = M.seed != HSA_SEED_NONE;
+                            ctl = (uint32_t)(M.strand & 1) << 3 | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 |
+                                  (M.seed == HSA_SEED_ALIAS ? 1u : 0u) << 7 | len << 10 |
+                                  (has_seed ? (uint32_t)J.seed_len : 0u) << 20;
+                        } else {
+                            const uint32_t has_seed = (int)len > J.seed_len;
+                            ctl = 8u | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 | len << 10 |
+                                  (has_seed ? (uint32_t)J.seed_len : 0u) << 20;     // strand 1 (rc first, bwtaln.c:343)
+                        }
+                        const hsa_regime_t *R = s_reg + (J.regime & 1);
+                        pen = (uint32_t)R->s_mm | (uint32_t)R->s_gapo << 10 | (uint32_t)R->s_gape << 20;
+                        rmode = (uint32_t)R->mode | (uint32_t)R->max_gapo << 8 | (uint32_t)R->max_gape << 16;
+                        if (opt_max_diff > R->max_diff) ctl |= 2u << 8;
+                        start_strand();
+                    } else {
+                        SET_PH(ctl, PH_EXIT);
+                    }
+                }
+            }
+        }
+        if (__all(C_PH(ctl) == PH_EXIT)) break;
+
+#ifdef HSA_DIAG
+        TMARK(0);
+#endif
+        // ---------------- (B) control until a rank step is needed
+        int req = 0;
+        IT rp1 = 0, rp2 = 0;
+#ifdef HSA_DIAG
+        if (lane == 0) DC(5);
+#endif
+        // One control pass per iteration (HSA_CTL_LOOP=0): a lane whose pop needs no
+        // rank step (pruned, hit, strand change) just skips this iteration's step
+        // instead of making the whole wave run the control code again.
+#if HSA_CTL_LOOP
+        while (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END && !req) {
+#else
+        if (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END) do {
+#endif
+#ifdef HSA_DIAG
+            { const uint64_t em = __ballot(1); if (lane == __ffsll((unsigned long long)em) - 1) DC(7); }
+#endif
+            if (C_OVF(ctl)) {
+                if (C_OVF(ctl) > 1) atomicAdd(&a.ctr[5], 1ull);
+                finish_job(HSA_F_OVERFLOW, 0, 0);
+                break;
+            }
+            const uint32_t ph = C_PH(ctl);
+            if (ph == PH_EXACT) {
+                const uint32_t c = getc((int)pos);
+                if (c > 3) { SET_PH(ctl, PH_POP); continue; }              // 2BWT-Interface.c:377
+                req = 1; rp1 = ik; rp2 = il + 1u;
+                break;
+            }
+            // PH_POP: bwtgap.c:144-186
+            if (n_entries == 0 || n_entries > RG(max_entries)) { SET_PH(ctl, PH_END); continue; }
+            if (C_VT(ctl)) {
+                DC(3);
+                ctl &= ~(1u << 6);                                        // e already holds it
+            } else {
+                DC(4);
+                // pop the head of the lowest non-empty bucket
+                const int b = mask.lowest();
+                const uint32_t slot = HEAD(b);
+                e = ent_load<IT>(a.pool, (size_t)wv * a.pcap + slot, lane);
+                const uint32_t nx = NXT(slot);
+                if (nx == NIL) mask.reset(b);
+                else HEAD(b) = (LT)nx;
+                if (HUGE) { NXT(slot) = (LT)free_head; free_head = slot; }
+            }
+            --n_entries;
+            ++st_p;
+            const uint32_t m = e.w;
+            if (!(R_MODE & MODE_NONSTOP) && SCORE(M_MM(m), M_GO(m), M_GE(m)) > best_score + S_MM) {
+                SET_PH(ctl, PH_END);
+                continue;
+            }
+            const int em = m_of(m);
+            if (em < 0) continue;
+            const int ei = M_I(m);
+            if (ei > 0 && em < (int)(WB(ei - 1) & F::BIDM)) continue;
+            if (ei == 0) {
+                if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
+                continue;
+            }
+            if (em == 0 && (M_ST(m) == ST_M || (R_MODE & MODE_GAPE) || M_GE(m) == R_MAXGE)) {
+                ik = e.x; il = e.y; aux = e.z + (e.y - e.x); pos = (uint32_t)(ei - 1);   // bwt_match_exact
+                SET_PH(ctl, PH_EXACT);
+                continue;
+            }
+            req = 1; rp1 = e.x; rp2 = e.y + 1u;
+            SET_PH(ctl, PH_EXPAND);
+        }
+#if !HSA_CTL_LOOP
+        while (0);
+#endif
+
+#ifdef HSA_DIAG
+        TMARK(1);
+#endif
+        // ---------------- (C) the rank step
+        IT oa[4], ob[4];
+        const uint64_t rq = __ballot(req);
+#ifdef HSA_DIAG
+        {
+            if (lane == 0) dc[6] += (uint32_t)__popcll(rq);
+            const uint32_t ph0 = C_PH(ctl);
+            if (req) DC(ph0 == PH_EXACT ? 1 : 2);
+            if (req && rp2 == rp1 + 1u) DC(ph0 == PH_EXACT ? 16 : 17);
+        }
+#endif
+        uint32_t two = 0;
+        if (req) two = occ_pair(Ix<IT>::fwd(a), rp1, rp2, oa, ob) - 1u;
+        st_q += 2u * (uint64_t)__popcll(rq);
+        st_b += (uint64_t)__popcll(rq) + (uint64_t)__popcll(__ballot(two));
+
+#ifdef HSA_DIAG
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        TMARK(2);
+#endif
+        // ---------------- (D) apply
+        const uint32_t ph = C_PH(ctl);
+        if (req && ph == PH_EXACT) {
+            // BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170), one character
+            const uint32_t c = getc((int)pos);
+            IT oc = 0;
+#pragma unroll
+            for (uint32_t d = 1; d < 4; ++d) oc += d > c ? ob[d] - oa[d] : (IT)0;
+            const IT cc = pick4(CC, c);
+            ik = cc + pick4(oa, c) + 1u;
+            il = cc + pick4(ob, c);
+            aux -= oc;                                                   // rev_l
+            if (ik > il) {
+                SET_PH(ctl, PH_POP);                                     // no match: continue (bwtgap.c:185)
+            } else if (pos-- == 0) {
+                // write-back guard of bwt_match_exact (2BWT-Interface.c:383-386)
+                const IT rk = aux - (il - ik), erl = e.z + (e.y - e.x);
+                const IT hk = e.x ? ik : (IT)0, hl = e.y ? il : (IT)0, hrk = e.z ? rk : (IT)0, hrl = erl ? aux : (IT)0;
+                SET_PH(ctl, PH_POP);
+                if (!on_hit(hk, hl, hrk, hrl) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
+            }
+        } else if (req && ph == PH_EXPAND) {
+            // children of the bidirectional step (2BWT-Interface.c:235-272), in place:
+            // oa -> k, ob -> l of child c; srk = rev_k
+            const uint32_t m = e.w;
+            const IT ek = e.x, el = e.y, erk = e.z, erl = erk + (el - ek);
+            const int i = M_I(m) - 1;                                    // --i (bwtgap.c:245)
+            const int est = M_ST(m), emm = M_MM(m), ego = M_GO(m), ege = M_GE(m);
+            const int em = m_of(m);
+            const int len = C_LEN(ctl);
+            IT srk[4];
+            {
+                IT oc = 0;
+#pragma unroll
+                for (int c = 3; c >= 0; --c) {
+                    const IT d = ob[c] - oa[c];
+                    oa[c] = CC[c] + oa[c] + 1u;
+                    ob[c] = CC[c] + ob[c];
+                    srk[c] = (erl - oc) - (ob[c] - oa[c]);
+                    oc += d;
+                }
+            }
+            int allow_diff = 1, allow_M = 1;
+            if (i > 0) {
+                // width[i-1].bid, width[i].bid and w[i-1] == w[i] (bwtgap.c:256-258)
+                const uint32_t w1 = WB(i - 1), w0 = WB(i);
+                const int b1 = (int)(w1 & F::BIDM), b0 = (int)(w0 & F::BIDM);
+                if (b1 > em - 1) allow_diff = 0;
+                else if (b1 == em - 1 && b0 == em - 1 && (w1 & F::EQ)) allow_M = 0;
+                const int ii = i - (len - C_SLEN(ctl));
+                if (C_SEED(ctl) && ii > 0) {
+                    int ems = RG(max_seed_diff) - (emm + ego);
+                    if (R_MODE & MODE_GAPE) ems -= ege;
+                    // width_seed aliased to width_back (bwtgap.c:809): the same LDS row
+                    const uint32_t s1 = C_ALIAS(ctl) ? (uint32_t)WB(ii - 1) : (uint32_t)WS(ii - 1);
+                    const uint32_t s0 = C_ALIAS(ctl) ? (uint32_t)WB(ii) : (uint32_t)WS(ii);
+                    const int c1 = (int)(s1 & F::BIDM), c0 = (int)(s0 & F::BIDM);
+                    if (c1 > ems - 1) allow_diff = 0;
+                    else if (c1 == ems - 1 && c0 == ems - 1 && (s1 & F::EQ)) allow_M = 0;
+                }
+            }
+            // The pushes of bwtgap.c:267-325 as a candidate mask in push order:
+            // bit 0 insertion, bits 1-4 deletion with child j = bit-1, bits 5-8
+            // match/mismatch with child (seq[i] + bit-4) & 3.  All but the last go to the
+            // pool in order; the last becomes the virtual top when it is the next pop.
+            const uint32_t sc = getc(i);
+            uint32_t cand = 0;
+            if (GAPS && allow_diff && (R_MAXGO > 0 || ego > 0)) {
+                const int ies = RG(indel_end_skip);
+                const int tmp = (R_MODE & MODE_LOGGAP) ? int_log2((uint32_t)(ege + ego)) / 2 + 1 : ego + ege;
+                if (i >= ies + tmp && len - i >= ies + tmp) {
+                    uint32_t dm = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) dm |= (oa[j] <= ob[j] ? 1u : 0u) << j;
+                    const IT occ = el - ek + 1u;
+                    if (est == ST_M) {
+                        if (ego < R_MAXGO) cand = 1u | dm << 1;
+                    } else if (est == ST_I) {
+                        if (ege < R_MAXGE) cand = 1u;
+                    } else if (ege < R_MAXGE && (ege + ego < max_diff || occ < (IT)RG(max_del_occ))) {
+                        cand = dm << 1;
+                    }
+                }
+            }
+            if (allow_diff && allow_M) {
+#pragma unroll
+                for (int j = 1; j <= 4; ++j) {
+                    const uint32_t c = (sc + (uint32_t)j) & 3u;
+                    cand |= (pick4(oa, c) <= pick4(ob, c) ? 1u : 0u) << (4 + j);
+                }
+            } else if (sc < 4) {
+                cand |= (pick4(oa, sc) <= pick4(ob, sc) ? 1u : 0u) << 8;    // == bit 8: c = sc, no mismatch
+            }
+            // entry of candidate bit b
+            auto entry = [&](uint32_t b) -> E {
+                const bool ins = GAPS && b == 0, del = GAPS && b >= 1 && b <= 4;
+                const uint32_t c = del ? b - 1u : (sc + b - 4u) & 3u;
+                const uint32_t is_mm = (b != 8u || sc > 3) ? 1u : 0u;
+                IT k = pick4(oa, c), l = pick4(ob, c), rk = pick4(srk, c);
+                uint32_t meta;
+                if (GAPS && (ins || del)) {
+                    if (ins) { k = ek; l = el; rk = erk; }
+                    const uint32_t go = (uint32_t)ego + (est == ST_M), ge = (uint32_t)ege + (est != ST_M);
+                    meta = meta_pack((uint32_t)(del ? i + 1 : i), ins ? ST_I : ST_D, 1u, (uint32_t)emm, go, ge);
+                } else {
+                    meta = meta_pack((uint32_t)i, ST_M, is_mm, (uint32_t)emm + is_mm, (uint32_t)ego, (uint32_t)ege);
+                }
+                return E{k, l, rk, meta};
+            };
+            if (cand) {
+                const uint32_t last = 31u - (uint32_t)__clz(cand);
+                n_entries += __popc(cand);
+                for (uint32_t rest = cand & ~(1u << last); rest; rest &= rest - 1u) {
+                    const E v = entry((uint32_t)__ffs(rest) - 1u);
+                    flush(v, bucket_of(v.w));
+                }
+                const E v = entry(last);
+                const int bk = bucket_of(v.w);
+                if (bk <= mask.lowest()) { e = v; ctl |= 1u << 6; }
+                else flush(v, bk);
+            }
+            SET_PH(ctl, PH_POP);
+        }
+#ifdef HSA_DIAG
+        TMARK(3);
+#endif
+    }
+
+#ifdef HSA_DIAG
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {
+        g_diag[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_memtime();
+        g_diag[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+    for (int i = 0; i < 18; ++i)
+        if (i < 9 || i > 12) atomicAdd(&g_dctr[i], (unsigned long long)dc[i]);
+    if (lane == 0)
+        for (int i = 0; i < 4; ++i) atomicAdd(&g_dctr[9 + i], (unsigned long long)tsec[i]);
+#endif
+    // statistics
+    if (lane == 0) {
+        atomicAdd(&a.ctr[2], (unsigned long long)st_q);
+        atomicAdd(&a.ctr[3], (unsigned long long)st_b);
+    }
+    atomicAdd(&a.ctr[4], (unsigned long long)st_p);
+    if (st_wq) {
+        atomicAdd(&a.ctr[2], (unsigned long long)st_wq);
+        atomicAdd(&a.ctr[7], (unsigned long long)st_wq);
+        atomicAdd(&a.ctr[14], (unsigned long long)st_wq);
+    }
+#undef HEAD
+#undef WB
+#undef WS
+#undef NXT
+#undef HB
+#undef RG
+#undef S_MM
+#undef S_GO
+#undef S_GE
+#undef R_MODE
+#undef R_MAXGO
+#undef R_MAXGE
+#undef SCORE
+}
+
+
+
+// ---------------------------------------------------------------- host helpers (both TUs)
+static int check_regimes(const hsa_regime_t *rg, int n)
+{
+    for (int r = 0; r < n; ++r) {
+        const hsa_regime_t &R = rg[r];
+        if (R.s_mm < 0 || R.s_gapo < 0 || R.s_gape < 0) { hsa_set_error("negative penalty"); return HSA_E_ARG; }
+        if (R.n_stacks <= 0 || R.n_stacks > MAXS) { hsa_set_error("n_stacks %d outside 1..%d", R.n_stacks, MAXS); return HSA_E_ARG; }
+        if (R.max_gapo > 14 || R.max_gape > 254) { hsa_set_error("max_gapo/max_gape out of range"); return HSA_E_ARG; }
+        if (R.max_diff < -1 || R.max_diff > 125) { hsa_set_error("max_diff out of range"); return HSA_E_ARG; }
+    }
+    return 0;
+}
+
+// Dense bucket numbering of the scores a search of this regime can push
+// (bwtgap.c:46-75): n_mm <= max_diff+1, n_gapo <= min(max_gapo, max_diff), n_gape > 0
+// only after a gap open.  Returns the bucket count.
+static int bucket_map(const hsa_regime_t &R, uint8_t map[MAXS])
+{
+    bool used[MAXS] = {false};
+    const int md = R.max_diff < 0 ? 0 : R.max_diff;
+    const int go_max = R.max_gapo < md ? R.max_gapo : md;
+    for (int mm = 0; mm <= md + 1; ++mm)
+        for (int go = 0; go <= go_max; ++go)
+            for (int ge = 0; ge <= (go > 0 ? R.max_gape : 0); ++ge) {
+                const int s = mm * R.s_mm + go * R.s_gapo + ge * R.s_gape;
+                if (s >= 0 && s < MAXS && s < R.n_stacks) used[s] = true;
+            }
+    int k = 0;
+    for (int s = 0; s < MAXS; ++s) map[s] = used[s] && k < 0xFF ? (uint8_t)k++ : (uint8_t)0xFF;
+    return k;
+}
+
+// The dense bucket of a score is simply its n_mm when no gap opens exist and every
+// reachable mismatch count has its own score (k_search skips the table then).
+static bool mm_buckets(const hsa_regime_t *rg, int n, const uint8_t *bmap)
+{
+    for (int r = 0; r < n; ++r) {
+        const hsa_regime_t &R = rg[r];
+        if (R.max_gapo != 0 || R.s_mm <= 0) return false;
+        const int md = R.max_diff < 0 ? 0 : R.max_diff;
+        for (int mm = 0; mm <= md + 1; ++mm) {
+            const int sc = mm * R.s_mm;
+            if (sc >= MAXS || bmap[r * MAXS + sc] != mm) return false;
+        }
+    }
+    return true;
+}
+
+struct LaunchPlan {
+    size_t lanes, blocks;
+    uint32_t nt;                     // lanes per workgroup of k_search (256 or 64)
+    uint32_t pcap, hcap, nb;
+    bool gaps, wide;                 // gap opens possible; 16-bit pruning elements (WFmt)
+    uint32_t off_heads, off_wb, off_ws;
+    size_t lds;
+    bool huge;                       // PASS_HUGE: 32-bit links, reused slots
+    uint32_t ntab;                   // score table entries per regime in LDS
+};
+
+// The capacity passes of one search: MAIN (every read), BIG (the reads that overflowed
+// their main-pass lane: 65 535 pool slots, 16 384 hits), HUGE (the reads that overflowed
+// BIG: reused slots up to max_entries + 16 live entries, 262 144 hits).
+enum { PASS_MAIN = 0, PASS_BIG = 1, PASS_HUGE = 2 };
+
+static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int nb, bool gaps, bool wide, int mode,
+                       LaunchPlan &P, int max_entries = 0, uint32_t ent_bytes = 16)
+{
+    const bool big = mode == PASS_BIG;
+    P.huge = mode == PASS_HUGE;
+    P.ntab = (uint32_t)ix->staged_ntab;
+    P.nb = (uint32_t)nb;
+    P.gaps = gaps;
+    P.wide = wide;
+    const uint32_t esz = wide ? 2u : 1u;
+    const uint32_t epw = 4u / esz;                       // elements per LDS word (WFmt::EPW)
+    // Resident workgroups per CU, from gfx950's own limits: 160 KiB of LDS per CU, at
+    // most 16 waves (__launch_bounds__(NT, 4) caps VGPRs at 4 waves per SIMD).  The
+    // per-lane LDS (bucket heads, pruning rows) decides between 256-lane workgroups
+    // and 64-lane ones, which pack the CU's LDS more finely: -n 4 -o 1 has 39 buckets
+    // and ~220 B per lane, i.e. 2 workgroups of 256 (8 waves) but 11 of 64 (11 waves).
+    // (hipOccupancyMaxActiveBlocksPerMultiprocessor is not used: depending on which
+    // HIP runtime the process loaded first it assumed 64 KiB of LDS and halved the
+    // grid -- measured 512 instead of 1024 workgroups, 1.5x slower.)
+    auto layout = [&](uint32_t nt) {
+        P.nt = nt;
+        P.off_heads = 2 * P.ntab + 128;   // score tables, then the two regimes
+        P.off_wb = P.off_heads + (uint32_t)nb * nt * (P.huge ? 4u : 2u);
+        P.off_ws = P.off_wb + ((uint32_t)max_len / epw + 1u) * nt * 4u;
+        P.lds = ((size_t)P.off_ws + ((size_t)max_seed / epw + 1u) * nt * 4u + 15) / 16 * 16;
+        int per_cu = (int)((160u * 1024u) / P.lds);
+        const int cap = 16 / (int)(nt / 64);                 // 16 waves per CU
+        const int want = g_waves_per_cu / (int)(nt / 64);
+        if (per_cu > cap) per_cu = cap;
+        if (per_cu > want) per_cu = want > 0 ? want : 1;
+        return per_cu;
+    };
+    static const int force256 = getenv("HSA_WG256") != nullptr;   // A/B runs only
+    int per_cu = layout(P.huge ? 64 : 256);
+    if (per_cu < 4 && !force256 && !P.huge) {
+        const int p64 = layout(64);
+        if (p64 > per_cu * 4) per_cu = p64;
+        else per_cu = layout(256);
+    }
+    if (P.lds > 160 * 1024) { hsa_set_error("reads too long for the LDS budget (%zu bytes)", P.lds); return HSA_E_ARG; }
+    if (per_cu < 1) { hsa_set_error("search kernel does not fit (LDS %zu)", P.lds); return HSA_E_ARG; }
+    const uint32_t NTB = P.nt;
+    size_t blocks = (size_t)ix->n_cu * per_cu;
+    size_t need_blocks = ((size_t)n_jobs + NTB - 1) / NTB;
+    if (P.huge) {
+        blocks = 1;                                          // 64 lanes: a handful of reads
+    } else if (big) {
+        static const size_t big_lanes = getenv("HSA_BIG_LANES") ? strtoull(getenv("HSA_BIG_LANES"), nullptr, 10) : 4096;
+        const size_t big_blocks = big_lanes / NTB > 0 ? big_lanes / NTB : 1;
+        blocks = need_blocks < big_blocks ? need_blocks : big_blocks;
+    } else if (need_blocks < blocks) {
+        blocks = need_blocks;
+    }
+    if (blocks < 1) blocks = 1;
+    P.blocks = blocks;
+    P.lanes = blocks * NTB;
+    static int verbose = -1;
+    if (verbose < 0) verbose = getenv("HSA_VERBOSE") != nullptr;
+    if (verbose) {
+        int occ = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_search<1, true, uint8_t, 256>, 256, P.lds);
+        fprintf(stderr, "[hsa] launch: %d CUs x %d workgroups of %u lanes (runtime occupancy query says %d), "
+                "LDS %zu B, %zu workgroups, %d buckets\n", ix->n_cu, per_cu, P.nt, occ, P.lds, blocks, nb);
+    }
+    // pool slots are not reused within a search: gapped searches push many more.  A
+    // deeper main-pass pool keeps the long gapped searches inside the main pass, where
+    // their tails overlap other lanes' work, instead of the serial overflow re-run:
+    // config 4 (150 bp, -o 1) 2.36 -> 2.07 s per 1M reads at 32768 (49152: same)
+    P.pcap = big ? 65535u : (uint32_t)(g_pool_entries ? g_pool_entries : (gaps ? 32768 : 8192));
+    P.hcap = big ? 16384u : (uint32_t)g_hit_cap;
+    if (P.huge) {
+        // live entries never exceed max_entries + 9 (bwtgap.c:150-151); the pool is
+        // capped at 4 Mi entries per lane (80 MB), beyond which a read stays unfinished
+        const uint64_t want = (uint64_t)(max_entries > 0 ? max_entries : 0) + 16u;
+        P.pcap = (uint32_t)(want < (4ull << 20) ? want : (4ull << 20));
+        P.hcap = 262144u;
+    } else if (ent_bytes > 16 && !big) {
+        // 64-bit entries are 32 bytes: the main pass's pools stay within 64 GB of HBM
+        // (next to an index of up to ~2 x 16 GB for a 15 Gbp text); reads that need
+        // more go to the big and huge passes as usual
+        const size_t budget = (size_t)64 << 30;
+        if (P.lanes * P.pcap * ent_bytes > budget) {
+            const size_t p = budget / (P.lanes * ent_bytes);
+            P.pcap = (uint32_t)(p < 1024 ? 1024 : p);
+        }
+    }
+    return 0;
+}
+
+template <typename WT, int NT, typename IT>
+static void launch_search_nt(const LaunchPlan &P, const SearchArgs &A, hipStream_t st)
+{
+    const dim3 g((unsigned)P.blocks), b(NT);
+    if (P.nb <= 32) {
+        if (P.gaps) hipLaunchKernelGGL((k_search<0, true, WT, NT, false, IT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<0, false, WT, NT, false, IT>), g, b, P.lds, st, A);
+    } else if (P.nb <= 64) {
+        if (P.gaps) hipLaunchKernelGGL((k_search<1, true, WT, NT, false, IT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<1, false, WT, NT, false, IT>), g, b, P.lds, st, A);
+    } else {
+        if (P.gaps) hipLaunchKernelGGL((k_search<2, true, WT, NT, false, IT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<2, false, WT, NT, false, IT>), g, b, P.lds, st, A);
+    }
+}
+
+template <typename WT, typename IT>
+static void launch_search(const LaunchPlan &P, const SearchArgs &A, hipStream_t st)
+{
+    if (P.huge) {
+        const dim3 g((unsigned)P.blocks), b(64);
+        if (P.gaps) hipLaunchKernelGGL((k_search<2, true, WT, 64, true, IT>), g, b, P.lds, st, A);
+        else hipLaunchKernelGGL((k_search<2, false, WT, 64, true, IT>), g, b, P.lds, st, A);
+        return;
+    }
+    if (P.nt == 64) launch_search_nt<WT, 64, IT>(P, A, st);
+    else launch_search_nt<WT, 256, IT>(P, A, st);
+}
+
+// One search pass over jobs (or a job_list subset) with device pointers: k_widths
+// fills the width rows of every (read, strand), then k_search runs the reads.
+// caller-width mode of a pass (hsa_match_gap_batch)
+struct MgPass {
+    const hsa_mg_job_t *d_mg;
+    int32_t *d_cw;
+};
+
+template <typename IT = uint32_t>
+static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
+                            const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
+                            int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
+                            uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, const MgPass *mg)
+{
+    constexpr size_t WGB = sizeof(IT);       // bytes per full w value (wg rows)
+    const uint32_t esz = P.wide ? 2u : 1u;
+    const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;
+    const uint32_t rg = (uint32_t)max_len + 1u;
+    const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
+    uint8_t *wr = (uint8_t *)ix->d_wrows;
+    SearchArgs A;
+    A.fwd = RankDir{ix->blk[0], ix->isa0};
+    A.rev = RankDir{ix->blk[1], ix->risa0};
+    A.T = ix->T;
+    memcpy(A.C, ix->C, sizeof A.C);
+    A.fwd64 = RankDir64{ix->blk[0], ix->sup[0], ix->isa0_64};
+    A.rev64 = RankDir64{ix->blk[1], ix->sup[1], ix->risa0_64};
+    A.T64 = ix->T64;
+    memcpy(A.C64, ix->C64, sizeof A.C64);
+    A.regimes = d_regimes; A.bmap = d_bmap; A.jobs = d_jobs; A.job_list = d_list; A.n_jobs = n; A.codes = d_codes;
+    A.n_aln = d_n; A.flags = d_fl; A.hit_off = d_ho; A.hits = d_hits; A.hit_cap = hit_cap; A.ctr = d_ctr;
+    A.wb = wr; A.ws = wr + rows * rb; A.wg = reinterpret_cast<uint32_t *>(wr + rows * (rb + rs));
+    A.rb = rb; A.rs = rs; A.rg = rg;
+    A.pool = S.pool; A.nxt = S.nxt; A.hbuf = S.hbuf;
+    A.pcap = P.pcap; A.hcap = P.hcap;        // the planned capacities (the scratch may be larger)
+    A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
+    A.mm_buckets = ix->staged_mmb ? 1u : 0u;
+    A.ntab = P.ntab;
+    A.batch_k = (uint32_t)g_batch_k;
+    A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0; A.ovf_ctr = 8;
+    A.mg = mg ? mg->d_mg : nullptr;
+    A.cw = mg ? mg->d_cw : nullptr;
+    A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg)) : nullptr;
+    A.wq = reinterpret_cast<uint32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg + (mg ? 4 * (size_t)rg : 0)));
+    return A;
+}
+
+template <typename IT = uint32_t>
+static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
+                       const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
+                       int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
+                       uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st,
+                       int32_t *ovf_list = nullptr, const unsigned long long *n_dev = nullptr, uint32_t qctr = 0,
+                       const MgPass *mg = nullptr, uint32_t ovf_ctr = 8)
+{
+    // 64-bit intervals: two uint4 per pool entry, 10 staged words per hit (HitW)
+    constexpr size_t EW = sizeof(IT) / 4;
+    int rc = hsa_scratch_reserve(S, P.lanes, P.pcap * EW, P.hcap * EW, P.huge ? 4 : 2);
+    if (rc) return rc;
+    const uint32_t esz = P.wide ? 2u : 1u;
+    const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;
+    const uint32_t rg = (uint32_t)max_len + 1u;
+    const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
+    const size_t row_bytes = rb + rs + sizeof(IT) * (size_t)rg + (mg ? 4 * (size_t)rg : 0);   // + full bids (caller widths)
+    if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * row_bytes + 4 * (size_t)n + 256))) return rc;
+    if (mg) {
+        if constexpr (sizeof(IT) != 4) {
+            hsa_set_error("caller-width searches (bwt_match_gap) take 32-bit indexes");
+            return HSA_E_ARG;
+        } else {
+            SearchArgs A = pass_args<IT>(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n,
+                                         d_fl, d_ho, d_hits, hit_cap, d_ctr, mg);
+            A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr; A.ovf_ctr = ovf_ctr;
+            if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
+            const unsigned nb = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
+            if (P.wide) hipLaunchKernelGGL(k_widths_import<uint16_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
+            else hipLaunchKernelGGL(k_widths_import<uint8_t>, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
+            HSA_HIP(hipGetLastError());
+            if (ix->ev_split) HSA_HIP(hipEventRecord(ix->ev_split, st));
+            if (P.wide) launch_search<uint16_t, uint32_t>(P, A, st);
+            else launch_search<uint8_t, uint32_t>(P, A, st);
+            HSA_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_widths_export, dim3(nb ? nb : 1), dim3(BLOCK), 0, st, A);
+            HSA_HIP(hipGetLastError());
+            return 0;
+        }
+    }
+    SearchArgs A = pass_args<IT>(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
+                                 d_ho, d_hits, hit_cap, d_ctr, nullptr);
+    A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr; A.ovf_ctr = ovf_ctr;
+    if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
+    size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
+    if (wblocks < 1) wblocks = 1;
+    if (P.wide) hipLaunchKernelGGL((k_widths<uint16_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
+    else hipLaunchKernelGGL((k_widths<uint8_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
+    HSA_HIP(hipGetLastError());
+    if (ix->ev_split && !n_dev) HSA_HIP(hipEventRecord(ix->ev_split, st));
+    if (P.wide) launch_search<uint16_t, IT>(P, A, st);
+    else launch_search<uint8_t, IT>(P, A, st);
+    HSA_HIP(hipGetLastError());
+    return 0;
+}
+
+static bool any_gaps(const hsa_regime_t *rg, int n)
+{
+    for (int r = 0; r < n; ++r)
+        if (rg[r].max_gapo > 0) return true;
+    return false;
+}
+
+// 16-bit pruning elements when a bid may be compared with a bound above 14 (WFmt).
+static bool need_wide(const hsa_regime_t *rg, int n)
+{
+    for (int r = 0; r < n; ++r)
+        if (rg[r].max_diff > 14 || rg[r].max_seed_diff > 14) return true;
+    return false;
+}
+
+static int jobs_limits(const hsa_job_t *jobs, int n, int &max_len, int &max_seed)
+{
+    max_len = 0; max_seed = 0;
+    for (int j = 0; j < n; ++j) {
+        if (jobs[j].len > 1023) { hsa_set_error("read %d longer than 1023", j); return HSA_E_ARG; }
+        if (jobs[j].max_diff > 125 || jobs[j].max_diff < -1) { hsa_set_error("max_diff out of range"); return HSA_E_ARG; }
+        if ((int)jobs[j].len > max_len) max_len = (int)jobs[j].len;
+        if ((int)jobs[j].len > jobs[j].seed_len && jobs[j].seed_len > max_seed) max_seed = jobs[j].seed_len;
+    }
+    return 0;
+}
+
+// regimes + bucket maps into the staging area: [regimes (256 B)][bmap 2*MAXS].
+// Repeated launches with the same options skip the copy (a pageable H2D copy
+// would otherwise wait for the stream and stall the host between launches).
+static int stage_regimes(hsa_index *ix, const hsa_regime_t *regimes, int n_regimes, char *dst, int &nb,
+                         hipStream_t st, bool force)
+{
+    static_assert(256 + 2 * MAXS <= sizeof(ix->staged), "staging copy");
+    uint8_t host[256 + 2 * MAXS];
+    memset(host, 0xFF, sizeof host);
+    memcpy(host, regimes, sizeof(hsa_regime_t) * n_regimes);
+    nb = 1;
+    int ntab = 8;
+    for (int r = 0; r < n_regimes; ++r) {
+        int k = bucket_map(regimes[r], host + 256 + r * MAXS);
+        nb = k > nb ? k : nb;
+        ntab = regimes[r].n_stacks > ntab ? regimes[r].n_stacks : ntab;
+    }
+    if (nb > MAXB) { hsa_set_error("%d reachable scores: at most %d stack buckets", nb, MAXB); return HSA_E_ARG; }
+    ix->staged_ntab = (ntab + 7) / 8 * 8;
+    ix->staged_mmb = mm_buckets(regimes, n_regimes, host + 256);
+    if (!force && ix->staged_valid && memcmp(ix->staged, host, sizeof host) == 0) return 0;
+    memcpy(ix->staged, host, sizeof host);
+    ix->staged_valid = 1;
+    HSA_HIP(hipMemcpyAsync(dst, ix->staged, sizeof host, hipMemcpyHostToDevice, st));
+    HSA_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+// hsa_search_device / hsa_search_device64: the main pass over a device-resident batch,
+// then the BIG and HUGE capacity re-runs, all queued on one stream without a host sync.
+template <typename IT>
+static int search_device_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_device_batch_t *b,
+                              void *stream)
+{
+    // regimes: host array; staged into the index's staging area
+    if (n_regimes < 1 || n_regimes > 2) { hsa_set_error("1 or 2 regimes"); return HSA_E_ARG; }
+    if (sizeof(IT) == 8 && !ix->has_sup) { hsa_set_error("not a 64-bit index (hsa_index_create_device64)"); return HSA_E_ARG; }
+    int rc = check_regimes(regimes, n_regimes);
+    if (rc) return rc;
+    if (b->max_len < 1 || b->max_len > 1023 || b->max_seed < 0 || b->max_seed > 1023) {
+        hsa_set_error("max_len/max_seed out of range");
+        return HSA_E_ARG;
+    }
+    HSA_HIP(hipSetDevice(ix->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+    void *before = ix->d_in;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1536))) return rc;
+    int nb = 0;
+    if ((rc = stage_regimes(ix, regimes, n_regimes, (char *)ix->d_in, nb, st, before != ix->d_in))) return rc;
+    LaunchPlan P, B, H;
+    constexpr uint32_t EB = 4u * sizeof(IT);        // pool entry bytes
+    const bool gaps = any_gaps(regimes, n_regimes), wide = need_wide(regimes, n_regimes);
+    int max_entries = 0;
+    for (int r = 0; r < n_regimes; ++r) max_entries = regimes[r].max_entries > max_entries ? regimes[r].max_entries : max_entries;
+    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_MAIN, P, 0, EB)) ||
+        (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_BIG, B, 0, EB)) ||
+        (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_HUGE, H, max_entries, EB)))
+        return rc;
+    if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, (size_t)b->n_jobs * 4 + 64)) ||
+        (rc = hsa_grow(&ix->d_ovf2, &ix->d_ovf2_cap, (size_t)b->n_jobs * 4 + 64)))
+        return rc;
+    unsigned long long *ctr = (unsigned long long *)b->d_counters;
+    const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
+    const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
+    hipEvent_t *pe = ix->pev[ix->pev_n % hsa_index::PASS_RING];
+    for (int j = 0; j < 3; ++j)
+        if (!pe[j]) HSA_HIP(hipEventCreate(&pe[j]));
+    ++ix->pev_n;
+    ix->ev_split = pe[1];
+    HSA_HIP(hipEventRecord(pe[0], st));
+    if ((rc = launch_pass<IT>(ix, P, ix->main, d_reg, d_bmap, b->d_jobs, nullptr, b->n_jobs, b->max_len, b->max_seed,
+                          b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st,
+                          (int32_t *)ix->d_ovf)))
+        return rc;
+    // exact re-runs of the reads that overflowed their lane's capacity: BIG for the
+    // main pass's (count ctr[8]), HUGE for BIG's (count ctr[12]); the read counts stay
+    // on the device, so an empty re-run is a launch whose lanes exit at once
+    if ((rc = launch_pass<IT>(ix, B, ix->big, d_reg, d_bmap, b->d_jobs, (const int32_t *)ix->d_ovf, b->n_jobs,
+                          b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
+                          b->hit_cap, ctr, st, (int32_t *)ix->d_ovf2, ctr + 8, 9, nullptr, 12)) ||
+        (rc = launch_pass<IT>(ix, H, ix->huge, d_reg, d_bmap, b->d_jobs, (const int32_t *)ix->d_ovf2, b->n_jobs,
+                          b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
+                          b->hit_cap, ctr, st, nullptr, ctr + 12, 15)))
+        return rc;
+    HSA_HIP(hipEventRecord(pe[2], st));
+    ix->ev_split = ix->evm;
+    return 0;
+}

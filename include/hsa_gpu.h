@@ -235,12 +235,47 @@ int hsa_sa_position_device(hsa_index_t *ix, size_t n, const uint32_t *d_sa_index
  * DESIGN.md "The random-access ceiling"). */
 int hsa_probe_gather(int device, uint64_t table_bytes, int per_sector, double *gbps);
 
+/* ---- 64-bit intervals (texts of 2^32 characters or more; config 5) ----
+ * The reference's bwtint_t is 32-bit (2BWT-Interface.h:26), so its index, its hit
+ * record and the drop-in ABI (hsa_bwtaln.h) end at 2^32 - 1 characters.  These entry
+ * points run the same search with 64-bit SA intervals.
+ *
+ * hsa_index_create_device64: as hsa_index_create_device, with 64-bit lengths, '$'
+ * rows and C tables.  The rank blocks keep their counts modulo 2^32 and a superblock
+ * table (exact u64 Occ every 2^24 characters, 32 bytes per entry) restores the high
+ * part.  An index under 2^32 characters also serves every 32-bit entry point; a
+ * longer one only the *64 ones (the others return HSA_E_ARG). */
+int hsa_index_create_device64(int device, uint64_t T, uint64_t isa0, const uint64_t C[5], const uint32_t *d_code_lsb,
+                              uint64_t rT, uint64_t risa0, const uint64_t rC[5], const uint32_t *d_rcode_lsb,
+                              hsa_index_t **out);
+int hsa_index_is64(const hsa_index_t *ix);
+/* BWTAllOccValue (BWT.c:793) at 64-bit positions 0..T+1: 4 u64 per position. */
+int hsa_occ4_batch64(hsa_index_t *ix, int dir, size_t n, const uint64_t *pos, uint64_t *occ4_out);
+/* The hit record of the 64-bit search: bwt_aln1_t (bwtaln.h:41-50) with 64-bit
+ * k, l, rev_k, rev_l; 14 u32 (56 bytes). */
+typedef struct {
+    uint32_t n_mm:16, n_gapo:8, n_gape:8;
+    uint32_t type:30, strand:2;
+    uint64_t k, l, rev_k, rev_l;
+    int32_t start, end;
+    int32_t score, pad;
+} hsa_aln64_t;
+/* hsa_search_device on a 64-bit index (hsa_index_create_device64): the same batch
+ * and counters; d_hits holds hit_cap hsa_aln64_t records. */
+int hsa_search_device64(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes,
+                        const hsa_device_batch_t *b, void *stream);
+
 /* Suffix-array based BWT construction on the device for a text given as LSB-first
  * 2-bit codes (16 per u32).  Produces the $-less BWT codes (LSB-first) and
  * inverseSa0 = rank of suffix 0 among T+1 suffixes incl. '$' (BWT.h:61-83).
  * `reverse` builds the BWT of the reversed text. */
 int hsa_build_bwt_device(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse,
                          uint32_t *d_bwt_lsb, uint32_t *isa0, uint32_t C[5]);
+/* The same for any T >= 1 (64-bit '$' row and C table); d_bwt_lsb holds ceil(T/16)
+ * words.  Device memory besides the text and the output: about T bytes plus 9 GB
+ * (u64 suffix positions past 2^32 characters). */
+int hsa_build_bwt_device64(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse,
+                           uint32_t *d_bwt_lsb, uint64_t *isa0, uint64_t C[5]);
 
 #ifdef __cplusplus
 }

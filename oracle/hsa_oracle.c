@@ -8,6 +8,12 @@
  *
  * Parity pin: tests/test_oracle.py checks every function here against the
  * golden vectors the compiled reference produced (tests/golden/).
+ *
+ * Compiled twice: liboracle.so (or_*: 32-bit intervals, the reference's bwtint_t,
+ * 2BWT-Interface.h:26) and, with -DOR_WIDE, liboracle64.so (or64_*: the same
+ * algorithm with 64-bit intervals, for texts of 2^32 characters or more, which the
+ * reference cannot index -- config 5).  The 64-bit build is pinned against the
+ * 32-bit one on the same sub-2^32 indexes (tests/test_oracle.py).
  */
 #include "hsa_oracle.h"
 
@@ -15,6 +21,22 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#ifdef OR_WIDE
+typedef uint64_t bw_t;     /* SA interval bound */
+typedef int64_t cnt_t;     /* best_cnt (int in bwtgap.c:127) */
+#define OR(name) or64_##name
+#define HW 14              /* hsa_aln64_t words */
+#define H_START 10
+#define H_END 11
+#else
+typedef uint32_t bw_t;
+typedef int cnt_t;
+#define OR(name) or_##name
+#define HW 9               /* bwt_aln1_t words (bwtaln.h:41-50) */
+#define H_START 6
+#define H_END 7
+#endif
 
 #define MODE_GAPE 0x01
 #define MODE_LOGGAP 0x04
@@ -24,9 +46,9 @@
 #define ST_D 2
 
 typedef struct {
-    uint32_t T, isa0, C[5];
+    bw_t T, isa0, C[5];
     uint64_t *w;    /* $-less BWT, 32 codes per word, code j at bits 2j..2j+1 */
-    uint32_t *cnt;  /* cnt[b*4+c] = #c in codes [0, 32b) */
+    bw_t *cnt;      /* cnt[b*4+c] = #c in codes [0, 32b) */
 } or_bwt_t;
 
 /* rank queries issued by this thread (statistics only; thread-local so that threads
@@ -46,57 +68,71 @@ static uint32_t rev_pairs32(uint32_t x)   /* reverse the order of the 16 2-bit f
     return ((x & 0xCCCCCCCCu) >> 2) | ((x & 0x33333333u) << 2);
 }
 
-static void bwt_init(or_bwt_t *b, uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code)
+/* code: .bwt words, char j of a word at bits 31-2j..30-2j (BWT.c:156-181,
+ * BWTConstruct.c:1209); or, lsb != 0, LSB-first words (char j at bits 2j..2j+1, the
+ * device builder's output). */
+static void bwt_init(or_bwt_t *b, bw_t T, bw_t isa0, const bw_t C[5], const uint32_t *code, int lsb)
 {
-    /* .bwt words: char j of a word at bits 31-2j..30-2j (BWT.c:156-181, BWTConstruct.c:1209) */
     uint64_t nw = ((uint64_t)T + 31) / 32, ncw = ((uint64_t)T + 15) / 16;
     b->T = T; b->isa0 = isa0;
-    memcpy(b->C, C, 5 * sizeof(uint32_t));
+    memcpy(b->C, C, 5 * sizeof(bw_t));
     b->w = (uint64_t *)calloc(nw + 1, sizeof(uint64_t));
-    b->cnt = (uint32_t *)calloc((nw + 2) * 4, sizeof(uint32_t));
+    b->cnt = (bw_t *)calloc((nw + 2) * 4, sizeof(bw_t));
     for (uint64_t q = 0; q < nw; ++q) {
-        uint64_t lo = rev_pairs32(code[2 * q]);
-        uint64_t hi = 2 * q + 1 < ncw ? rev_pairs32(code[2 * q + 1]) : 0;
+        uint64_t lo = lsb ? code[2 * q] : rev_pairs32(code[2 * q]);
+        uint64_t hi = 2 * q + 1 < ncw ? (lsb ? code[2 * q + 1] : rev_pairs32(code[2 * q + 1])) : 0;
         b->w[q] = lo | hi << 32;
     }
     if (T & 31) b->w[nw - 1] &= (1ull << (2 * (T & 31))) - 1;   /* BWTClearTrailingBwtCode */
-    uint32_t acc[4] = {0, 0, 0, 0};
+    bw_t acc[4] = {0, 0, 0, 0};
     for (uint64_t q = 0; q <= nw; ++q) {
         memcpy(b->cnt + q * 4, acc, sizeof acc);
         if (q == nw) break;
         uint64_t x = b->w[q], lo = x & 0x5555555555555555ull, hi = (x >> 1) & 0x5555555555555555ull;
         uint32_t n3 = (uint32_t)__builtin_popcountll(lo & hi);
         uint32_t n1 = (uint32_t)__builtin_popcountll(lo) - n3, n2 = (uint32_t)__builtin_popcountll(hi) - n3;
-        uint32_t valid = (q + 1) * 32 <= T ? 32u : (uint32_t)(T - q * 32);
+        uint32_t valid = (q + 1) * 32 <= (uint64_t)T ? 32u : (uint32_t)(T - q * 32);
         acc[0] += valid - n1 - n2 - n3; acc[1] += n1; acc[2] += n2; acc[3] += n3;
     }
 }
 
+#ifdef OR_WIDE
+or_index_t *or64_index_create(uint64_t T, uint64_t isa0, const uint64_t C[5], const uint32_t *code_lsb,
+                              uint64_t rT, uint64_t risa0, const uint64_t rC[5], const uint32_t *rcode_lsb)
+{
+    or_index_t *ix = (or_index_t *)calloc(1, sizeof(or_index_t));
+    bwt_init(&ix->f, T, isa0, C, code_lsb, 1);
+    bwt_init(&ix->r, rT, risa0, rC, rcode_lsb, 1);
+    return ix;
+}
+#else
 or_index_t *or_index_create(uint32_t T, uint32_t isa0, const uint32_t C[5], const uint32_t *code,
                             uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *rcode)
 {
     or_index_t *ix = (or_index_t *)calloc(1, sizeof(or_index_t));
-    bwt_init(&ix->f, T, isa0, C, code);
-    bwt_init(&ix->r, rT, risa0, rC, rcode);
+    bwt_init(&ix->f, T, isa0, C, code, 0);
+    bwt_init(&ix->r, rT, risa0, rC, rcode, 0);
     return ix;
 }
+#endif
 
-void or_index_free(or_index_t *ix)
+void OR(index_free)(or_index_t *ix)
 {
     if (!ix) return;
     free(ix->f.w); free(ix->f.cnt); free(ix->r.w); free(ix->r.cnt); free(ix);
 }
 
-void or_free(void *p) { free(p); }
+void OR(free)(void *p) { free(p); }
 
 /* BWTAllOccValue (BWT.c:793-837): $ is not encoded, so an index past inverseSa0
  * is shifted down by one (BWT.c:690); the sampled-Occ + SSE decode then equals the
  * prefix count #{p < i' : code[p] == c} (checked at every i in [0, T+1] on the
  * fixtures).  Here: prefix count at the 32-char word + popcount inside it. */
-static void occ4(const or_bwt_t *b, uint32_t i, uint32_t o[4])
+static void occ4(const or_bwt_t *b, bw_t i, bw_t o[4])
 {
     i -= (i > b->isa0);
-    uint32_t q = i >> 5, r = i & 31;
+    uint64_t q = i >> 5;
+    uint32_t r = (uint32_t)(i & 31);
     for (int c = 0; c < 4; ++c) o[c] = b->cnt[q * 4 + c];
     if (r) {
         uint64_t x = b->w[q] & ((1ull << (2 * r)) - 1);
@@ -108,11 +144,12 @@ static void occ4(const or_bwt_t *b, uint32_t i, uint32_t o[4])
     }
 }
 
-void or_occ4(const or_index_t *ix, int dir, uint32_t i, uint32_t occ[4])
+void OR(occ4)(const or_index_t *ix, int dir, bw_t i, bw_t occ[4])
 {
     occ4(dir ? &ix->r : &ix->f, i, occ);
 }
 
+#ifndef OR_WIDE   /* SA -> position: the 32-bit path only (hsa_sa.hip) */
 /* BWTPsiMinusValue (BWT.c:1142-1162) via BWTOccValueOnSpot (BWT.c:924-959): for
  * index != inverseSa0, i = index + 1 shifted past '$' (BWT.c:949), c = the BWT
  * character before i, result C[c] + Occ(c, i) (the count includes that character). */
@@ -169,12 +206,12 @@ void or_sa_position(const or_index_t *ix, const uint32_t *sa_values, uint32_t in
         }
     }
 }
+#endif
 
 /* BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235-272). */
-static void step_all(or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl,
-                     uint32_t ok[4], uint32_t ol[4], uint32_t ork[4], uint32_t orl[4])
+static void step_all(or_index_t *ix, bw_t k, bw_t l, bw_t rk, bw_t rl, bw_t ok[4], bw_t ol[4], bw_t ork[4], bw_t orl[4])
 {
-    uint32_t oL[4], oR[4], oC[4];
+    bw_t oL[4], oR[4], oC[4];
     (void)rk;
     occ4(&ix->f, k, oL);
     occ4(&ix->f, l + 1, oR);
@@ -189,26 +226,25 @@ static void step_all(or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint32
     }
 }
 
-void or_step_all(const or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl,
-                 uint32_t ok[4], uint32_t ol[4], uint32_t ork[4], uint32_t orl[4])
+void OR(step_all)(const or_index_t *ix, bw_t k, bw_t l, bw_t rk, bw_t rl, bw_t ok[4], bw_t ol[4], bw_t ork[4],
+                   bw_t orl[4])
 {
     step_all((or_index_t *)ix, k, l, rk, rl, ok, ol, ork, orl);
 }
 
 /* BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170): one character. */
-static void step1(or_index_t *ix, uint32_t c, uint32_t *k, uint32_t *l, uint32_t *rk, uint32_t *rl)
+static void step1(or_index_t *ix, uint32_t c, bw_t *k, bw_t *l, bw_t *rk, bw_t *rl)
 {
-    uint32_t ok[4], ol[4], ork[4], orl[4];
+    bw_t ok[4], ol[4], ork[4], orl[4];
     step_all(ix, *k, *l, *rk, *rl, ok, ol, ork, orl);
     *k = ok[c]; *l = ol[c]; *rk = ork[c]; *rl = orl[c];
 }
 
 /* bwt_match_exact (2BWT-Interface.c:365-388), including the write-back guard
  * (:383-386): an output is only written if its incoming value is non-zero (Q1). */
-static int match_exact(or_index_t *ix, const uint8_t *seq, int len,
-                       uint32_t *sk, uint32_t *sl, uint32_t *srk, uint32_t *srl)
+static int match_exact(or_index_t *ix, const uint8_t *seq, int len, bw_t *sk, bw_t *sl, bw_t *srk, bw_t *srl)
 {
-    uint32_t k = *sk, l = *sl, rk = *srk, rl = *srl;
+    bw_t k = *sk, l = *sl, rk = *srk, rl = *srl;
     for (int i = len - 1; i >= 0; i--) {
         if (seq[i] > 3) return 0;
         step1(ix, seq[i], &k, &l, &rk, &rl);
@@ -224,14 +260,14 @@ static int match_exact(or_index_t *ix, const uint8_t *seq, int len,
 
 /* bwt_cal_width, type 1 (bwtaln.c:73-98): forward extension on the REVERSE BWT
  * with the FORWARD C[] (BWTSARangeForeward, 2BWT-Interface.c:121-132). */
-static int cal_width(or_index_t *ix, int len, const uint8_t *str, uint32_t *w)
+static int cal_width(or_index_t *ix, int len, const uint8_t *str, bw_t *w)
 {
-    uint32_t k = 0, l = ix->f.T;
+    bw_t k = 0, l = ix->f.T;
     int bid = 0;
     for (int i = 0; i < len; ++i) {
         uint8_t c = str[i];
         if (c < 4) {
-            uint32_t a[4], b[4];
+            bw_t a[4], b[4];
             occ4(&ix->r, k, a);
             occ4(&ix->r, l + 1, b);
             tl_queries += 2;
@@ -240,19 +276,19 @@ static int cal_width(or_index_t *ix, int len, const uint8_t *str, uint32_t *w)
         }
         if (k > l || c > 3) { k = 0; l = ix->f.T; ++bid; }
         w[2 * i] = l - k + 1;
-        w[2 * i + 1] = (uint32_t)bid;
+        w[2 * i + 1] = (bw_t)bid;
     }
     w[2 * len] = 0;
-    w[2 * len + 1] = (uint32_t)++bid;
+    w[2 * len + 1] = (bw_t)++bid;
     return bid;
 }
 
-int or_cal_width(const or_index_t *ix, int len, const uint8_t *str, uint32_t *width)
+int OR(cal_width)(const or_index_t *ix, int len, const uint8_t *str, bw_t *width)
 {
     return cal_width((or_index_t *)ix, len, str, width);
 }
 
-void or_init_opt(or_opt_t *o)
+void OR(init_opt)(or_opt_t *o)
 {
     memset(o, 0, sizeof *o);
     o->s_mm = 3; o->s_gapo = 11; o->s_gape = 4;
@@ -263,7 +299,7 @@ void or_init_opt(or_opt_t *o)
     o->fnr = 0.04f; o->n_threads = 1; o->max_top2 = 30; o->trim_qual = 0;
 }
 
-int or_cal_maxdiff(int l, double err, double thres)
+int OR(cal_maxdiff)(int l, double err, double thres)
 {
     double elambda = exp(-l * err);
     double sum, y = 1.0;
@@ -281,7 +317,7 @@ int or_cal_maxdiff(int l, double err, double thres)
 typedef struct {
     uint32_t info;          /* score<<21 | i */
     uint8_t n_mm, n_gapo, n_gape, state;
-    uint32_t k, l, rk, rl;
+    bw_t k, l, rk, rl;
     int last_diff_pos;
 } ent_t;
 typedef struct { int n, m; ent_t *a; } bucket_t;
@@ -310,7 +346,7 @@ static void stack_reset(stack_t_ *s)
     s->best = s->n_stacks; s->n_entries = 0;
 }
 
-static void push(stack_t_ *s, int i, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl,
+static void push(stack_t_ *s, int i, bw_t k, bw_t l, bw_t rk, bw_t rl,
                  int n_mm, int n_gapo, int n_gape, int state, int is_diff, const or_opt_t *o)
 {
     int score = SCORE(o, n_mm, n_gapo, n_gape);
@@ -343,12 +379,12 @@ static void pop(stack_t_ *s, ent_t *e)
 }
 
 /* gap_shadow (bwtgap.c:94-105) */
-static void shadow(uint32_t x, uint32_t max, int last_diff_pos, uint32_t *w)
+static void shadow(bw_t x, bw_t max, int last_diff_pos, bw_t *w)
 {
     int j = 0;
     for (int i = 0; i < last_diff_pos; ++i) {
         if (w[2 * i] > x) w[2 * i] -= x;
-        else if (w[2 * i] == x) { w[2 * i + 1] = 1; w[2 * i] = max - (uint32_t)(++j); }
+        else if (w[2 * i] == x) { w[2 * i + 1] = 1; w[2 * i] = max - (bw_t)(++j); }
     }
 }
 
@@ -363,24 +399,60 @@ static int int_log2(uint32_t v)   /* bwtgap.c:107-116 */
     return c;
 }
 
-typedef struct { int n, m; uint32_t *a; } hitv_t;   /* 9 words per hit */
+typedef struct { int n, m; uint32_t *a; } hitv_t;   /* HW words per hit */
+
+/* one hit record: bwt_aln1_t (bwtaln.h:41-50), or hsa_aln64_t (include/hsa_gpu.h) */
+static void put_hit(uint32_t *p, const ent_t *e, bw_t k, bw_t l, bw_t rk, bw_t rl, int strand, int score)
+{
+    memset(p, 0, HW * sizeof(uint32_t));
+    p[0] = (uint32_t)e->n_mm | (uint32_t)e->n_gapo << 16 | (uint32_t)e->n_gape << 24;
+#ifdef OR_WIDE
+    const bw_t v[4] = {k, l, rk, rl};
+    p[1] = (uint32_t)(strand & 3) << 30;            /* type 0 */
+    for (int j = 0; j < 4; ++j) { p[2 + 2 * j] = (uint32_t)v[j]; p[3 + 2 * j] = (uint32_t)(v[j] >> 32); }
+    p[12] = (uint32_t)score;
+#else
+    p[1] = k; p[2] = l; p[3] = rk; p[4] = rl;
+    p[5] = (uint32_t)(strand & 3) << 30;            /* type 0 */
+    p[8] = (uint32_t)score;
+#endif
+}
+
+static bw_t hit_k(const uint32_t *p)
+{
+#ifdef OR_WIDE
+    return (uint64_t)p[2] | (uint64_t)p[3] << 32;
+#else
+    return p[1];
+#endif
+}
+
+static bw_t hit_l(const uint32_t *p)
+{
+#ifdef OR_WIDE
+    return (uint64_t)p[4] | (uint64_t)p[5] << 32;
+#else
+    return p[2];
+#endif
+}
 
 /* bwt_match_gap (bwtgap.c:118-331).  width/width_seed are 2*(len+1) word arrays. */
 static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const uint8_t *seq, int len,
-                      int strand, uint32_t *width, const uint32_t *width_seed, hitv_t *out,
+                      int strand, bw_t *width, const bw_t *width_seed, hitv_t *out,
                       uint64_t *pops)
 {
     int best_score = SCORE(opt, opt->max_diff + 1, opt->max_gapo + 1, opt->max_gape + 1);
     int best_diff = opt->max_diff + 1, max_diff = opt->max_diff;
-    int best_cnt = 0, n_aln = 0;
-    const uint32_t T = ix->f.T;
+    cnt_t best_cnt = 0;
+    int n_aln = 0;
+    const bw_t T = ix->f.T;
     out->n = 0;
     stack_reset(st);
     push(st, len, 0, T, 0, T, 0, 0, 0, 0, 0, opt);
     while (st->n_entries) {
         ent_t e;
         int i, m, m_seed = 0, hit = 0, allow_diff, allow_M, tmp;
-        uint32_t k, l, rk, rl, sk[4], sl[4], srk[4], srl[4], occ;
+        bw_t k, l, rk, rl, sk[4], sl[4], srk[4], srl[4], occ;
         if (st->n_entries > opt->max_entries) break;
         pop(st, &e);
         if (pops) ++*pops;
@@ -410,26 +482,21 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
                 if (!(opt->mode & MODE_NONSTOP))
                     max_diff = (best_diff + 1 > opt->max_diff) ? opt->max_diff : best_diff + 1;
             }
-            if (score == best_score) best_cnt += (int)(l - k + 1);
+            if (score == best_score) best_cnt += (cnt_t)(l - k + 1);
             else if (best_cnt > opt->max_top2) break;
             if (e.n_gapo) {
                 int j;
                 for (j = 0; j != n_aln; ++j)
-                    if (out->a[9 * j + 1] == k && out->a[9 * j + 2] == l) break;
+                    if (hit_k(out->a + HW * j) == k && hit_l(out->a + HW * j) == l) break;
                 if (j < n_aln) do_add = 0;
             }
             if (do_add) {
                 shadow(l - k + 1, T, e.last_diff_pos, width);
                 if (out->n == out->m) {
                     out->m = out->m ? out->m * 2 : 16;
-                    out->a = (uint32_t *)realloc(out->a, sizeof(uint32_t) * 9 * out->m);
+                    out->a = (uint32_t *)realloc(out->a, sizeof(uint32_t) * HW * out->m);
                 }
-                uint32_t *p = out->a + 9 * out->n;
-                p[0] = (uint32_t)e.n_mm | (uint32_t)e.n_gapo << 16 | (uint32_t)e.n_gape << 24;
-                p[1] = k; p[2] = l; p[3] = rk; p[4] = rl;
-                p[5] = (uint32_t)(strand & 3) << 30;     /* type 0 */
-                p[6] = 0; p[7] = 0;
-                p[8] = (uint32_t)score;
+                put_hit(out->a + HW * out->n, &e, k, l, rk, rl, strand, score);
                 ++out->n; ++n_aln;
             }
             continue;
@@ -463,7 +530,7 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
                     push(st, i, k, l, rk, rl, e.n_mm, e.n_gapo, e.n_gape + 1, ST_I, 1, opt);
             } else if (e.state == ST_D) {
                 if (e.n_gape < opt->max_gape) {
-                    if (e.n_gape + e.n_gapo < max_diff || occ < (uint32_t)opt->max_del_occ) {
+                    if (e.n_gape + e.n_gapo < max_diff || occ < (bw_t)opt->max_del_occ) {
                         for (int j = 0; j != 4; ++j)
                             if (sk[j] <= sl[j])
                                 push(st, i + 1, sk[j], sl[j], srk[j], srl[j], e.n_mm, e.n_gapo, e.n_gape + 1, ST_D, 1, opt);
@@ -490,16 +557,16 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
  * (bwtgap.c:812, :919, :1192): the caller's widths, mutated in place by gap_shadow
  * (Q6); seed 0 = width_seed NULL, 1 = its own array, 2 = aliased to width
  * (bwtgap.c:809).  The stack has the caller's n_stacks (aux->stack). */
-int or_match_gap(const or_index_t *cix, const or_opt_t *opt, int n_stacks, const uint8_t *seq, int len, int strand,
-                 uint32_t *width, int seed, const uint32_t *width_seed, uint32_t **hits)
+int OR(match_gap)(const or_index_t *cix, const or_opt_t *opt, int n_stacks, const uint8_t *seq, int len, int strand,
+                  bw_t *width, int seed, const bw_t *width_seed, uint32_t **hits)
 {
     or_index_t *ix = (or_index_t *)cix;
     stack_t_ *st = stack_new(n_stacks);
     hitv_t hv = {0, 0, NULL};
-    const uint32_t *ws = seed == 2 ? width : seed == 1 ? width_seed : NULL;
+    const bw_t *ws = seed == 2 ? width : seed == 1 ? width_seed : NULL;
     match_gap(ix, st, opt, seq, len, strand, width, ws, &hv, NULL);
     stack_del(st);
-    *hits = hv.a ? hv.a : (uint32_t *)calloc(9, sizeof(uint32_t));
+    *hits = hv.a ? hv.a : (uint32_t *)calloc(HW, sizeof(uint32_t));
     return hv.n;
 }
 
@@ -513,7 +580,7 @@ static void revcomp(int len, const uint8_t *s, uint8_t *d)   /* seq_reverse(.., 
 
 /* bwa_cal_sa_reg_gap (bwtaln.c:246-417).  `opt` is the caller's option block and
  * is mutated exactly as the reference mutates it through aux->opt. */
-long or_cal_sa_reg_gap(const or_index_t *cix, int n, const uint32_t *lens, const uint8_t *codes,
+long OR(cal_sa_reg_gap)(const or_index_t *cix, int n, const uint32_t *lens, const uint8_t *codes,
                        or_opt_t *opt, int32_t *n_aln, uint32_t *flags, uint32_t **hits_out,
                        uint64_t *stats)
 {
@@ -524,11 +591,11 @@ long or_cal_sa_reg_gap(const or_index_t *cix, int n, const uint32_t *lens, const
     uint64_t pops = 0, q0 = tl_queries;
     opt->mode &= ~MODE_GAPE;               /* :261 */
     for (int i = 0; i < n; ++i) if ((int)lens[i] > max_len) max_len = (int)lens[i];
-    if (opt->fnr > 0.0) local.max_diff = or_cal_maxdiff(max_len, 0.02, opt->fnr);
+    if (opt->fnr > 0.0) local.max_diff = OR(cal_maxdiff)(max_len, 0.02, opt->fnr);
     if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;
     stack_t_ *st = stack_new(SCORE(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1));
-    uint32_t *wb = (uint32_t *)calloc(2 * (max_len + 1), sizeof(uint32_t));
-    uint32_t *ws = (uint32_t *)calloc(2 * (max_len + 1), sizeof(uint32_t));
+    bw_t *wb = (bw_t *)calloc(2 * (max_len + 1), sizeof(bw_t));
+    bw_t *ws = (bw_t *)calloc(2 * (max_len + 1), sizeof(bw_t));
     uint8_t *rc = (uint8_t *)calloc(max_len + 1, 1);
     hitv_t hv = {0, 0, NULL}, all = {0, 0, NULL};
     size_t off = 0;
@@ -546,7 +613,7 @@ long or_cal_sa_reg_gap(const or_index_t *cix, int n, const uint32_t *lens, const
             for (int j = 0; j < 15; ++j) { a &= seq[j] == 0; t &= seq[j] == 3; }
             if (a || t) continue;
         }
-        if (opt->fnr > 0.0) cur->max_diff = or_cal_maxdiff(len, 0.02, opt->fnr);   /* :330-331 */
+        if (opt->fnr > 0.0) cur->max_diff = OR(cal_maxdiff)(len, 0.02, opt->fnr);   /* :330-331 */
         cur->seed_len = opt->seed_len < len ? opt->seed_len : 0x7fffffff;          /* :332 */
         revcomp(len, seq, rc);
         int found = 0;
@@ -566,18 +633,18 @@ long or_cal_sa_reg_gap(const or_index_t *cix, int n, const uint32_t *lens, const
             cur = &local;
             continue;
         }
-        hv.a[6] = 0; hv.a[7] = (uint32_t)(len - 1);                   /* :371-372 */
+        hv.a[H_START] = 0; hv.a[H_END] = (uint32_t)(len - 1);         /* :371-372 */
         n_aln[r] = found;
         if (all.n + found > all.m) {
             all.m = (all.n + found) * 2 + 16;
-            all.a = (uint32_t *)realloc(all.a, sizeof(uint32_t) * 9 * all.m);
+            all.a = (uint32_t *)realloc(all.a, sizeof(uint32_t) * HW * all.m);
         }
-        memcpy(all.a + 9 * all.n, hv.a, sizeof(uint32_t) * 9 * found);
+        memcpy(all.a + HW * all.n, hv.a, sizeof(uint32_t) * HW * found);
         all.n += found;
     }
     free(wb); free(ws); free(rc); free(hv.a);
     stack_del(st);
     if (stats) { stats[0] = tl_queries - q0; stats[1] = pops; }
-    *hits_out = all.a ? all.a : (uint32_t *)calloc(9, sizeof(uint32_t));
+    *hits_out = all.a ? all.a : (uint32_t *)calloc(HW, sizeof(uint32_t));
     return all.n;
 }

@@ -73,6 +73,26 @@ int or_match_gap(const or_index_t *ix, const or_opt_t *opt, int n_stacks, const 
                  uint32_t *width, int seed, const uint32_t *width_seed, uint32_t **hits);
 void or_free(void *p);
 
+/* ---- liboracle64.so (hsa_oracle.c built with -DOR_WIDE): the same functions with
+ * 64-bit intervals (texts of 2^32 characters or more; the reference's bwtint_t is
+ * 32-bit, 2BWT-Interface.h:26).  Codes are LSB-first 2-bit words (16 per u32, the
+ * device builder's layout); widths are 2*(len+1) u64 {w, bid}; hits are 14 u32 per
+ * record in hsa_aln64_t layout (include/hsa_gpu.h). */
+or_index_t *or64_index_create(uint64_t T, uint64_t isa0, const uint64_t C[5], const uint32_t *code_lsb,
+                              uint64_t rT, uint64_t risa0, const uint64_t rC[5], const uint32_t *rcode_lsb);
+void or64_index_free(or_index_t *ix);
+void or64_occ4(const or_index_t *ix, int dir, uint64_t i, uint64_t occ[4]);
+void or64_step_all(const or_index_t *ix, uint64_t k, uint64_t l, uint64_t rk, uint64_t rl,
+                   uint64_t ok[4], uint64_t ol[4], uint64_t ork[4], uint64_t orl[4]);
+int or64_cal_width(const or_index_t *ix, int len, const uint8_t *str, uint64_t *width);
+void or64_init_opt(or_opt_t *o);
+int or64_cal_maxdiff(int l, double err, double thres);
+long or64_cal_sa_reg_gap(const or_index_t *ix, int n, const uint32_t *lens, const uint8_t *codes,
+                         or_opt_t *opt, int32_t *n_aln, uint32_t *flags, uint32_t **hits, uint64_t *stats);
+int or64_match_gap(const or_index_t *ix, const or_opt_t *opt, int n_stacks, const uint8_t *seq, int len, int strand,
+                   uint64_t *width, int seed, const uint64_t *width_seed, uint32_t **hits);
+void or64_free(void *p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+LIB64 = os.path.join(ROOT, "oracle", "liboracle64.so")   # the same restatement, 64-bit intervals
 
 OPT_FIELDS = [("s_mm", C.c_int), ("s_gapo", C.c_int), ("s_gape", C.c_int), ("mode", C.c_int),
               ("indel_end_skip", C.c_int), ("max_del_occ", C.c_int), ("max_entries", C.c_int),
@@ -66,6 +67,47 @@ def lib():
                                      C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
+
+
+_lib64 = None
+
+
+def lib64():
+    global _lib64
+    if _lib64 is None:
+        if not os.path.exists(LIB64):
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "liboracle64.so"], check=True,
+                           capture_output=True)
+        L = C.CDLL(LIB64)
+        u32p = np.ctypeslib.ndpointer(np.uint32, flags="C")
+        u64p = np.ctypeslib.ndpointer(np.uint64, flags="C")
+        L.or64_index_create.restype = C.c_void_p
+        L.or64_index_create.argtypes = [C.c_uint64, C.c_uint64, u64p, u32p, C.c_uint64, C.c_uint64, u64p, u32p]
+        L.or64_index_free.argtypes = [C.c_void_p]
+        L.or64_occ4.argtypes = [C.c_void_p, C.c_int, C.c_uint64, u64p]
+        L.or64_step_all.argtypes = [C.c_void_p] + [C.c_uint64] * 4 + [u64p] * 4
+        L.or64_cal_width.argtypes = [C.c_void_p, C.c_int, np.ctypeslib.ndpointer(np.uint8, flags="C"), u64p]
+        L.or64_cal_sa_reg_gap.restype = C.c_long
+        L.or64_cal_sa_reg_gap.argtypes = [C.c_void_p, C.c_int, u32p, np.ctypeslib.ndpointer(np.uint8, flags="C"),
+                                          C.POINTER(Opt), np.ctypeslib.ndpointer(np.int32, flags="C"), u32p,
+                                          C.POINTER(C.POINTER(C.c_uint32)), np.ctypeslib.ndpointer(np.uint64, flags="C")]
+        L.or64_free.argtypes = [C.c_void_p]
+        _lib64 = L
+    return _lib64
+
+
+def msb_to_lsb(code, T):
+    """.bwt words (char j at bits 31-2j..30-2j) -> LSB-first words (char j at bits
+    2j..2j+1), the trailing codes past T cleared."""
+    x = np.ascontiguousarray(code, np.uint32).copy()
+    x = (x >> 16) | (x << 16)
+    x = ((x & 0xFF00FF00) >> 8) | ((x & 0x00FF00FF) << 8)
+    x = ((x & 0xF0F0F0F0) >> 4) | ((x & 0x0F0F0F0F) << 4)
+    x = ((x & 0xCCCCCCCC) >> 2) | ((x & 0x33333333) << 2)
+    x = x.astype(np.uint32)
+    if T % 16:
+        x[-1] &= np.uint32((1 << (2 * (T % 16))) - 1)
+    return x
 
 
 def default_opt():
@@ -154,3 +196,71 @@ class OracleIndex:
         hits = np.concatenate([o[2] for o in outs]) if outs else np.zeros((0, 9), np.uint32)
         stats = sum(o[3] for o in outs)
         return n_aln, flags, hits, stats
+
+
+class OracleIndex64:
+    """liboracle64.so: the restatement with 64-bit intervals over LSB-first codes."""
+
+    HW = 14
+
+    def __init__(self, T, isa0, Cf, code_lsb, rT, risa0, Cr, rcode_lsb):
+        self.T = int(T)
+        self.h = lib64().or64_index_create(int(T), int(isa0), np.ascontiguousarray(Cf, np.uint64),
+                                           np.ascontiguousarray(code_lsb, np.uint32), int(rT), int(risa0),
+                                           np.ascontiguousarray(Cr, np.uint64), np.ascontiguousarray(rcode_lsb, np.uint32))
+
+    @classmethod
+    def from_index(cls, fwd, rev):
+        """From index_io BWT objects (.bwt MSB-first words)."""
+        return cls(fwd.T, fwd.isa0, np.asarray(fwd.C, np.uint64), msb_to_lsb(fwd.code, fwd.T), rev.T, rev.isa0,
+                   np.asarray(rev.C, np.uint64), msb_to_lsb(rev.code, rev.T))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib64().or64_index_free(self.h)
+            self.h = None
+
+    def occ4(self, d, i):
+        o = np.zeros(4, np.uint64)
+        lib64().or64_occ4(self.h, d, int(i), o)
+        return o
+
+    def step_all(self, k, l, rk, rl):
+        out = [np.zeros(4, np.uint64) for _ in range(4)]
+        lib64().or64_step_all(self.h, int(k), int(l), int(rk), int(rl), *out)
+        return out
+
+    def cal_width(self, seq):
+        seq = np.ascontiguousarray(seq, np.uint8)
+        w = np.zeros(2 * (len(seq) + 1), np.uint64)
+        lib64().or64_cal_width(self.h, len(seq), seq, w)
+        return w.reshape(-1, 2)
+
+    def cal_sa_reg_gap(self, lens, codes, opt: Opt):
+        """One batch; returns (n_aln, flags, hits(H,14), stats[queries, pops]); mutates opt."""
+        n = len(lens)
+        n_aln = np.zeros(n, np.int32)
+        flags = np.zeros(n, np.uint32)
+        stats = np.zeros(2, np.uint64)
+        hp = C.POINTER(C.c_uint32)()
+        tot = lib64().or64_cal_sa_reg_gap(self.h, n, np.ascontiguousarray(lens, np.uint32),
+                                           np.ascontiguousarray(codes, np.uint8), C.byref(opt),
+                                           n_aln, flags, C.byref(hp), stats)
+        hits = np.ctypeslib.as_array(hp, shape=(max(tot, 1) * 14,))[:tot * 14].reshape(tot, 14).copy()
+        lib64().or64_free(hp)
+        return n_aln, flags, hits, stats
+
+
+def aln64_to_aln32(h64):
+    """hsa_aln64_t rows (14 u32) -> bwt_aln1_t rows (9 u32) when every interval bound
+    fits 32 bits (sub-2^32 parity between the two instantiations)."""
+    h64 = np.asarray(h64, np.uint32).reshape(-1, 14)
+    assert not h64[:, [3, 5, 7, 9]].any(), "interval bound >= 2^32"
+    out = np.zeros((len(h64), 9), np.uint32)
+    out[:, 0] = h64[:, 0]
+    out[:, 1:5] = h64[:, [2, 4, 6, 8]]
+    out[:, 5] = h64[:, 1]
+    out[:, 6] = h64[:, 10]
+    out[:, 7] = h64[:, 11]
+    out[:, 8] = h64[:, 12]
+    return out

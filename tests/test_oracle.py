@@ -123,3 +123,66 @@ def test_sa_position_matches_reference(name):
     assert np.array_equal(got[:, 1], g["seq_id"])
     assert np.array_equal(got[:, 2], g["ori_pos"])
     assert np.array_equal(got[:, 3], g["occ_pos"])
+
+
+# ---- the 64-bit restatement (liboracle64.so, -DOR_WIDE): pinned against the 32-bit
+# one and the reference's golden vectors on the sub-2^32 indexes
+_IDX64 = {}
+
+
+def oracle_index64(name):
+    from oracle_ctypes import OracleIndex64
+    if name not in _IDX64:
+        _IDX64[name] = OracleIndex64.from_index(*index_io.read_index(INDEX[name]))
+    return _IDX64[name]
+
+
+def test_oracle64_occ_step_width_equal_32():
+    fwd, rev = index_io.read_index(INDEX["rep"])
+    o32, o64 = oracle_index("rep"), oracle_index64("rep")
+    for d, b in enumerate((fwd, rev)):
+        for i in list(range(0, 300)) + list(range(b.T - 200, b.T + 2)) + [b.isa0, b.isa0 + 1]:
+            assert np.array_equal(o64.occ4(d, i), o32.occ4(d, i).astype(np.uint64)), (d, i)
+    T = fwd.T
+    k, l, rk, rl = 0, T, 0, T
+    rng = np.random.default_rng(11)
+    for _ in range(500):
+        a = o32.step_all(k, l, rk, rl)
+        b = o64.step_all(k, l, rk, rl)
+        for x, y in zip(a, b):
+            assert np.array_equal(x.astype(np.uint64), y)
+        c = int(rng.integers(4))
+        if a[0][c] > a[1][c] or rng.random() < 0.05:
+            k, l, rk, rl = 0, T, 0, T
+        else:
+            k, l, rk, rl = (int(v[c]) for v in a)
+    g = np.load(f"{GOLD}/tiny_width.npz")
+    o32, o64 = oracle_index("tiny"), oracle_index64("tiny")
+    o = 0
+    for L in g["lens"][:50]:
+        seq = g["codes"][o:o + int(L)]
+        o += int(L)
+        assert np.array_equal(o64.cal_width(seq), o32.cal_width(seq).astype(np.uint64))
+
+
+@pytest.mark.parametrize("name", sorted(cases().keys()))
+def test_oracle64_batch_matches_reference(name):
+    """bwa_cal_sa_reg_gap with 64-bit intervals on every golden case: the reference's
+    hits, widened to hsa_aln64_t (bwt_aln1_t fields, 64-bit k/l/rev_k/rev_l)."""
+    from oracle_ctypes import Opt, aln64_to_aln32
+    g = load_case(name)
+    ix = oracle_index64(g["index"])
+    opt = Opt.from_dict(parse_opts(g["args"], default_opt()))
+    offs = np.concatenate([[0], np.cumsum(g["lens"].astype(np.int64))])
+    ns, fs, hs = [], [], []
+    for b0 in range(0, len(g["lens"]), g["batch"]):      # bwa_aln_core's batches (bwtaln.c:477-506)
+        b1 = min(b0 + g["batch"], len(g["lens"]))
+        n_aln, flags, hits, _ = ix.cal_sa_reg_gap(g["lens"][b0:b1], g["codes"][offs[b0]:offs[b1]], opt)
+        ns.append(n_aln); fs.append(flags); hs.append(aln64_to_aln32(hits))
+    n_aln, flags, hits = np.concatenate(ns), np.concatenate(fs), np.concatenate(hs)
+    exp_splice = (g["flags"] & 1).astype(bool)
+    assert np.array_equal((flags & 1).astype(bool), exp_splice)
+    got = split_hits(n_aln, hits)
+    exp = split_hits(g["n_aln"], g["hits"])
+    bad = [i for i in range(len(got)) if not exp_splice[i] and not np.array_equal(got[i], exp[i])]
+    assert not bad, f"{len(bad)} reads differ, first {bad[:5]}"
