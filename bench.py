@@ -11,6 +11,11 @@ loop feeds 100 000 reads per call, bwtaln.c:477; that is fewer reads than the
 batches: INTEGRATION.md.)  Reads, job table and outputs are resident in HBM for
 the timed region; steps cycle over a few distinct read sets.
 
+--config 5 (BASELINE configs[4], the HBM-capacity stress): 250 bp reads against a
+synthetic ~15 Gbp plant-scale text, which the reference's 32-bit bwtint_t cannot
+index: the 64-bit interval instantiation (hsa_search_device64, hsa_aln64_t hits) over
+a device-built 64-bit index, parity against the 64-bit restatement (liboracle64.so).
+
 Multi-GPU (torch.distributed.run, one rank per GPU): every rank holds the whole
 index, searches its own K batches of reads (weak scaling, no collective on the data
 path), and the per-rank hit lists are gathered to rank 0 over RCCL after timing.
@@ -31,6 +36,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import hsa_amd  # noqa: E402,F401  (loads libhsa_gpu.so before torch: hsa_amd/_lib.py)
 
 GENOME_T = 3_000_000_005
+GENOME5_T = 15_000_000_003  # config 5: plant-scale, past 2^32
 GENOME_SEED = 1234
 RECORDS = 24
 READ_LEN = 100
@@ -65,6 +71,39 @@ def build_index(T, seed, device):
     gi = _lib.GpuIndex.from_device_codes(T, res[0][1], res[0][2], res[0][0].data_ptr(), T, res[1][1], res[1][2],
                                          res[1][0].data_ptr(), device=device)
     return gi, res
+
+
+def build_index64(T, seed, device):
+    """config 5: the 64-bit index (hsa_build_bwt_device64 + hsa_index_create_device64)."""
+    import torch
+    from hsa_amd import _lib
+    L = _lib.lib()
+    nw = (T + 15) // 16
+    text = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
+    _lib.check(L.hsa_synth_genome_device(device, T, seed, text.data_ptr()))
+    res = {}
+    for rev in (0, 1):
+        bw = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
+        isa0 = C.c_uint64()
+        Cc = np.zeros(5, np.uint64)
+        t0 = time.time()
+        _lib.check(L.hsa_build_bwt_device64(device, T, text.data_ptr(), rev, bw.data_ptr(), C.byref(isa0), Cc))
+        log(f"[bench] BWT{' (reverse)' if rev else ''} of {T} bp built on the device in {time.time() - t0:.1f} s "
+            f"(64-bit)")
+        res[rev] = (bw, int(isa0.value), Cc)
+    del text
+    torch.cuda.empty_cache()
+    gi = _lib.GpuIndex.from_device_codes64(T, res[0][1], res[0][2], res[0][0].data_ptr(), T, res[1][1], res[1][2],
+                                           res[1][0].data_ptr(), device=device)
+    return gi, res
+
+
+def host_oracle_index64(res, T):
+    """The 64-bit restatement's index (liboracle64.so) from the device-built BWTs."""
+    from oracle_ctypes import OracleIndex64
+    nw = (T + 15) // 16
+    w = [res[r][0][:nw].cpu().numpy().view(np.uint32) for r in (0, 1)]
+    return OracleIndex64(T, res[0][1], res[0][2], w[0], T, res[1][1], res[1][2], w[1])
 
 
 def host_oracle_index(res, T):
@@ -207,15 +246,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--genome", type=int, default=GENOME_T)
+    ap.add_argument("--genome", type=int, default=0, help="text length (default: hg19-sized; config 5: 15 Gbp)")
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--cpu-sample", type=int, default=20000, help="reads timed on the CPU restatement")
     ap.add_argument("--parity-sample", type=int, default=-1,
                     help="reads of the timed batch checked against the CPU restatement (-1: all of them; 0: none)")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
                     help="BASELINE.json config: 2 = 0-4 substitutions, -n 4 -o 0 (default, the metric's config); "
                          "3 = one 1-3 bp indel + 0-2 substitutions, -n 4 -o 1; "
-                         "4 = 150 bp spliced reads, -n 4 -o 1, main path + the splice path's seed searches")
+                         "4 = 150 bp spliced reads, -n 4 -o 1, main path + the splice path's seed searches; "
+                         "5 = 250 bp reads, 0-4 substitutions, -n 4 -o 0, 15 Gbp text, 64-bit intervals")
     ap.add_argument("--dropin", type=int, default=1, help="also time the host-array drop-in path (1) or not (0)")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0)
@@ -235,10 +275,12 @@ def main():
     device = torch.cuda.current_device()
     _lib.configure(a.waves, a.pool, 0)
 
-    T = a.genome
-    RL = 150 if a.config == 4 else READ_LEN
+    wide = a.config == 5                      # the 64-bit interval instantiation
+    T = a.genome or (GENOME5_T if wide else GENOME_T)
+    RL = {4: 150, 5: 250}.get(a.config, READ_LEN)
+    HW = _lib.ALN64_WORDS if wide else 9      # u32 words per hit record
     t0 = time.time()
-    gi, res = build_index(T, GENOME_SEED, device)
+    gi, res = (build_index64 if wide else build_index)(T, GENOME_SEED, device)
     log(f"[bench] rank {rank}: index ready ({gi.nbytes() / 2**30:.2f} GiB of rank blocks) in {time.time() - t0:.1f} s")
 
     # reads: rank r searches batches r, r+world, ... of one global stream (seed 5)
@@ -252,6 +294,8 @@ def main():
         gidx = j * world + rank
         if a.config == 2:
             reads, _ = synth.make_reads(genome, recs, a.batch, READ_LEN, 5 * 1_000_000 + gidx, max_mm=4)
+        elif a.config == 5:
+            reads, _ = synth.make_reads(genome, recs, a.batch, RL, 8 * 1_000_000 + gidx, max_mm=4)
         elif a.config == 4:  # SURVEY §8d config 4 (seed 7): exon A 40-110, GT..AG intron 200-5000
             reads, _ = synth.make_spliced_reads(genome, recs, a.batch, RL, 7 * 1_000_000 + gidx)
         else:   # SURVEY §8d config 3 reads (seed 6): one indel of 1-3 bp + 0-2 substitutions
@@ -263,7 +307,7 @@ def main():
     # bwa_cal_sa_reg_gap prologue on the host (bwtaln.c:254-337): -n 4 -o 0|1, fixed length.
     # The timed batches are steady-state batches (not the process's first): GAPE is
     # already cleared in the caller's block, so both option regimes coincide.
-    max_gapo = 0 if a.config == 2 else 1
+    max_gapo = 0 if a.config in (2, 5) else 1
     opt_str = f"-n 4 -o {max_gapo}"
     opt = GapOpt.default()
     opt.max_diff, opt.fnr, opt.max_gapo = 4, -1.0, max_gapo
@@ -286,7 +330,7 @@ def main():
         outs.append(dict(n=torch.zeros(a.batch, dtype=torch.int32, device="cuda"),
                          f=torch.zeros(a.batch, dtype=torch.int32, device="cuda"),
                          o=torch.zeros(a.batch, dtype=torch.int64, device="cuda"),
-                         h=torch.zeros(hit_cap * 9, dtype=torch.int32, device="cuda"),
+                         h=torch.zeros(hit_cap * HW, dtype=torch.int32, device="cuda"),
                          c=torch.zeros(16, dtype=torch.int64, device="cuda")))
         if a.config == 4:   # the splice seeds: six records per read
             outs[-1].update(sn=torch.zeros(6 * a.batch, dtype=torch.int32, device="cuda"),
@@ -306,7 +350,7 @@ def main():
                         d_n_aln=o["n"].data_ptr(), d_flags=o["f"].data_ptr(), d_hit_off=o["o"].data_ptr(),
                         d_hits=o["h"].data_ptr(), hit_cap=hit_cap, d_counters=o["c"].data_ptr(),
                         max_len=RL, max_seed=opt.seed_len)
-        gi.search_device([rg], b)
+        (gi.search_device64 if wide else gi.search_device)([rg], b)
         if a.config == 4:   # same stream: the seeds read the main pass's flags
             gi.splice_seeds_device(srg, SeedBatch(
                 d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[j].data_ptr(), d_flags=o["f"].data_ptr(),
@@ -393,7 +437,7 @@ def main():
         nh_last = int(last["c"][1].item())
         gidx = (a.warmup + a.steps - 1) * world + rank          # global batch index of that launch
         res = {gidx: (last["n"].cpu().numpy(), last["f"].cpu().numpy().view(np.uint32), last["o"].cpu().numpy(),
-                      last["h"][:nh_last * 9].cpu().numpy().view(np.uint32).reshape(-1, 9))}
+                      last["h"][:nh_last * HW].cpu().numpy().view(np.uint32).reshape(-1, HW))}
         t0 = time.perf_counter()
         g = shard.gather_to_root(res, dist, torch.device("cuda", local))
         if rank == 0:
@@ -422,14 +466,16 @@ def main():
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64" if wide else "u32", "data": "synthetic",
             "config": {"workload": f"{a.batch // 1000}k x {RL}bp reads per step and GPU, "
                                    + {2: "0-4 substitutions", 3: "one 1-3 bp indel + 0-2 substitutions",
                                       4: "spliced (exon 40-110 bp, GT..AG intron 200-5000 bp), main path + the splice "
                                          "path's 6 seed searches per fallback read on the GPU (the host's "
-                                         "correlation/extension not included)"}[a.config]
-                                   + f", 50% rc, vs synthetic hg19-sized 2BWT ({T} bp, {RECORDS} records), {opt_str} "
-                                   f"(BASELINE configs[{a.config - 1}]); {a.steps} timed steps",
+                                         "correlation/extension not included)",
+                                      5: "0-4 substitutions, 64-bit SA intervals (hsa_search_device64)"}[a.config]
+                                   + f", 50% rc, vs synthetic {'plant-scale' if wide else 'hg19-sized'} 2BWT ({T} bp, "
+                                   f"{RECORDS} records), {opt_str} (BASELINE configs[{a.config - 1}]); "
+                                   f"{a.steps} timed steps",
                        "genome_bp": T, "reads_per_step": a.batch, "read_len": RL, "options": opt_str,
                        "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
             "roofline": {"bound": "hbm", "kernel": "k_search", "achieved": round(ach_search, 1), "peak": HBM_PEAK_GBS,
@@ -467,7 +513,7 @@ def main():
     # (flat form) on HOST arrays, the way a host HSA aln calls it -- reads copied in,
     # hits copied out and unpacked per read -- at the reference's 100 000 reads per
     # call (bwtaln.c:477) and at the whole 1 M-read batch per call
-    if rank == 0 and world == 1 and a.config != 4 and a.dropin:
+    if rank == 0 and world == 1 and a.config in (2, 3) and a.dropin:
         src = batches[0]
         dres = {}
         for per_call in (100_000, a.batch):
@@ -493,7 +539,7 @@ def main():
     # Python one by one)
     if rank == 0 and world == 1 and (a.parity_sample or a.cpu_sample):
         t0 = time.time()
-        ox = host_oracle_index(res, T)
+        ox = (host_oracle_index64 if wide else host_oracle_index)(res, T)
         log(f"[bench] CPU restatement index built in {time.time() - t0:.1f} s")
         from oracle_ctypes import Opt, default_opt
         od = default_opt()
@@ -504,7 +550,7 @@ def main():
         g_n = last["n"].cpu().numpy()
         g_f = last["f"].cpu().numpy().astype(np.uint32)
         g_o = last["o"].cpu().numpy()
-        g_h = last["h"].cpu().numpy().view(np.uint32).reshape(-1, 9)
+        g_h = last["h"].cpu().numpy().view(np.uint32).reshape(-1, HW)
         if a.config != 4 and a.parity_sample:
             n = a.batch if a.parity_sample < 0 else min(a.parity_sample, a.batch)
             threads = cpu["threads"]
@@ -514,8 +560,10 @@ def main():
             bad, first = compare_batch(g_n[:n], g_f[:n], g_o[:n], g_h, o_n, o_f, o_h)
             gq = int(outs[j0]["c"][2].item())
             result["parity_full" if n == a.batch else "parity_sample"] = {
-                "reads": n, "mismatching_reads": bad, "first_mismatch": first, "against": "oracle (C restatement)",
-                "fields": "n_aln, splice-fallback flag, every bwt_aln1_t field of every hit, hit order",
+                "reads": n, "mismatching_reads": bad, "first_mismatch": first,
+                "fields": f"n_aln, splice-fallback flag, every {'hsa_aln64_t' if wide else 'bwt_aln1_t'} field of "
+                          "every hit, hit order",
+                "against": "oracle (C restatement" + (", 64-bit intervals: liboracle64.so)" if wide else ")"),
                 "rank_queries_gpu": gq if n == a.batch else None, "rank_queries_oracle": int(o_q)}
             log(f"[bench] parity: {n} reads, {bad} differ from the CPU restatement; rank queries GPU "
                 f"{gq} vs oracle {int(o_q)} ({threads} threads, {dt:.1f} s)")

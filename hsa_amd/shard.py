@@ -88,15 +88,17 @@ def search_sharded(search, make_opt, opt0: dict, lens, codes, batch: int, world:
 
 
 def pack(res: dict) -> np.ndarray:
-    """Per-batch results as one int32 stream: [b, n, nh] + n_aln + flags + hits."""
+    """Per-batch results as one int32 stream: [b, n, nh, hw] + n_aln + flags + hits
+    (hw = words per hit record: 9 for bwt_aln1_t, 14 for hsa_aln64_t)."""
     parts = []
     for b in sorted(res):
         n_aln, flags, hoff, hits = res[b]
         n = len(n_aln)
+        hw = int(np.asarray(hits).shape[1]) if np.asarray(hits).ndim == 2 else 9
         # hits in read order (hit_off may point anywhere in the batch's hit array)
         order = [np.asarray(hits[int(hoff[j]):int(hoff[j]) + max(int(n_aln[j]), 0)], np.uint32) for j in range(n)]
-        h = np.concatenate(order) if order else np.zeros((0, 9), np.uint32)
-        parts += [np.array([b, n, len(h)], np.int32), np.asarray(n_aln, np.int32),
+        h = np.concatenate(order) if order else np.zeros((0, hw), np.uint32)
+        parts += [np.array([b, n, len(h), hw], np.int32), np.asarray(n_aln, np.int32),
                   np.asarray(flags, np.uint32).view(np.int32), h.reshape(-1).view(np.int32)]
     return np.concatenate(parts) if parts else np.zeros(0, np.int32)
 
@@ -104,14 +106,14 @@ def pack(res: dict) -> np.ndarray:
 def unpack(buf: np.ndarray) -> dict:
     out, i = {}, 0
     while i < len(buf):
-        b, n, nh = (int(x) for x in buf[i:i + 3])
-        i += 3
+        b, n, nh, hw = (int(x) for x in buf[i:i + 4])
+        i += 4
         n_aln = buf[i:i + n].copy()
         i += n
         flags = buf[i:i + n].view(np.uint32).copy()
         i += n
-        hits = buf[i:i + 9 * nh].view(np.uint32).reshape(nh, 9).copy()
-        i += 9 * nh
+        hits = buf[i:i + hw * nh].view(np.uint32).reshape(nh, hw).copy()
+        i += hw * nh
         out[b] = (n_aln, flags, hits)
     return out
 
