@@ -124,8 +124,10 @@ def host_oracle_index(res, T):
 
 
 # per-config PMC summaries (tools/profile_run.sh + tools/pmc_summary.py; config 4's in
-# its "step" mode, which sums the main path's and the splice seeds' kernels)
-TRAFFIC_SRCS = {2: "profiles/r01_pmc_summary.json", 3: "profiles/r01_pmc_summary_config3.json",
+# its "step" mode, which sums the main path's and the splice seeds' kernels); the
+# kernel-trace summaries next to them (tools/trace_summary.py) give the same runs'
+# per-launch durations
+TRAFFIC_SRCS = {2: "profiles/r02_pmc_summary_config2.json", 3: "profiles/r02_pmc_summary_config3.json",
                 4: "profiles/r01_pmc_summary_config4.json"}
 
 

@@ -19,9 +19,11 @@
 static thread_local char g_err[1024] = "";
 int g_waves_per_cu = 16;
 int g_pool_entries = 0;      // 0: 8192 per lane, 32768 when gap opens are allowed
-// k_search: waiting lanes per wave before the wave runs the strand-end / next-read
-// paths (HSA_BATCH_K overrides, for A/B runs)
-int g_batch_k = getenv("HSA_BATCH_K") ? atoi(getenv("HSA_BATCH_K")) : 16;
+// k_search: when a wave runs the strand-end / next-read paths of its waiting lanes:
+// at most HSA_BATCH_K waiting lanes, or HSA_BATCH_IDLE lane-iterations of waiting
+// (overrides for A/B runs)
+int g_batch_k = getenv("HSA_BATCH_K") ? atoi(getenv("HSA_BATCH_K")) : 32;
+int g_batch_idle = getenv("HSA_BATCH_IDLE") ? atoi(getenv("HSA_BATCH_IDLE")) : 768;
 int g_hit_cap = 64;
 
 void hsa_set_error(const char *fmt, ...)

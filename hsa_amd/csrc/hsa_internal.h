@@ -82,4 +82,5 @@ int hsa_need32(const hsa_index *ix);
 extern int g_waves_per_cu;
 extern int g_pool_entries;
 extern int g_batch_k;
+extern int g_batch_idle;
 extern int g_hit_cap;

@@ -106,7 +106,8 @@ struct SearchArgs {
     int32_t *cw;
     int32_t *wbid;
     uint32_t *wq;                  // k_widths: rank queries of each forward-strand width row
-    uint32_t batch_k;              // rare-event batching threshold (see (A) in k_search)
+    uint32_t batch_k;              // rare-event batching: at most this many lanes wait (see (A) in k_search)
+    uint32_t batch_idle;           //   ... or run once the waiting lanes have idled this many lane-iterations
 };
 
 // entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
@@ -506,6 +507,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     CT best_cnt = 0;
     uint32_t pool_top = 0;
     uint32_t free_head = NIL;      // HUGE: popped slots, linked through NXT
+    uint32_t idle_acc = 0;         // (A): lane-iterations the waiting lanes idled since the last batch
     BMask<MW> mask;
     // the current entry (k, l, rev_k, meta); between an expansion and the next pop
     // it holds the virtual top when C_VT is set (the last child pushed, when it is
@@ -754,11 +756,18 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         // The rare steps of a read -- copying its hits out (end_strand), the switch to
         // the forward strand with its row DMA, taking the next read -- are long code
         // paths that the whole wave executes whenever one lane needs one.  A lane that
-        // reaches one waits (PH_END / PH_IDLE) until batch_k lanes of the wave wait, or
-        // no lane is searching, and the wave then runs each path once for all of them.
+        // reaches one waits (PH_END / PH_IDLE) and the wave then runs each path once for
+        // all waiting lanes, when running it costs less than the waiting has (ski
+        // rental): once the waiting lanes have idled batch_idle lane-iterations since
+        // the last run (or batch_k lanes wait, or no lane is searching).  Reads that end
+        // often (config 2: ~430 pops per read) gather ~16 waiters first; long gapped
+        // searches (config 3: ~6 600 pops) run it with a few, instead of idling lanes
+        // for hundreds of iterations.
         const uint64_t wm = __ballot(C_PH(ctl) == PH_IDLE || C_PH(ctl) == PH_END);
-        if (wm && ((uint32_t)__popcll(wm) >= a.batch_k ||
+        idle_acc += (uint32_t)__popcll(wm);
+        if (wm && (idle_acc >= a.batch_idle || (uint32_t)__popcll(wm) >= a.batch_k ||
                    __ballot(C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END) == 0)) {
+            idle_acc = 0;
             if (C_PH(ctl) == PH_END) end_strand();
             const bool need = C_PH(ctl) == PH_IDLE;
             const uint64_t mb = __ballot(need);
@@ -1287,6 +1296,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.mm_buckets = ix->staged_mmb ? 1u : 0u;
     A.ntab = P.ntab;
     A.batch_k = (uint32_t)g_batch_k;
+    A.batch_idle = (uint32_t)g_batch_idle;
     A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0; A.ovf_ctr = 8;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;

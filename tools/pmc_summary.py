@@ -8,7 +8,10 @@ widths other than 16 B/lane streaming are uncalibrated): membench's k_indep
 issues a known number of random 64-byte block loads per dispatch; the ratio
 FETCH_SIZE*1024 / known bytes on that pattern is applied to k_search.
 
-usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>_pmc_summary.json [step]
+usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>_pmc_summary.json [step] [--cal DIR]
+
+--cal DIR takes the FETCH_SIZE calibration pass (pmc_membench) from another profile
+directory of the same box run; SQ / TCC passes are summarised when present.
 
 With "step", a step's traffic sums every kernel instantiation of the step, each as
 all its dispatches (overflow re-runs included) over its full-size launches: config
@@ -57,14 +60,20 @@ def med(agg, name):
 
 
 def main():
-    src, dst = sys.argv[1], sys.argv[2]
+    args = sys.argv[1:]
+    cal_dir = None
+    if "--cal" in args:
+        i = args.index("--cal")
+        cal_dir = args[i + 1]
+        del args[i:i + 2]
+    src, dst = args[0], args[1]
     out = {"source": src}
     # calibration on membench k_indep<1>: 1024 workgroups x 256 lanes x 2000 iterations x 64 B
-    mb, _ = counters(os.path.join(src, "pmc_membench"), "k_indep<1>")
+    mb, _ = counters(os.path.join(cal_dir or src, "pmc_membench"), "k_indep<1>")
     known = 256 * 16 // 4 * 256 * 2000 * 64
     cal = med(mb, "FETCH_SIZE") * 1024 / known
     out["fetch_calibration_random64"] = round(cal, 4)
-    launches = len(sys.argv) > 3 and sys.argv[3] == "step"
+    launches = len(args) > 2 and args[2] == "step"
     if launches:
         out["per_kernel"] = {}
         for k in STEP_KERNELS:
@@ -96,14 +105,15 @@ def main():
                                 "ms_median_pmc_pass": statistics.median(dur.values())}
     out["fetch_bytes_per_launch"] = sum(v["fetch_bytes"] for v in out["per_kernel"].values())
     out["write_bytes_per_launch"] = sum(v["write_bytes"] for v in out["per_kernel"].values())
-    sq, _ = counters(os.path.join(src, "pmc_sq"), "k_search")
-    wc = med(sq, "SQ_WAVE_CYCLES")
-    out["sq"] = {"wait_any_frac": med(sq, "SQ_WAIT_ANY") / wc,
-                 "active_inst_any_frac": med(sq, "SQ_ACTIVE_INST_ANY") / wc,
-                 "active_valu_frac": med(sq, "SQ_ACTIVE_INST_VALU") / wc,
-                 "vmem_rd_wave_insts": med(sq, "SQ_INSTS_VMEM_RD"),
-                 "waves": med(sq, "SQ_WAVES"),
-                 "grbm_gui_active_per_xcd": med(sq, "GRBM_GUI_ACTIVE") / 8}
+    if os.path.isdir(os.path.join(src, "pmc_sq")):
+        sq, _ = counters(os.path.join(src, "pmc_sq"), "k_search")
+        wc = med(sq, "SQ_WAVE_CYCLES")
+        out["sq"] = {"wait_any_frac": med(sq, "SQ_WAIT_ANY") / wc,
+                     "active_inst_any_frac": med(sq, "SQ_ACTIVE_INST_ANY") / wc,
+                     "active_valu_frac": med(sq, "SQ_ACTIVE_INST_VALU") / wc,
+                     "vmem_rd_wave_insts": med(sq, "SQ_INSTS_VMEM_RD"),
+                     "waves": med(sq, "SQ_WAVES"),
+                     "grbm_gui_active_per_xcd": med(sq, "GRBM_GUI_ACTIVE") / 8}
     tcc, _ = counters(os.path.join(src, "pmc_tcc"), "k_search")
     h, m = med(tcc, "TCC_HIT_sum"), med(tcc, "TCC_MISS_sum")
     out["tcc"] = {"hit_rate": h / (h + m), "ea_rdreq": med(tcc, "TCC_EA0_RDREQ_sum")}

@@ -17,9 +17,15 @@ pmc() {  # name, counters...
   local n=$1; shift
   timeout -s KILL 300 rocprofv3 --kernel-trace --pmc "$@" --kernel-include-regex "${PMC_REGEX:-k_search|k_widths}" --output-format csv -d $OUT/pmc_$n -o run -- python3 $BENCH > $OUT/pmc_$n.json 2> $OUT/pmc_$n.err || exit 12
 }
-pmc fetch FETCH_SIZE
-pmc write WRITE_SIZE
-pmc sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
-pmc tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum
-timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex k_indep --output-format csv -d $OUT/pmc_membench -o run -- $R/tools/membench 2147483648 16 > $OUT/pmc_membench.log 2>&1 || exit 13
+# PASSES selects the counter passes (default: all)
+PASSES=${PASSES:-"fetch write sq tcc membench"}
+for p in $PASSES; do
+  case $p in
+    fetch) pmc fetch FETCH_SIZE ;;
+    write) pmc write WRITE_SIZE ;;
+    sq) pmc sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE ;;
+    tcc) pmc tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum ;;
+    membench) timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex k_indep --output-format csv -d $OUT/pmc_membench -o run -- $R/tools/membench 2147483648 16 > $OUT/pmc_membench.log 2>&1 || exit 13 ;;
+  esac
+done
 echo done
