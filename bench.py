@@ -259,6 +259,9 @@ def main():
                          "4 = 150 bp spliced reads, -n 4 -o 1, main path + the splice path's seed searches; "
                          "5 = 250 bp reads, 0-4 substitutions, -n 4 -o 0, 15 Gbp text, 64-bit intervals")
     ap.add_argument("--dropin", type=int, default=1, help="also time the host-array drop-in path (1) or not (0)")
+    ap.add_argument("--intervals", type=int, default=0, choices=(0, 32, 64),
+                    help="SA interval width of the search (0: 64 for config 5, else 32); 64 on a sub-2^32 text "
+                         "and 32 with config 5's reads on one are A/B runs of the two instantiations")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0)
     a = ap.parse_args()
@@ -277,8 +280,8 @@ def main():
     device = torch.cuda.current_device()
     _lib.configure(a.waves, a.pool, 0)
 
-    wide = a.config == 5                      # the 64-bit interval instantiation
-    T = a.genome or (GENOME5_T if wide else GENOME_T)
+    wide = a.intervals == 64 or (a.intervals == 0 and a.config == 5)   # the 64-bit interval instantiation
+    T = a.genome or (GENOME5_T if a.config == 5 else GENOME_T)
     RL = {4: 150, 5: 250}.get(a.config, READ_LEN)
     HW = _lib.ALN64_WORDS if wide else 9      # u32 words per hit record
     t0 = time.time()
@@ -475,7 +478,7 @@ def main():
                                          "path's 6 seed searches per fallback read on the GPU (the host's "
                                          "correlation/extension not included)",
                                       5: "0-4 substitutions, 64-bit SA intervals (hsa_search_device64)"}[a.config]
-                                   + f", 50% rc, vs synthetic {'plant-scale' if wide else 'hg19-sized'} 2BWT ({T} bp, "
+                                   + f", 50% rc, vs synthetic {'plant-scale' if T >= 1 << 32 else 'hg19-sized'} 2BWT ({T} bp, "
                                    f"{RECORDS} records), {opt_str} (BASELINE configs[{a.config - 1}]); "
                                    f"{a.steps} timed steps",
                        "genome_bp": T, "reads_per_step": a.batch, "read_len": RL, "options": opt_str,

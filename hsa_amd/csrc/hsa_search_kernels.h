@@ -110,6 +110,18 @@ struct SearchArgs {
     uint32_t batch_idle;           //   ... or run once the waiting lanes have idled this many lane-iterations
 };
 
+// The kernel's arguments re-read from the kernarg segment where a rare path uses them
+// (strand start and end, next read, hit staging): the asm barrier keeps the compiler
+// from hoisting those loads out of the search loop, where holding every argument in
+// SGPRs across the loop forced SGPR spills (v_writelane / v_readlane round trips).
+typedef const __attribute__((address_space(4))) SearchArgs *ColdArgs;
+__device__ __forceinline__ ColdArgs cold_args()
+{
+    ColdArgs p = (ColdArgs)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
 // entry meta word: i:10 | state:2 | is_diff:1 | n_mm:7 | n_gapo:4 | n_gape:8
 __device__ __forceinline__ uint32_t meta_pack(uint32_t i, uint32_t st, uint32_t isd, uint32_t mm, uint32_t go,
                                               uint32_t ge)
@@ -165,26 +177,34 @@ template <typename IT> struct Ent {
     IT x, y, z;
     uint32_t w;
 };
+// Slot s of a lane's pool: uint4 element base + s * 64 (32-bit entries) or the two
+// elements base + s * 128 and base + s * 128 + 64 (64-bit entries); base (pool_base)
+// is the lane's slot 0, computed once per launch.
 template <typename IT>
-__device__ __forceinline__ Ent<IT> ent_load(const uint4 *pool, size_t idx, int lane)
+__device__ __forceinline__ size_t pool_base(size_t wv, uint32_t pcap, int lane)
+{
+    return (sizeof(IT) == 4 ? 1u : 2u) * wv * pcap * 64 + (size_t)lane;
+}
+template <typename IT>
+__device__ __forceinline__ Ent<IT> ent_load(const uint4 *pool, size_t base, uint32_t slot)
 {
     if constexpr (sizeof(IT) == 4) {
-        const uint4 v = pool[idx * 64 + lane];
+        const uint4 v = pool[base + (size_t)slot * 64];
         return Ent<IT>{v.x, v.y, v.z, v.w};
     } else {
-        const uint4 u = pool[(2 * idx) * 64 + lane], v = pool[(2 * idx + 1) * 64 + lane];
+        const uint4 u = pool[base + (size_t)slot * 128], v = pool[base + (size_t)slot * 128 + 64];
         return Ent<IT>{(uint64_t)u.x | (uint64_t)u.y << 32, (uint64_t)u.z | (uint64_t)u.w << 32,
                        (uint64_t)v.x | (uint64_t)v.y << 32, v.z};
     }
 }
 template <typename IT>
-__device__ __forceinline__ void ent_store(uint4 *pool, size_t idx, int lane, const Ent<IT> &e)
+__device__ __forceinline__ void ent_store(uint4 *pool, size_t base, uint32_t slot, const Ent<IT> &e)
 {
     if constexpr (sizeof(IT) == 4) {
-        pool[idx * 64 + lane] = make_uint4(e.x, e.y, e.z, e.w);
+        pool[base + (size_t)slot * 64] = make_uint4(e.x, e.y, e.z, e.w);
     } else {
-        pool[(2 * idx) * 64 + lane] = make_uint4((uint32_t)e.x, (uint32_t)(e.x >> 32), (uint32_t)e.y, (uint32_t)(e.y >> 32));
-        pool[(2 * idx + 1) * 64 + lane] = make_uint4((uint32_t)e.z, (uint32_t)(e.z >> 32), e.w, 0u);
+        pool[base + (size_t)slot * 128] = make_uint4((uint32_t)e.x, (uint32_t)(e.x >> 32), (uint32_t)e.y, (uint32_t)(e.y >> 32));
+        pool[base + (size_t)slot * 128 + 64] = make_uint4((uint32_t)e.z, (uint32_t)(e.z >> 32), e.w, 0u);
     }
 }
 // staged words per hit (HB) and words per output hit record: bwt_aln1_t (bwtaln.h:41-50)
@@ -485,8 +505,10 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     // (w * cap + e) * 64 + l, so one wave's accesses stay inside one small region
     // (few pages) and lanes at equal e coalesce
     const size_t wv = gid >> 6;
-#define NXT(s) reinterpret_cast<LT *>(a.nxt)[(wv * a.pcap + (uint32_t)(s)) * 64 + lane]
-#define HB(i) a.hbuf[(wv * a.hcap * HW + (uint32_t)(i)) * 64 + lane]
+    const size_t link0 = wv * a.pcap * 64 + (size_t)lane;        // the lane's slot-0 link
+    const size_t pbase = pool_base<IT>(wv, a.pcap, lane);        // ... and slot-0 pool entry
+#define NXT(s) reinterpret_cast<LT *>(a.nxt)[link0 + (size_t)(s) * 64]
+#define HB(i) r->hbuf[(wv * r->hcap * HW + (uint32_t)(i)) * 64 + lane]   // r = cold_args() in scope
 #define HEAD(b) s_heads[(uint32_t)(b) * NT + tid]
     // pruning elements in LDS, word-interleaved: the word holding elements
     // [EPW*q, EPW*q + EPW) of a lane is word q * NT + tid, so every lane reads its
@@ -513,8 +535,9 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     // it holds the virtual top when C_VT is set (the last child pushed, when it is
     // the next pop: it never goes to the pool)
     E e{0, 0, 0, 0};
-    uint32_t st_p = 0, st_wq = 0;
-    uint64_t st_q = 0, st_b = 0;          // wave-uniform (ballot counts)
+    // per-lane statistics (a lane's counts of one launch stay far below 2^32); kept in
+    // VGPRs: wave-uniform accumulators pushed the kernel's SGPRs into spills
+    uint32_t st_p = 0, st_wq = 0, st_q = 0, st_b = 0;
     const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
 #ifdef HSA_DIAG
     uint32_t dc[18] = {0};
@@ -551,9 +574,15 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             slot = pool_top++;
         }
         DC(8);
-        ent_store<IT>(a.pool, wv * a.pcap + slot, lane, v);
+        ent_store<IT>(a.pool, pbase, slot, v);
         const uint32_t old = mask.test(b) ? (uint32_t)HEAD(b) : NIL;
         NXT(slot) = (LT)old;
+#ifdef HSA_X_LINKSTORE2      // sensitivity experiment only: one more link store per push (into
+        if (!HUGE && pool_top < a.pcap) NXT(pool_top) = (LT)old;   // the next free slot: harmless)
+#endif
+#ifdef HSA_X_ENTSTORE2       // sensitivity experiment only: one more entry store per push
+        if (!HUGE && pool_top < a.pcap) ent_store<IT>(a.pool, pbase, pool_top, v);
+#endif
         HEAD(b) = (LT)slot;
         mask.set(b);
     };
@@ -578,15 +607,16 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         // LDS-DMA (global_load_lds_dword): word q of every active lane lands at
         // word q * NT + tid, which is exactly the wave's slice of the LDS layout, so
         // the whole row is in flight at once and one wait covers it
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.wb) + row_base(a.rb / 4);
+        const ColdArgs r = cold_args();
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(r->wb) + row_base(r->rb / 4);
         uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + (tid & ~63u);
-        const uint32_t nwb = a.rb / 4;                 // row capacity in words (uniform)
+        const uint32_t nwb = r->rb / 4;                // row capacity in words (uniform)
         for (uint32_t q = 0; q < nwb; ++q)
             __builtin_amdgcn_global_load_lds(src + q * 64, db + q * NT, 4, 0, 0);
         if (C_SEED(ctl) && !C_ALIAS(ctl)) {
-            const uint32_t *ss = reinterpret_cast<const uint32_t *>(a.ws) + row_base(a.rs / 4);
+            const uint32_t *ss = reinterpret_cast<const uint32_t *>(r->ws) + row_base(r->rs / 4);
             uint32_t *const ds = reinterpret_cast<uint32_t *>(s_ws) + (tid & ~63u);
-            const uint32_t nws = a.rs / 4;
+            const uint32_t nws = r->rs / 4;
             for (uint32_t q = 0; q < nws; ++q)
                 __builtin_amdgcn_global_load_lds(ss + q * 64, ds + q * NT, 4, 0, 0);
         }
@@ -607,25 +637,27 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         start_search();
     };
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
-        const int job = a.job_list ? a.job_list[qpos] : (int)qpos;
+        const ColdArgs r = cold_args();
+        const int job = r->job_list ? r->job_list[qpos] : (int)qpos;
         if (fl & HSA_F_OVERFLOW) {
-            if (a.ovf_list) a.ovf_list[atomicAdd(&a.ctr[a.ovf_ctr], 1ull)] = job;   // re-run by the next pass
-            else atomicAdd(&a.ctr[11], 1ull);                               // the last pass: stays unfinished
+            if (r->ovf_list) r->ovf_list[atomicAdd(&r->ctr[r->ovf_ctr], 1ull)] = job;   // re-run by the next pass
+            else atomicAdd(&r->ctr[11], 1ull);                                  // the last pass: stays unfinished
         }
-        a.n_aln[job] = na;
-        a.flags[job] = fl;
-        a.hit_off[job] = ho;
+        r->n_aln[job] = na;
+        r->flags[job] = fl;
+        r->hit_off[job] = ho;
         SET_PH(ctl, PH_IDLE);
     };
     auto end_strand = [&]() {
         if (n_aln > 0) {
-            const unsigned long long o = atomicAdd(&a.ctr[1], (unsigned long long)n_aln);
-            if (o + (uint64_t)n_aln > a.hit_cap) { finish_job(HSA_F_OVERFLOW, 0, 0); return; }
-            uint32_t *dst = a.hits + o * OW;
+            const ColdArgs r = cold_args();
+            const unsigned long long o = atomicAdd(&r->ctr[1], (unsigned long long)n_aln);
+            if (o + (uint64_t)n_aln > r->hit_cap) { finish_job(HSA_F_OVERFLOW, 0, 0); return; }
+            uint32_t *dst = r->hits + o * OW;
             const uint32_t s30 = C_STRAND(ctl) << 30;
             for (int h = 0; h < n_aln; ++h) {
                 // bwtaln.c:371-372 (a direct bwt_match_gap call leaves start/end 0)
-                const uint32_t end = h == 0 && !a.mg ? (uint32_t)(C_LEN(ctl) - 1) : 0u;
+                const uint32_t end = h == 0 && !r->mg ? (uint32_t)(C_LEN(ctl) - 1) : 0u;
                 if constexpr (sizeof(IT) == 4) {
                     // the six staged words first, then the record: one memory round trip per hit
                     const uint32_t v0 = HB(h * 9 + 0), v1 = HB(h * 9 + 1), v2 = HB(h * 9 + 2), v3 = HB(h * 9 + 3),
@@ -655,11 +687,11 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 }
             }
             finish_job(0, n_aln, o);
-        } else if (a.mg) {
+        } else if (cold_args()->mg) {
             finish_job(0, 0, 0);        // one call, one strand
         } else if (C_STRAND(ctl)) {
             ctl &= ~(1u << 3);          // strand 0
-            st_wq += a.wq[qpos];        // its widths are the reference's work now (bwtaln.c:344-348)
+            st_wq += cold_args()->wq[qpos];   // its widths are the reference's work now (bwtaln.c:344-348)
             start_strand();
         } else {
             finish_job(HSA_F_FALLBACK, 0, 0);
@@ -668,6 +700,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     // hit handling (bwtgap.c:188-243) for entry e with final interval (k,l,rk,rl);
     // returns false when the search must stop
     auto on_hit = [&](IT k, IT l, IT rk, IT rl) -> bool {
+        const ColdArgs r = cold_args();
         const uint32_t m = e.w;
         const int score = SCORE(M_MM(m), M_GO(m), M_GE(m));
         if (n_aln == 0) {
@@ -694,7 +727,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             }
         }
         if (add) {
-            if ((uint32_t)n_aln >= a.hcap) { ctl |= 1u << 8; return false; }
+            if ((uint32_t)n_aln >= r->hcap) { ctl |= 1u << 8; return false; }
             // gap_shadow (bwtgap.c:94-105) on width_back[0, last_diff_pos), then the
             // pruning elements of those positions (eq bit of p needs w[p+1])
             const IT x = l - k + 1u;
@@ -703,8 +736,8 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 #ifdef HSA_DIAG
                 DC(13); dc[14] += (uint32_t)ldp;
 #endif
-                IT *const wg = reinterpret_cast<IT *>(a.wg) + row_base(a.rg);
-                int32_t *const wd = a.wbid ? a.wbid + row_base(a.rg) : nullptr;
+                IT *const wg = reinterpret_cast<IT *>(r->wg) + row_base(r->rg);
+                int32_t *const wd = r->wbid ? r->wbid + row_base(r->rg) : nullptr;
 #define WG(p) wg[(uint32_t)(p) * 64]
                 IT jj = 0;
                 for (int p = 0; p < ldp; ++p) {
@@ -774,20 +807,21 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             if (mb) {
                 const int leader = __ffsll((unsigned long long)mb) - 1;
                 unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(&a.ctr[a.qctr], (unsigned long long)__popcll(mb));
+                const ColdArgs r = cold_args();
+                if (lane == leader) base = atomicAdd(&r->ctr[r->qctr], (unsigned long long)__popcll(mb));
                 base = __shfl(base, leader);
                 if (need) {
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
                     if (j < (unsigned long long)n_jobs) {
                         qpos = (uint32_t)j;
-                        const int job = a.job_list ? a.job_list[j] : (int)j;
-                        const hsa_job_t J = a.jobs[job];
+                        const int job = r->job_list ? r->job_list[j] : (int)j;
+                        const hsa_job_t J = r->jobs[job];
                         opt_max_diff = J.max_diff;
                         const uint32_t len = J.len;
-                        if (a.mg) {
+                        if (r->mg) {
                             // one direct bwt_match_gap call: its strand, its width_seed kind
                             // (host-checked: 0 <= seed_len <= len when width_seed is given)
-                            const hsa_mg_job_t M = a.mg[job];
+                            const hsa_mg_job_t M = r->mg[job];
                             const uint32_t has_seed = M.seed != HSA_SEED_NONE;
                             ctl = (uint32_t)(M.strand & 1) << 3 | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 |
                                   (M.seed == HSA_SEED_ALIAS ? 1u : 0u) << 7 | len << 10 |
@@ -831,7 +865,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             { const uint64_t em = __ballot(1); if (lane == __ffsll((unsigned long long)em) - 1) DC(7); }
 #endif
             if (C_OVF(ctl)) {
-                if (C_OVF(ctl) > 1) atomicAdd(&a.ctr[5], 1ull);
+                if (C_OVF(ctl) > 1) atomicAdd(&cold_args()->ctr[5], 1ull);
                 finish_job(HSA_F_OVERFLOW, 0, 0);
                 break;
             }
@@ -852,8 +886,11 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 // pop the head of the lowest non-empty bucket
                 const int b = mask.lowest();
                 const uint32_t slot = HEAD(b);
-                e = ent_load<IT>(a.pool, (size_t)wv * a.pcap + slot, lane);
+                e = ent_load<IT>(a.pool, pbase, slot);
                 const uint32_t nx = NXT(slot);
+#ifdef HSA_X_POPLOAD2        // sensitivity experiment only: one more link load per pool pop
+                if (*(volatile LT *)&NXT(slot) == (LT)0xFFFE && nx == 0x12345u) e.w ^= 1u;
+#endif
                 if (nx == NIL) mask.reset(b);
                 else HEAD(b) = (LT)nx;
                 if (HUGE) { NXT(slot) = (LT)free_head; free_head = slot; }
@@ -890,9 +927,9 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 #endif
         // ---------------- (C) the rank step
         IT oa[4], ob[4];
-        const uint64_t rq = __ballot(req);
 #ifdef HSA_DIAG
         {
+            const uint64_t rq = __ballot(req);
             if (lane == 0) dc[6] += (uint32_t)__popcll(rq);
             const uint32_t ph0 = C_PH(ctl);
             if (req) DC(ph0 == PH_EXACT ? 1 : 2);
@@ -901,8 +938,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 #endif
         uint32_t two = 0;
         if (req) two = occ_pair(Ix<IT>::fwd(a), rp1, rp2, oa, ob) - 1u;
-        st_q += 2u * (uint64_t)__popcll(rq);
-        st_b += (uint64_t)__popcll(rq) + (uint64_t)__popcll(__ballot(two));
+        if (req) { st_q += 2u; st_b += 1u + two; }
 
 #ifdef HSA_DIAG
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1048,10 +1084,8 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         for (int i = 0; i < 4; ++i) atomicAdd(&g_dctr[9 + i], (unsigned long long)tsec[i]);
 #endif
     // statistics
-    if (lane == 0) {
-        atomicAdd(&a.ctr[2], (unsigned long long)st_q);
-        atomicAdd(&a.ctr[3], (unsigned long long)st_b);
-    }
+    atomicAdd(&a.ctr[2], (unsigned long long)st_q);
+    atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);
     if (st_wq) {
         atomicAdd(&a.ctr[2], (unsigned long long)st_wq);

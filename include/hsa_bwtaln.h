@@ -11,6 +11,7 @@
  *   hsa_gpu_attach       new hook, called once after BWTLoad2BWT (bwtaln.c:467)
  *   hsa_gpu_detach       new hook, before BWTFree2BWT (bwtaln.c:527)
  *   hsa_gpu_set_devices  new hook: device slots one call is split over (see below)
+ *   bwa_cal_pac_pos      replaces bwtse.c:350 (SAM stage: SA -> position, batched)
  *
  * The structs below are declared here only so that the library reads and writes
  * the host's objects at the right offsets; their layouts are those of the
@@ -83,7 +84,15 @@ typedef struct { int n_entries, m_entries; gap_entry_t *stack; } gap_stack1_t;
 typedef struct { int n_stacks, best, n_entries; gap_stack1_t *stacks; } gap_stack_t;
 
 typedef uint32_t bwa_cigar_t;
-struct bwt_multi1_t;
+/* bwtaln.h:84-91 -- one more hit position of a read (40 bytes) */
+typedef struct bwt_multi1_t {
+    uint32_t n_cigar:15, gap:8, mm:8, strand:1;
+    bwtint_t sa, ori_pos, occ_pos;
+    unsigned int seq_id;
+    unsigned int aln_id;
+    int start, end;
+    bwa_cigar_t *cigar;
+} bwt_multi1_t;
 /* bwtaln.h:93-120 (208 bytes) */
 typedef struct {
     char *name;
@@ -109,6 +118,12 @@ typedef struct {
 } bwa_seq_t;
 
 /* bwtaln.h:122-131 mode bits */
+/* bwtaln.h:9-13 */
+#define BWA_TYPE_NO_MATCH   0
+#define BWA_TYPE_UNIQUE     1
+#define BWA_TYPE_REPEAT     2
+#define BWA_TYPE_SPLICING   4
+
 #define BWA_MODE_GAPE       0x01
 #define BWA_MODE_COMPREAD   0x02
 #define BWA_MODE_LOGGAP     0x04
@@ -166,6 +181,15 @@ void hsa_gpu_detach(const Idx2BWT *bi_bwt);
  * Returns 0, or HSA_E_ARG (n out of range or no device). */
 #define HSA_MAX_SLOTS 16
 int  hsa_gpu_set_devices(int n);
+
+/* bwa_cal_pac_pos: replaces bwtse.c:350 (declared bwtse.h).  The SAM stage's
+ * SA -> position step: the lookups of every non-splicing read of the batch (its SA
+ * value bwtse.c:146 and every other hit position bwtse.c:362) run as one GPU batch
+ * (hsa_sa_position_batch: BWTSaValue + BWTRetrievePositionFromSAIndex), then the same
+ * per-read updates (mapQ, seq_id/ori_pos/occ_pos, duplicate-position filter) in the
+ * same order.  Splicing reads keep the host's bwt_aln2pos_splicing (bwtse.c:295).
+ * Needs the host's bwa_approx_mapQ, bwa_cal_maxdiff and bwt_aln2pos_splicing. */
+void bwa_cal_pac_pos(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, int max_mm, float fnr);
 
 /* The host's splice fallback (bwtgap.c:748).  Weak: when the host program does
  * not provide it, reads without a hit are left with n_aln = 0. */

@@ -15,7 +15,7 @@ REFOBJS   = bwtaln bwtgap BWT BWTConstruct utils dictionary DNACount HSP inipars
             bamlite 2BWT-Interface bwaseqio r250 cs2nt bwtse kstring stdaln bwt_array
 OBJS      = $(addprefix $(OUT)/obj/,$(addsuffix .o,$(REFOBJS)))
 
-all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/ref_mgcap $(OUT)/HSA_gpu $(OUT)/HSA_gpu_mg
+all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/ref_mgcap $(OUT)/HSA_gpu $(OUT)/HSA_gpu_mg $(OUT)/HSA_gpu_all
 
 $(OUT)/obj/%.o: $(REF)/%.c
 	@mkdir -p $(OUT)/obj
@@ -78,6 +78,21 @@ GPUOBJ_MG = $(CURDIR)/../hsa_amd/csrc/bwtgap_gpu.o
 $(OUT)/HSA_gpu_mg: $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPULIB)
 	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPUOBJ_MG) -L$(dir $(GPULIB)) -lhsa_gpu \
 	    -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
+
+# HSA_gpu_all: every drop-in entry point replaced -- bwa_cal_sa_reg_gap, bwt_match_gap
+# (as HSA_gpu_mg) and the SAM stage's bwa_cal_pac_pos, weakened in bwtse.o, so that
+# generate_sam_se_core (bwtse.c:911) calls OUR bwa_cal_pac_pos (hsa_amd/csrc/bwtse_gpu.c:
+# the batch's SA -> position lookups on the GPU).
+$(OUT)/obj/bwtse_weak.o: $(OUT)/obj/bwtse.o
+	objcopy --weaken-symbol=bwa_cal_pac_pos $< $@
+
+ALLOBJS   = $(filter-out $(OUT)/obj/bwtaln.o $(OUT)/obj/bwtgap.o $(OUT)/obj/bwtse.o,$(OBJS)) \
+            $(OUT)/obj/bwtaln_weak.o $(OUT)/obj/bwtgap_weak.o $(OUT)/obj/bwtse_weak.o
+GPUOBJ_SA = $(CURDIR)/../hsa_amd/csrc/bwtse_gpu.o
+
+$(OUT)/HSA_gpu_all: $(OUT)/obj/main.o $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) $(GPULIB)
+	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) -L$(dir $(GPULIB)) \
+	    -lhsa_gpu -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
 
 clean:
 	rm -rf $(OUT)

@@ -66,3 +66,26 @@ def test_dropin_fails_loudly_without_gpu():
     assert r.returncode == 1
     assert b"[bwa_cal_sa_reg_gap]" in r.stderr
     assert r.stdout == b""
+
+
+HSA_GPU_ALL = os.path.join(ROOT, "oracle", "_ref", "HSA_gpu_all")
+
+
+@pytest.mark.skipif(not os.path.exists(HSA_GPU_ALL), reason="oracle/_ref/HSA_gpu_all not built (make -C oracle)")
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,reads", [("default", "reads"), ("n4o0", "reads"), ("splice_default", "splice_reads"),
+                                        ("splice_n4o1", "splice_reads")])
+def test_dropin_all_entry_points_sam_identical(name, reads):
+    """Every drop-in entry point replaced at once (oracle/ref.mk HSA_gpu_all):
+    bwa_cal_sa_reg_gap, bwt_match_gap, and the SAM stage's bwa_cal_pac_pos, whose SA ->
+    position lookups (seq_id, position and the duplicate filter of the extra hits in
+    every SAM line) run as one GPU batch per read batch (hsa_amd/csrc/bwtse_gpu.c)."""
+    idx = os.path.join(GOLD, "index", "tiny.fa")
+    fq = os.path.join(GOLD, MAN[reads])
+    r = subprocess.run([HSA_GPU_ALL, "aln", *MAN[name]["args"], idx, fq], capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    if hashlib.sha256(r.stdout).hexdigest() != MAN[name]["sam_sha256"]:
+        ref = gzip.open(os.path.join(GOLD, f"dropin_ref_{name}.sam.gz")).read().splitlines()
+        got = r.stdout.splitlines()
+        diff = [(i, a, b) for i, (a, b) in enumerate(zip(ref, got)) if a != b][:5]
+        pytest.fail(f"SAM differs: {len(got)} vs {len(ref)} lines; first differences {diff}")
