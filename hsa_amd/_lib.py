@@ -29,6 +29,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "bwt_match_gap", "bwt_match_gap_batch", "hsa_splice_seeds_device", "hsa_pass_times",
     "hsa_cal_sa_reg_gap_multi", "hsa_index_create_device64", "hsa_index_is64", "hsa_occ4_batch64",
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
+    "hsa_build_bwt_index_device",
 ]
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
@@ -188,6 +189,9 @@ def lib():
         L.hsa_occ4_batch64.argtypes = [vp, C.c_int, C.c_size_t, u64, u64]
         L.hsa_search_device64.argtypes = [vp, C.POINTER(Regime), C.c_int, C.POINTER(DeviceBatch), vp]
         L.hsa_build_bwt_device64.argtypes = [C.c_int, C.c_uint64, vp, C.c_int, vp, C.POINTER(C.c_uint64), u64]
+    if hasattr(L, "hsa_build_bwt_index_device"):
+        L.hsa_build_bwt_index_device.argtypes = [C.c_int, C.c_uint64, vp, vp, C.POINTER(C.c_uint64), u64, C.c_uint32,
+                                                 vp]
     f32 = np.ctypeslib.ndpointer(np.float32, flags="C")
     L.hsa_pass_times.argtypes = [vp, C.c_int, f32, f32]
     if hasattr(L, "hsa_cal_sa_reg_gap_multi"):      # (older A/B builds lack it)

@@ -114,13 +114,16 @@ __global__ void k_tie_flags(const uint64_t *keys, size_t n, uint8_t *flag)
 }
 
 // rows [row0, row0+n) of the full (T+1)-row BWT; row = 1 + sorted rank.
+// ... and, with sa_out, every sa_int-th suffix-array value (BWTGenerateSaValue's
+// samples, BWTConstruct.c:1241-1316: saValue[row / s] = SA[row] for row % s == 0).
 template <typename P>
 __global__ void k_bwt_chars(const uint32_t *t, const P *sa, size_t n, uint64_t row0, uint8_t *bwt,
-                            unsigned long long *isa0)
+                            unsigned long long *isa0, uint32_t *sa_out, uint32_t sa_int)
 {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const P p = sa[i];
+    if (sa_out && (row0 + i) % sa_int == 0) sa_out[(row0 + i) / sa_int] = (uint32_t)p;
     if (p == 0) { *isa0 = row0 + i; bwt[row0 + i] = 0; }
     else bwt[row0 + i] = (uint8_t)char_at(t, p - 1);
 }
@@ -160,7 +163,7 @@ struct HostText {
 
 template <typename P>
 static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d_out, uint64_t *isa0_out,
-                     uint64_t C[5])
+                     uint64_t C[5], uint32_t sa_int = 0, uint32_t *d_sa = nullptr)
 {
     (void)device;
     hipStream_t st = 0;
@@ -272,7 +275,7 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
             }
         }
         // 4. BWT characters of these rows
-        k_bwt_chars<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d_text, d_pos2, n, row, d_bwt, d_isa0);
+        k_bwt_chars<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d_text, d_pos2, n, row, d_bwt, d_isa0, d_sa, sa_int);
         HSA_HIP(hipGetLastError());
         row += n;
         b = e;
@@ -290,7 +293,7 @@ static int build_one(int device, uint64_t T, const uint32_t *d_text, uint32_t *d
 }
 
 static int build_bwt(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse, uint32_t *d_bwt_lsb,
-                     uint64_t *isa0, uint64_t C[5])
+                     uint64_t *isa0, uint64_t C[5], uint32_t sa_int = 0, uint32_t *d_sa = nullptr)
 {
     if (T == 0) { hsa_set_error("empty text"); return HSA_E_ARG; }
     HSA_HIP(hipSetDevice(device));
@@ -311,8 +314,8 @@ static int build_bwt(int device, uint64_t T, const uint32_t *d_text_lsb, int rev
         }
     }
     // u32 suffix positions while they fit (half the sort traffic of u64)
-    int rc = T < 0xFFFFFFFFull ? build_one<uint32_t>(device, T, t, d_bwt_lsb, isa0, C)
-                               : build_one<uint64_t>(device, T, t, d_bwt_lsb, isa0, C);
+    int rc = T < 0xFFFFFFFFull ? build_one<uint32_t>(device, T, t, d_bwt_lsb, isa0, C, sa_int, d_sa)
+                               : build_one<uint64_t>(device, T, t, d_bwt_lsb, isa0, C, sa_int, d_sa);
     (void)hipFree(t);
     return rc;
 }
@@ -321,6 +324,18 @@ extern "C" int hsa_build_bwt_device64(int device, uint64_t T, const uint32_t *d_
                                       uint32_t *d_bwt_lsb, uint64_t *isa0, uint64_t C[5])
 {
     return build_bwt(device, T, d_text_lsb, reverse, d_bwt_lsb, isa0, C);
+}
+
+// The BWT of the text as given plus its sampled suffix array (hsa_amd/index_build.py:
+// the .sa file of `HSA index`, whose values are u32, BWTConstruct.c:1373-1392).  SA
+// samples rows 1, 2, ... of every sa_interval-th row go to d_sa[row / sa_interval];
+// d_sa[0] (the '$' row, SA = T) is the caller's.
+extern "C" int hsa_build_bwt_index_device(int device, uint64_t T, const uint32_t *d_text_lsb, uint32_t *d_bwt_lsb,
+                                          uint64_t *isa0, uint64_t C[5], uint32_t sa_interval, uint32_t *d_sa)
+{
+    if (T == 0 || T >= 0xFFFFFFFFull) { hsa_set_error("text length must be in [1, 2^32-1) (u32 SA values)"); return HSA_E_ARG; }
+    if (d_sa && sa_interval == 0) { hsa_set_error("sa_interval must be > 0"); return HSA_E_ARG; }
+    return build_bwt(device, T, d_text_lsb, 0, d_bwt_lsb, isa0, C, sa_interval, d_sa);
 }
 
 // The 32-bit entry point: the .bwt header fields are u32 (BWT.h:61-83)

@@ -271,6 +271,12 @@ int hsa_search_device64(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regi
  * `reverse` builds the BWT of the reversed text. */
 int hsa_build_bwt_device(int device, uint64_t T, const uint32_t *d_text_lsb, int reverse,
                          uint32_t *d_bwt_lsb, uint32_t *isa0, uint32_t C[5]);
+/* The BWT of the text as given (no reversal) and, when d_sa is given, its sampled
+ * suffix array as `HSA index` stores it (BWTGenerateSaValue, BWTConstruct.c:1241):
+ * d_sa[r / sa_interval] = SA[r] for every row r > 0 with r % sa_interval == 0 (row 0,
+ * the '$' row, is the caller's: SA = T).  T < 2^32 - 1 (the .sa values are u32). */
+int hsa_build_bwt_index_device(int device, uint64_t T, const uint32_t *d_text_lsb, uint32_t *d_bwt_lsb,
+                               uint64_t *isa0, uint64_t C[5], uint32_t sa_interval, uint32_t *d_sa);
 /* The same for any T >= 1 (64-bit '$' row and C table); d_bwt_lsb holds ceil(T/16)
  * words.  Device memory besides the text and the output: about T bytes plus 9 GB
  * (u64 suffix positions past 2^32 characters). */

@@ -1,11 +1,12 @@
 """Device BWT construction (hsa_build_bwt_device) against the reference's own index
 files, and the device synthetic genome against hsa_amd/synth.py."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
 
-from golden_io import INDEX
+from golden_io import GOLD, INDEX
 from hsa_amd import index_io, synth
 
 pytestmark = pytest.mark.gpu
@@ -61,3 +62,33 @@ def test_synth_genome_device_matches_host():
         check(lib().hsa_synth_genome_device(0, T, 1234, out.data_ptr()))
         got = index_io.unpack_lsb_u32(out.cpu().numpy().view(np.uint32), T)
         assert np.array_equal(got, synth.genome_codes(T, 1234))
+
+
+@pytest.mark.parametrize("name", ["tiny", "rep", "nrun"])
+def test_full_index_build_matches_reference(tmp_path, name):
+    """hsa_amd/index_build.py: FASTA -> every file `HSA index` writes (.pac .ann .rev.pac
+    .bwt .fmv .rev.bwt .rev.fmv .sa), suffix sorting and SA sampling on the device,
+    byte-identical to the reference's files for the same FASTA (nrun: N-runs that split
+    blocks, short runs turned into G, the .pac length byte counting the Ns)."""
+    from test_index_build import fasta
+    from hsa_amd import index_build
+    fa = fasta(name, str(tmp_path / f"{name}.fa"))
+    index_build.build_index(fa)
+    for e in ("pac", "ann", "rev.pac", "bwt", "fmv", "rev.bwt", "rev.fmv", "sa"):
+        got = open(f"{fa}.index.{e}", "rb").read()
+        exp = open(os.path.join(GOLD, "index", f"{name}.fa.index.{e}"), "rb").read()
+        assert got == exp, f"{name}.index.{e} differs ({len(got)} vs {len(exp)} bytes)"
+
+
+def test_full_index_build_ecoli_digests(tmp_path):
+    """The E.coli-sized genome (4.6 Mbp): every index file's SHA-256 equals the
+    reference's (manifest_ecoli.json)."""
+    import hashlib
+    import json
+    from test_index_build import fasta
+    from hsa_amd import index_build
+    man = json.load(open(os.path.join(GOLD, "manifest_ecoli.json")))
+    fa = fasta("ecoli", str(tmp_path / "ecoli.fa"))
+    index_build.build_index(fa)
+    for e, digest in man["index_sha256"].items():
+        assert hashlib.sha256(open(f"{fa}.index.{e}", "rb").read()).hexdigest() == digest, e
