@@ -1054,32 +1054,14 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 return E{k, l, rk, meta};
             };
             if (cand) {
-                // the children's buckets: three scores at most -- the parent's (exact
-                // child), + s_mm (mismatch), + a gap open or extension (I, D)
-                int bk_m0, bk_mm, bk_gap = 0xFF;
-                if (!GAPS && a.mm_buckets) {
-                    bk_m0 = emm; bk_mm = emm + 1;
-                } else {
-                    auto bsc = [&](int scr) -> int {
-                        return (uint32_t)scr < a.ntab ? (int)s_lds[C_REG(ctl) * a.ntab + scr] : 0xFF;
-                    };
-                    const int s0 = SCORE(emm, ego, ege);
-                    bk_m0 = bsc(s0); bk_mm = bsc(s0 + S_MM);
-                    if (GAPS) bk_gap = bsc(s0 + (est == ST_M ? S_GO : S_GE));
-                }
-                auto bk_of = [&](uint32_t b) -> int {
-                    return (GAPS && b < 5u) ? bk_gap : (b < 8u || sc > 3) ? bk_mm : bk_m0;
-                };
                 const uint32_t last = 31u - (uint32_t)__clz(cand);
                 n_entries += __popc(cand);
-                // all but the last in push order, one candidate kind per step: with b a
-                // constant the kind, the child character and the bucket are known
-                const uint32_t rest = cand & ~(1u << last);
-#pragma unroll
-                for (uint32_t b = GAPS ? 0u : 5u; b < 9u; ++b)
-                    if ((rest >> b) & 1u) flush(entry(b), bk_of(b));
+                for (uint32_t rest = cand & ~(1u << last); rest; rest &= rest - 1u) {
+                    const E v = entry((uint32_t)__ffs(rest) - 1u);
+                    flush(v, bucket_of(v.w));
+                }
                 const E v = entry(last);
-                const int bk = bk_of(last);
+                const int bk = bucket_of(v.w);
                 if (bk <= mask.lowest()) { e = v; ctl |= 1u << 6; }
                 else flush(v, bk);
             }
