@@ -6,6 +6,7 @@
  * gap_shadow leaves it.  Its own object so that a host can take the GPU
  * bwa_cal_sa_reg_gap alone (bwtaln_gpu.o) or both entry points.
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -148,9 +149,13 @@ typedef struct {
     int len;
 } memo_ent_t;
 
+/* The table is process-global (the reference's host calls bwt_splice_match from one
+ * thread, but the entry points may be called from several): every access holds
+ * g_memo_mu, and a lookup copies its answer out before releasing it. */
 static memo_ent_t *g_memo;
 static size_t g_memo_cap, g_memo_n;
 static uint64_t g_memo_hits, g_memo_misses;
+static pthread_mutex_t g_memo_mu = PTHREAD_MUTEX_INITIALIZER;
 
 static size_t key_of(const bwt_aux_t *a, uint8_t *buf)
 {
@@ -178,11 +183,13 @@ static uint64_t fnv1a(const uint8_t *p, size_t n)
 
 void hsa_splice_memo_clear(void)
 {
+    pthread_mutex_lock(&g_memo_mu);
     for (size_t i = 0; i < g_memo_cap; ++i)
         if (g_memo[i].h) { free(g_memo[i].key); free(g_memo[i].hits); free(g_memo[i].wout); }
     free(g_memo);
     g_memo = NULL;
     g_memo_cap = g_memo_n = 0;
+    pthread_mutex_unlock(&g_memo_mu);
 }
 
 static void memo_put(const bwt_aux_t *in, const bwt_width_t *wout, const bwt_aln1_t *hits, int n_aln)
@@ -316,6 +323,7 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
         w += 4;
     }
     bwt_match_gap_batch(cp, c, out, n_out);
+    pthread_mutex_lock(&g_memo_mu);
     for (int i = 0; i < c; ++i) {
         /* the table is keyed by the inputs: widths as they were before the search */
         bwt_width_t *after = calls[i].width_back;
@@ -323,6 +331,7 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
         memo_put(calls + i, after, out[i], n_out[i]);
         free(after); free(win[i]); free(out[i]);
     }
+    pthread_mutex_unlock(&g_memo_mu);
     free(offs); free(lens); free(codes); free(wout);
     free(calls); free(cp); free(opts); free(win); free(out); free(n_out);
     return 0;
@@ -331,8 +340,10 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
 /* Table statistics since the last call (hits, misses), for logs. */
 void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses)
 {
+    pthread_mutex_lock(&g_memo_mu);
     *hits = g_memo_hits; *misses = g_memo_misses;
     g_memo_hits = g_memo_misses = 0;
+    pthread_mutex_unlock(&g_memo_mu);
 }
 
 /* bwt_match_gap (bwtgap.c:118, declared bwtgap.h:26): the reference's entry point,
@@ -340,6 +351,7 @@ void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses)
  * Same return contract: a calloc'd array, never NULL, freed by the caller. */
 bwt_aln1_t *bwt_match_gap(bwt_aux_t *aux, int *_n_aln)
 {
+    pthread_mutex_lock(&g_memo_mu);
     const memo_ent_t *e = memo_get(aux);
     if (e) {
         ++g_memo_hits;
@@ -347,9 +359,11 @@ bwt_aln1_t *bwt_match_gap(bwt_aux_t *aux, int *_n_aln)
         if (e->n_aln > 0) memcpy(out, e->hits, sizeof(bwt_aln1_t) * (size_t)e->n_aln);
         memcpy(aux->width_back, e->wout, sizeof(bwt_width_t) * ((size_t)e->len + 1));
         *_n_aln = e->n_aln;
+        pthread_mutex_unlock(&g_memo_mu);
         return out;
     }
     if (g_memo_n) ++g_memo_misses;
+    pthread_mutex_unlock(&g_memo_mu);
     bwt_aln1_t *out = NULL;
     bwt_match_gap_batch(&aux, 1, &out, _n_aln);
     return out;
