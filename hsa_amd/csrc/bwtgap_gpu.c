@@ -240,31 +240,87 @@ static const memo_ent_t *memo_get(const bwt_aux_t *a)
     return hit;
 }
 
-/* The six seed searches bwt_splice_match can ask for (bwtgap.c:762-812) of each
- * read it will be called on: aux[r] as bwt_splice_match receives it (seq, rc_seq,
- * len, opt = local_opt of that read, stack).  Widths of the read prefixes on the
- * GPU (bwt_cal_width type 1, as bwtgap.c:807 computes them), then one batch of
- * searches; the answers go to the table bwt_match_gap consults. */
+/* Search calls[0..c) in one batch (bwt_match_gap_batch) and put every answer in the
+ * table, keyed by the call's inputs: win[i] holds its width_back as it was before the
+ * search (calls[i].width_back is a scratch copy the search rewrites; a width_seed
+ * aliased to it is re-aliased to win[i]).  n_out[i] receives the hit counts. */
+static void batch_into_memo(bwt_aux_t *calls, int c, bwt_width_t **win, int *n_out)
+{
+    if (c <= 0) return;
+    bwt_aux_t **cp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)c);
+    bwt_aln1_t **out = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)c);
+    for (int i = 0; i < c; ++i) cp[i] = calls + i;
+    bwt_match_gap_batch(cp, c, out, n_out);
+    pthread_mutex_lock(&g_memo_mu);
+    for (int i = 0; i < c; ++i) {
+        bwt_width_t *after = calls[i].width_back;
+        const int alias = calls[i].width_seed == after;
+        calls[i].width_back = win[i];
+        if (alias) calls[i].width_seed = win[i];
+        memo_put(calls + i, after, out[i], n_out[i]);
+        free(after); free(out[i]);
+    }
+    pthread_mutex_unlock(&g_memo_mu);
+    free(cp); free(out);
+}
+
+/* One call of the batch: aux[r] copied as bwt_splice_match copies it (bwtgap.c:756-759),
+ * with its own option block, strand, length, and a scratch width_back initialised from
+ * w (n + 1 pairs, kept in win). */
+static bwt_aux_t *add_call(bwt_aux_t *calls, gap_opt_t *opts, bwt_width_t **win, int c, const bwt_aux_t *a,
+                           const gap_opt_t *o, int strand, int len, const uint32_t *w)
+{
+    bwt_aux_t *x = calls + c;
+    *x = *a;
+    opts[c] = *o;
+    x->opt = opts + c;
+    x->len = len;
+    x->strand = strand;
+    win[c] = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)len + 1));
+    memcpy(win[c], w, sizeof(bwt_width_t) * ((size_t)len + 1));
+    x->width_back = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)len + 1));
+    memcpy(x->width_back, win[c], sizeof(bwt_width_t) * ((size_t)len + 1));
+    x->width_seed = NULL;
+    return x;
+}
+
+#define ANCHOR 12   /* the anchor length of bwtgap.c:911 and :1187 */
+
+/* The splice path's searches of each read bwt_splice_match will be called on, run on the
+ * GPU as two batches before the host asks for them; aux[r] as bwt_splice_match receives
+ * it (seq, rc_seq, len, opt = local_opt of that read, stack).
+ *  1. The six seed searches (bwtgap.c:762-812): widths of the strand prefixes
+ *     (bwt_cal_width type 1, as :807 computes them), width_seed aliased to width_back.
+ *  2. The 12-mer anchor searches made after an extension succeeds (options of aux_ext:
+ *     max_gape 3, :782; width_seed NULL):
+ *       - seeds 0 and 1 of a strand map and seed 2 does not (seg_mtype 3): the strand's
+ *         last 12 bases with their own widths (:911-919);
+ *       - seeds 1 and 2 map and seed 0 does not (seg_mtype 6): its first 12 bases with
+ *         the whole read's widths (:867/:871, :1187-1192), i.e. the first 13 width
+ *         entries of the prefix of length 13.
+ *     Whether the host reaches them depends on the seed correlation and the
+ *     backtracking, so the anchor of every strand whose seed pattern leads there is
+ *     searched: one small search per such strand, where the host would otherwise make a
+ *     GPU round trip per call. */
 int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
 {
     if (n <= 0) return 0;
     hsa_index_t *ix = hsa_gpu_index_of(bi);
     /* widths: per read, strand s, the prefix of seed_len and of seed_len + len % 3 */
     int nw = 0;
-    size_t wcodes = 0, wpairs = 0;
+    size_t wcodes = 0;
     for (int r = 0; r < n; ++r) {
         const int L = aux[r]->len, sl = L / 3;
         if (sl < 1) continue;
         nw += 4;
         wcodes += 4 * (size_t)sl + 2 * (size_t)(L % 3);
-        wpairs += 4 * (size_t)(sl + 1) + 2 * (size_t)(L % 3);
     }
     if (nw == 0) return 0;
     uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)nw);
     uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)nw);
+    size_t *woff = (size_t *)malloc(sizeof(size_t) * (size_t)nw);
     uint8_t *codes = (uint8_t *)malloc(wcodes + 1);
-    uint32_t *wout = (uint32_t *)malloc(sizeof(uint32_t) * 2 * (wpairs + 1));
-    size_t co = 0;
+    size_t co = 0, wo = 0;
     int q = 0;
     for (int r = 0; r < n; ++r) {
         const int L = aux[r]->len, sl = L / 3;
@@ -272,68 +328,114 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
         for (int s = 0; s < 2; ++s)
             for (int k = 0; k < 2; ++k) {
                 const int la = sl + (k ? L % 3 : 0);
-                offs[q] = co; lens[q] = (uint32_t)la;
+                offs[q] = co; lens[q] = (uint32_t)la; woff[q] = wo;
                 memcpy(codes + co, s ? aux[r]->rc_seq : aux[r]->seq, (size_t)la);
                 co += (size_t)la;
+                wo += 2 * ((size_t)la + 1);
                 ++q;
             }
     }
+    uint32_t *wout = (uint32_t *)malloc(sizeof(uint32_t) * (wo + 2));
     int rc = hsa_width_batch(ix, (size_t)nw, offs, lens, codes, co, wout);
     if (rc) hsa_gpu_fatal("GPU bwt_cal_width", rc);
     /* the seed calls, set up as bwtgap.c:797-810 sets up aux_seed */
     const int nc = 6 * (nw / 4);
     bwt_aux_t *calls = (bwt_aux_t *)calloc((size_t)nc, sizeof(bwt_aux_t));
-    bwt_aux_t **cp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)nc);
     gap_opt_t *opts = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nc);
     bwt_width_t **win = (bwt_width_t **)malloc(sizeof(bwt_width_t *) * (size_t)nc);
-    bwt_aln1_t **out = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)nc);
     int *n_out = (int *)malloc(sizeof(int) * (size_t)nc);
-    size_t wo = 0;
     int c = 0, w = 0;
     for (int r = 0; r < n; ++r) {
         const bwt_aux_t *a = aux[r];
         const int L = a->len, sl = L / 3;
         if (sl < 1) continue;
-        size_t woff[4];
-        for (int k = 0; k < 4; ++k) { woff[k] = wo; wo += 2 * ((size_t)lens[w + k] + 1); }
+        gap_opt_t so = *a->opt;                                 /* :769-774 */
+        so.mode &= ~BWA_MODE_GAPE;
+        so.max_gapo = 0;
+        so.max_gape = 0;
+        so.max_diff = a->opt->max_seed_diff;
         for (int i = 0; i < 6; ++i) {
             const int s = i / 3, la = sl + (i % 3 == 2 ? L % 3 : 0);
-            bwt_aux_t *x = calls + c;
-            *x = *a;                                            /* bwtgap.c:756-757 */
-            gap_opt_t *o = opts + c;
-            *o = *a->opt;                                       /* :769-774 */
-            o->mode &= ~BWA_MODE_GAPE;
-            o->max_gapo = 0;
-            o->max_gape = 0;
-            o->max_diff = a->opt->max_seed_diff;
-            o->seed_len = la;                                   /* :802 */
-            x->opt = o;
-            x->len = la;
-            x->strand = s;
+            so.seed_len = la;                                   /* :802 */
+            const uint32_t *wk = wout + woff[w + 2 * s + (i % 3 == 2 && L % 3 ? 1 : 0)];
+            bwt_aux_t *x = add_call(calls, opts, win, c, a, &so, s, la, wk);
             if (s) x->rc_seq = a->rc_seq + (i % 3) * sl;       /* :805-806 */
             else x->seq = a->seq + (i % 3) * sl;
-            const size_t wk = woff[2 * s + (i % 3 == 2 && L % 3 ? 1 : 0)];
-            win[c] = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)la + 1));
-            memcpy(win[c], wout + wk, sizeof(bwt_width_t) * ((size_t)la + 1));
-            x->width_seed = x->width_back = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)la + 1));
-            memcpy(x->width_back, win[c], sizeof(bwt_width_t) * ((size_t)la + 1));   /* :804-809 */
-            cp[c] = x;
+            x->width_seed = x->width_back;                      /* :804-809 */
             ++c;
         }
         w += 4;
     }
-    bwt_match_gap_batch(cp, c, out, n_out);
-    pthread_mutex_lock(&g_memo_mu);
-    for (int i = 0; i < c; ++i) {
-        /* the table is keyed by the inputs: widths as they were before the search */
-        bwt_width_t *after = calls[i].width_back;
-        calls[i].width_back = calls[i].width_seed = win[i];
-        memo_put(calls + i, after, out[i], n_out[i]);
-        free(after); free(win[i]); free(out[i]);
+    batch_into_memo(calls, c, win, n_out);
+
+    /* the anchors of the strands whose seed pattern is 3 or 6 */
+    int na = 0;
+    size_t acodes = 0;
+    for (int r = 0, rr = 0; r < n; ++r) {
+        const int L = aux[r]->len;
+        if (L / 3 < 1) continue;
+        for (int s = 0; s < 2 && L > ANCHOR; ++s) {
+            const int *no = n_out + 6 * rr + 3 * s;
+            const int mask = (no[0] > 0) | (no[1] > 0) << 1 | (no[2] > 0) << 2;
+            if (mask == 3) { ++na; acodes += ANCHOR; }
+            if (mask == 6) { ++na; acodes += ANCHOR + 1; }
+        }
+        ++rr;
     }
-    pthread_mutex_unlock(&g_memo_mu);
-    free(offs); free(lens); free(codes); free(wout);
-    free(calls); free(cp); free(opts); free(win); free(out); free(n_out);
+    if (na > 0) {
+        uint64_t *ao = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)na);
+        uint32_t *al = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)na);
+        uint8_t *ac = (uint8_t *)malloc(acodes + 1);
+        int *ar = (int *)malloc(sizeof(int) * (size_t)na);     /* read, strand, kind */
+        size_t aco = 0, awo = 0;
+        int k = 0;
+        for (int r = 0, rr = 0; r < n; ++r) {
+            const bwt_aux_t *a = aux[r];
+            const int L = a->len;
+            if (L / 3 < 1) continue;
+            for (int s = 0; s < 2 && L > ANCHOR; ++s) {
+                const int *no = n_out + 6 * rr + 3 * s;
+                const int mask = (no[0] > 0) | (no[1] > 0) << 1 | (no[2] > 0) << 2;
+                if (mask != 3 && mask != 6) continue;
+                const ubyte_t *sq = s ? a->rc_seq : a->seq;
+                const int tail = mask == 3;
+                al[k] = tail ? ANCHOR : ANCHOR + 1;
+                ao[k] = aco;
+                memcpy(ac + aco, tail ? sq + L - ANCHOR : sq, al[k]);
+                aco += al[k];
+                awo += 2 * ((size_t)al[k] + 1);
+                ar[k] = r << 2 | s << 1 | tail;
+                ++k;
+            }
+            ++rr;
+        }
+        uint32_t *aw = (uint32_t *)malloc(sizeof(uint32_t) * (awo + 2));
+        rc = hsa_width_batch(ix, (size_t)na, ao, al, ac, aco, aw);
+        if (rc) hsa_gpu_fatal("GPU bwt_cal_width", rc);
+        bwt_aux_t *acalls = (bwt_aux_t *)calloc((size_t)na, sizeof(bwt_aux_t));
+        gap_opt_t *aopts = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)na);
+        bwt_width_t **awin = (bwt_width_t **)malloc(sizeof(bwt_width_t *) * (size_t)na);
+        int *an = (int *)malloc(sizeof(int) * (size_t)na);
+        size_t wp = 0;
+        for (int j = 0; j < na; ++j) {
+            const bwt_aux_t *a = aux[ar[j] >> 2];
+            const int s = (ar[j] >> 1) & 1, tail = ar[j] & 1, L = a->len;
+            gap_opt_t eo = *a->opt;
+            eo.max_gape = 3;                                    /* aux_ext (:777-782) */
+            bwt_aux_t *x = add_call(acalls, aopts, awin, j, a, &eo, s, ANCHOR, aw + wp);
+            if (tail) {                                         /* :912 */
+                if (s) x->rc_seq = a->rc_seq + L - ANCHOR;
+                else x->seq = a->seq + L - ANCHOR;
+            }
+            wp += 2 * ((size_t)al[j] + 1);
+        }
+        batch_into_memo(acalls, na, awin, an);
+        for (int j = 0; j < na; ++j) free(awin[j]);
+        free(ao); free(al); free(ac); free(ar); free(aw); free(acalls); free(aopts); free(awin); free(an);
+    }
+    for (int i = 0; i < c; ++i) free(win[i]);
+    free(offs); free(lens); free(woff); free(codes); free(wout);
+    free(calls); free(opts); free(win); free(n_out);
     return 0;
 }
 
