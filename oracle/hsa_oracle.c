@@ -648,3 +648,169 @@ long OR(cal_sa_reg_gap)(const or_index_t *cix, int n, const uint32_t *lens, cons
     *hits_out = all.a ? all.a : (uint32_t *)calloc(HW, sizeof(uint32_t));
     return all.n;
 }
+
+#ifndef OR_WIDE   /* the splice path's seed extension: 32-bit only, as the reference */
+/* BWTAllSARangesForward_Bidirection (2BWT-Interface.c:274-304): the rank queries on
+ * the REVERSE BWT at rev_k and rev_l + 1, the FORWARD C table. */
+static void step_all_fwd(or_index_t *ix, bw_t k, bw_t l, bw_t rk, bw_t rl, bw_t ok[4], bw_t ol[4], bw_t ork[4],
+                         bw_t orl[4])
+{
+    bw_t oL[4], oR[4], oC[4];
+    (void)k;
+    occ4(&ix->r, rk, oL);
+    occ4(&ix->r, rl + 1, oR);
+    tl_queries += 2;
+    oC[3] = 0;
+    for (int c = 2; c >= 0; --c) oC[c] = oC[c + 1] + oR[c + 1] - oL[c + 1];
+    for (int c = 0; c < 4; ++c) {
+        ork[c] = ix->f.C[c] + oL[c] + 1;
+        orl[c] = ix->f.C[c] + oR[c];
+        ol[c] = l - oC[c];
+        ok[c] = ol[c] - (orl[c] - ork[c]);
+    }
+}
+
+/* The extension's view of the read: the strand sequence and the direction's width
+ * bids at read positions [lo, lo + n).  Any access outside is a restatement error. */
+typedef struct { const uint8_t *seq; const int32_t *bid; int lo, n; } ext_win_t;
+
+static uint8_t win_seq(const ext_win_t *w, int p)
+{
+    if (p < w->lo || p >= w->lo + w->n) { fprintf(stderr, "oracle: extension reads position %d outside [%d, %d)\n", p, w->lo, w->lo + w->n); abort(); }
+    return w->seq[p - w->lo];
+}
+
+static int win_bid(const ext_win_t *w, int p)
+{
+    if (p < w->lo || p >= w->lo + w->n) { fprintf(stderr, "oracle: extension reads width %d outside [%d, %d)\n", p, w->lo, w->lo + w->n); abort(); }
+    return w->bid[p - w->lo];
+}
+
+/* bwt_extend_exact (2BWT-Interface.c:394-439): the outputs change only on a step that
+ * keeps the interval non-empty.  Backward consumes *leav; forward never decrements it
+ * (:422-436) and extends by the same character until the interval empties. */
+static void extend_exact(or_index_t *ix, const ext_win_t *w, int start, int *leav, int type, bw_t *sk, bw_t *sl,
+                         bw_t *srk, bw_t *srl)
+{
+    bw_t k = *sk, l = *sl, rk = *srk, rl = *srl;
+    if (type == 1) {
+        start -= *leav;
+        while (*leav != 0) {
+            const uint8_t c = win_seq(w, start + *leav);
+            if (c > 3) break;
+            step1(ix, c, &k, &l, &rk, &rl);
+            if (k > l) break;
+            *sk = k; *sl = l; *srk = rk; *srl = rl;
+            --*leav;
+        }
+    } else {
+        start += *leav;
+        while (*leav != 0) {
+            const uint8_t c = win_seq(w, start - *leav);
+            if (c > 3) break;
+            bw_t ok[4], ol[4], ork[4], orl[4];
+            step_all_fwd(ix, k, l, rk, rl, ok, ol, ork, orl);   /* BWTSARangeForward_Bidirection */
+            k = ok[c]; l = ol[c]; rk = ork[c]; rl = orl[c];
+            if (k > l) break;
+            *sk = k; *sl = l; *srk = rk; *srl = rl;
+        }
+    }
+}
+
+/* bwt_extend_backward / bwt_extend_foreward (bwtgap.c:640-663): the stack reset, the
+ * seed's entry (i = len, state M, is_diff 0), then bwt_backtracing_search
+ * (bwtgap.c:346-511).  aln: the 9 words of the bwt_aln1_t, updated in place;
+ * *max_pos in/out; returns 1, 2 or -1.  The gap entry's info word is the reference's
+ * score << 21 | i in 32 bits, so a negative len gives a score field of 2047 (the
+ * search stops at its first pop unless NONSTOP). */
+int or_extend(const or_index_t *cix, const or_opt_t *opt, int n_stacks, int is_backward, int len, const uint8_t *seq,
+              const int32_t *bid, int lo, int n, uint32_t *aln, int *max_pos_io)
+{
+    or_index_t *ix = (or_index_t *)cix;
+    const ext_win_t w = {seq, bid, lo, n};
+    stack_t_ *st = stack_new(n_stacks);
+    stack_reset(st);
+    const int a_mm = (int)(aln[0] & 0xFFFF), a_go = (int)((aln[0] >> 16) & 0xFF), a_ge = (int)(aln[0] >> 24);
+    push(st, len, aln[1], aln[2], aln[3], aln[4], a_mm, a_go, a_ge, ST_M, 0, opt);
+    const int best_score = SCORE(opt, opt->max_diff + 1, opt->max_gapo + 1, opt->max_gape + 1);
+    const int max_diff = opt->max_diff;
+    const int start = (int)aln[6], end = (int)aln[7];
+    int max_pos = *max_pos_io, ret = 0;
+    while (st->n_entries != 0) {
+        if (st->n_entries > opt->max_entries) break;
+        ent_t e;
+        pop(st, &e);
+        bw_t k = e.k, l = e.l, rk = e.rk, rl = e.rl;
+        int i = (int)(e.info & 0xffff);
+        if (!(opt->mode & MODE_NONSTOP) && (int)(e.info >> 21) > best_score + opt->s_mm) break;
+        int m = max_diff - (e.n_mm + e.n_gapo);
+        if (opt->mode & MODE_GAPE) m -= e.n_gape;
+        if (m <= 0 || i == 0) {
+            if (m == 0 && i != 0)
+                extend_exact(ix, &w, is_backward == 0 ? end + len - i + 1 : start - len + i - 1, &i, is_backward,
+                             &k, &l, &rk, &rl);
+            if (is_backward == 1 && max_pos >= start + i - len && (int)aln[6] > start + i - len) {
+                aln[6] = (uint32_t)(start + i - len);
+                max_pos = (int)aln[6];
+            } else if (is_backward == 0 && max_pos <= end + len - i && (int)aln[7] < end + len - i) {
+                aln[7] = (uint32_t)(end + len - i);
+                max_pos = (int)aln[7];
+            } else {
+                continue;
+            }
+            aln[1] = k; aln[2] = l; aln[3] = rk; aln[4] = rl;
+            aln[5] = (aln[5] & 0xC0000000u) | 4u;                       /* BWA_TYPE_SPLICING, strand kept */
+            aln[0] = (uint32_t)e.n_mm | (uint32_t)e.n_gapo << 16 | (uint32_t)e.n_gape << 24;
+            aln[8] = e.info >> 21;
+            if (i == 0) { ret = 1; break; }
+            continue;
+        }
+        --i;
+        const int real_pos = is_backward == 1 ? start - len + i : len + end - i;
+        bw_t ok[4], ol[4], ork[4], orl[4];
+        if (is_backward == 1) step_all(ix, k, l, rk, rl, ok, ol, ork, orl);
+        else step_all_fwd(ix, k, l, rk, rl, ok, ol, ork, orl);
+        const bw_t occ = l - k + 1;
+        int allow_diff = 1;
+        if (is_backward == 1 && max_pos < real_pos) {
+            const int d = win_bid(&w, real_pos) - win_bid(&w, max_pos);
+            if (d > m || (d == m && win_bid(&w, max_pos) != win_bid(&w, max_pos + 1))) allow_diff = 0;
+        }
+        if (is_backward == 0 && max_pos > real_pos) {
+            const int d = win_bid(&w, real_pos) - win_bid(&w, max_pos);
+            if (d > m || (d == m && win_bid(&w, max_pos) != win_bid(&w, max_pos - 1))) allow_diff = 0;
+        }
+        const int tmp = (opt->mode & MODE_LOGGAP) ? int_log2((uint32_t)(e.n_gape + e.n_gapo)) / 2 + 1
+                                                  : e.n_gapo + e.n_gape;
+        if (allow_diff && i >= opt->indel_end_skip + tmp && len - i >= opt->indel_end_skip + tmp) {
+            if (e.state == ST_M) {
+                if (e.n_gapo < opt->max_gapo) {
+                    push(st, i, k, l, rk, rl, e.n_mm, e.n_gapo + 1, e.n_gape, ST_I, 1, opt);
+                    for (int j = 0; j != 4; ++j)
+                        if ((is_backward == 1 && ok[j] <= ol[j]) || (is_backward == 0 && ork[j] <= orl[j]))
+                            push(st, i + 1, ok[j], ol[j], ork[j], orl[j], e.n_mm, e.n_gapo + 1, e.n_gape, ST_D, 1, opt);
+                }
+            } else if (e.state == ST_I) {
+                if (e.n_gape < opt->max_gape) push(st, i, k, l, rk, rl, e.n_mm, e.n_gapo, e.n_gape + 1, ST_I, 1, opt);
+            } else if (e.state == ST_D) {
+                if (e.n_gape < opt->max_gape && (e.n_gape + e.n_gapo < max_diff || occ < (bw_t)opt->max_del_occ))
+                    for (int j = 0; j != 4; ++j)
+                        if (ok[j] <= ol[j])
+                            push(st, i + 1, ok[j], ol[j], ork[j], orl[j], e.n_mm, e.n_gapo, e.n_gape + 1, ST_D, 1, opt);
+            }
+        }
+        if (allow_diff == 1) {
+            const uint8_t sc = win_seq(&w, real_pos);
+            for (int j = 1; j <= 4; ++j) {
+                const int c = (sc + j) & 3, is_mm = (j != 4 || sc > 3);
+                if ((is_backward == 1 && ok[c] <= ol[c]) || (is_backward == 0 && ork[c] <= orl[c]))
+                    push(st, i, ok[c], ol[c], ork[c], orl[c], e.n_mm + is_mm, e.n_gapo, e.n_gape, ST_M, is_mm, opt);
+            }
+        }
+    }
+    stack_del(st);
+    if (ret == 1) { *max_pos_io = max_pos; return 1; }
+    if (*max_pos_io != max_pos) { *max_pos_io = max_pos; return 2; }
+    return -1;
+}
+#endif

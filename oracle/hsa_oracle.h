@@ -72,6 +72,14 @@ long or_cal_sa_reg_gap(const or_index_t *ix, int n, const uint32_t *lens, const 
 int or_match_gap(const or_index_t *ix, const or_opt_t *opt, int n_stacks, const uint8_t *seq, int len, int strand,
                  uint32_t *width, int seed, const uint32_t *width_seed, uint32_t **hits);
 void or_free(void *p);
+/* bwt_extend_backward (is_backward 1) / bwt_extend_foreward (0), bwtgap.c:640-663 ->
+ * bwt_backtracing_search (:346-511): extend the seed hit aln (9 words, bwt_aln1_t
+ * layout, updated in place) over len read positions toward *max_pos (in/out).  seq /
+ * bid: the strand sequence and the direction's width bids (width_back backward,
+ * width_fore forward) at read positions [lo, lo + n); reading outside aborts.
+ * Returns 1, 2 or -1 as the reference. */
+int or_extend(const or_index_t *ix, const or_opt_t *opt, int n_stacks, int is_backward, int len, const uint8_t *seq,
+              const int32_t *bid, int lo, int n, uint32_t *aln, int *max_pos_io);
 
 /* ---- liboracle64.so (hsa_oracle.c built with -DOR_WIDE): the same functions with
  * 64-bit intervals (texts of 2^32 characters or more; the reference's bwtint_t is

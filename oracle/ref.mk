@@ -15,7 +15,7 @@ REFOBJS   = bwtaln bwtgap BWT BWTConstruct utils dictionary DNACount HSP inipars
             bamlite 2BWT-Interface bwaseqio r250 cs2nt bwtse kstring stdaln bwt_array
 OBJS      = $(addprefix $(OUT)/obj/,$(addsuffix .o,$(REFOBJS)))
 
-all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/ref_mgcap $(OUT)/HSA_gpu $(OUT)/HSA_gpu_mg $(OUT)/HSA_gpu_all
+all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/ref_mgcap $(OUT)/ref_extcap $(OUT)/HSA_gpu $(OUT)/HSA_gpu_mg $(OUT)/HSA_gpu_all
 
 $(OUT)/obj/%.o: $(REF)/%.c
 	@mkdir -p $(OUT)/obj
@@ -66,6 +66,22 @@ CAPOBJS   = $(filter-out $(OUT)/obj/bwtgap.o,$(OBJS)) $(OUT)/obj/bwtgap_weak.o $
 
 $(OUT)/ref_mgcap: ref_mgcap.c $(CAPOBJS)
 	$(CC) $(REFFLAGS) -I$(REF) ref_mgcap.c $(CAPOBJS) -lm -lz -o $@
+
+# ref_extcap.c is ours: it records every seed extension of the splice path
+# (bwt_extend_foreward / bwt_extend_backward, bwtgap.c:640-663), the same way.
+$(OUT)/obj/bwtgap_weakx.o: $(OUT)/obj/bwtgap.o
+	objcopy --weaken-symbol=bwt_extend_foreward --weaken-symbol=bwt_extend_backward $< $@
+
+$(OUT)/obj/bwtgap_renx.o: $(OUT)/obj/bwtgap.o
+	objcopy --redefine-sym bwt_extend_foreward=ref_bwt_extend_foreward \
+	        --redefine-sym bwt_extend_backward=ref_bwt_extend_backward $< $@.tmp
+	objcopy --keep-global-symbol=ref_bwt_extend_foreward --keep-global-symbol=ref_bwt_extend_backward $@.tmp $@
+	rm -f $@.tmp
+
+EXTOBJS   = $(filter-out $(OUT)/obj/bwtgap.o,$(OBJS)) $(OUT)/obj/bwtgap_weakx.o $(OUT)/obj/bwtgap_renx.o
+
+$(OUT)/ref_extcap: ref_extcap.c $(EXTOBJS)
+	$(CC) $(REFFLAGS) -I$(REF) ref_extcap.c $(EXTOBJS) -lm -lz -o $@
 
 # HSA_gpu_mg: as HSA_gpu, with bwt_match_gap weakened too, so the host's splice path
 # (bwt_splice_match, bwtgap.c:748) calls OUR bwt_match_gap for its seed and anchor

@@ -106,3 +106,22 @@ def load_mgcap(name):
 def ecoli_manifest():
     with open(os.path.join(GOLD, "manifest_ecoli.json")) as f:
         return json.load(f)
+
+
+EXTCAP_CASES = ["extcap_default", "extcap_n4o1"]
+
+
+def load_extcap(name):
+    """Seed extensions recorded from the reference (tools/make_golden.py --extcap): per
+    call the header (dir, len, strand, n_stacks, max_pos in, window lo, window n, read
+    length), the option block, aln in/out, the window of sequence and width bids, and
+    (ret, max_pos out).  Yields dicts."""
+    z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    hdr, opt, ai, ao, tail = z["hdr"], z["opt"], z["aln_in"], z["aln_out"], z["tail"]
+    seq, bid = z["seq"], z["bid"]
+    off = np.concatenate([[0], np.cumsum(hdr[:, 6].astype(np.int64))])
+    for j in range(len(hdr)):
+        yield dict(dir=int(hdr[j, 0]), len=int(hdr[j, 1]), strand=int(hdr[j, 2]), n_stacks=int(hdr[j, 3]),
+                   max_pos=int(hdr[j, 4]), lo=int(hdr[j, 5]), read_len=int(hdr[j, 7]), opt=opt[j],
+                   aln_in=ai[j], aln_out=ao[j], ret=int(tail[j, 0]), max_pos_out=int(tail[j, 1]),
+                   seq=seq[off[j]:off[j + 1]], bid=bid[off[j]:off[j + 1]])

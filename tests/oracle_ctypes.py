@@ -65,6 +65,10 @@ def lib():
         L.or_sa_value.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32]
         L.or_sa_position.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_int, C.c_uint32,
                                      C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.or_extend.restype = C.c_int
+        L.or_extend.argtypes = [C.c_void_p, C.POINTER(Opt), C.c_int, C.c_int, C.c_int,
+                                np.ctypeslib.ndpointer(np.uint8, flags="C"), i32p, C.c_int, C.c_int, u32p,
+                                C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -169,6 +173,18 @@ class OracleIndex:
         lib().or_free(hp)
         return hits, w
 
+    def extend(self, opt: Opt, n_stacks, is_backward, length, seq, bid, lo, aln, max_pos):
+        """bwt_extend_backward / bwt_extend_foreward (or_extend) on a window of the read:
+        returns (ret, max_pos, aln after (9,) uint32)."""
+        a = np.ascontiguousarray(aln, np.uint32).copy()
+        mp = C.c_int(int(max_pos))
+        seq = np.ascontiguousarray(seq, np.uint8)
+        bid = np.ascontiguousarray(bid, np.int32)
+        ret = lib().or_extend(self.h, C.byref(opt), int(n_stacks), int(is_backward), int(length),
+                              seq if len(seq) else np.zeros(1, np.uint8), bid if len(bid) else np.zeros(1, np.int32),
+                              int(lo), len(seq), a, C.byref(mp))
+        return ret, mp.value, a
+
     def cal_sa_reg_gap(self, lens, codes, opt: Opt):
         """One batch; returns (n_aln, flags, hits(H,9), stats[queries, pops]); mutates opt."""
         n = len(lens)
@@ -235,6 +251,18 @@ class OracleIndex64:
         w = np.zeros(2 * (len(seq) + 1), np.uint64)
         lib64().or64_cal_width(self.h, len(seq), seq, w)
         return w.reshape(-1, 2)
+
+    def extend(self, opt: Opt, n_stacks, is_backward, length, seq, bid, lo, aln, max_pos):
+        """bwt_extend_backward / bwt_extend_foreward (or_extend) on a window of the read:
+        returns (ret, max_pos, aln after (9,) uint32)."""
+        a = np.ascontiguousarray(aln, np.uint32).copy()
+        mp = C.c_int(int(max_pos))
+        seq = np.ascontiguousarray(seq, np.uint8)
+        bid = np.ascontiguousarray(bid, np.int32)
+        ret = lib().or_extend(self.h, C.byref(opt), int(n_stacks), int(is_backward), int(length),
+                              seq if len(seq) else np.zeros(1, np.uint8), bid if len(bid) else np.zeros(1, np.int32),
+                              int(lo), len(seq), a, C.byref(mp))
+        return ret, mp.value, a
 
     def cal_sa_reg_gap(self, lens, codes, opt: Opt):
         """One batch; returns (n_aln, flags, hits(H,14), stats[queries, pops]); mutates opt."""

@@ -2,9 +2,9 @@
 import numpy as np
 import pytest
 
-from golden_io import GOLD, INDEX, cases, load_case, parse_opts, split_hits
+from golden_io import EXTCAP_CASES, GOLD, INDEX, cases, load_case, load_extcap, parse_opts, split_hits
 from hsa_amd import index_io
-from oracle_ctypes import OracleIndex, default_opt
+from oracle_ctypes import Opt, OracleIndex, default_opt
 
 _IDX = {}
 
@@ -186,3 +186,23 @@ def test_oracle64_batch_matches_reference(name):
     exp = split_hits(g["n_aln"], g["hits"])
     bad = [i for i in range(len(got)) if not exp_splice[i] and not np.array_equal(got[i], exp[i])]
     assert not bad, f"{len(bad)} reads differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("name", EXTCAP_CASES)
+def test_extension_matches_reference(name):
+    """bwt_extend_backward / bwt_extend_foreward (bwtgap.c:640-663, the splice path's
+    seed extensions through bwt_backtracing_search :346-511): every call the compiled
+    reference made on the splice read set, restated from the recorded window of the
+    read alone -- return value, max_pos and every bwt_aln1_t field."""
+    fwd, rev = index_io.read_index(INDEX["tiny"])
+    ox = OracleIndex(fwd, rev)
+    n = bad = 0
+    for c in load_extcap(name):
+        opt = Opt.from_buffer_copy(np.ascontiguousarray(c["opt"], np.uint32).tobytes())
+        ret, mp, a = ox.extend(opt, c["n_stacks"], c["dir"], c["len"], c["seq"], c["bid"], c["lo"], c["aln_in"],
+                               c["max_pos"])
+        n += 1
+        if ret != c["ret"] or mp != c["max_pos_out"] or not np.array_equal(a, c["aln_out"]):
+            bad += 1
+    assert n > 3000
+    assert bad == 0, f"{bad} of {n} extensions differ"

@@ -480,12 +480,63 @@ def mgcap_cases(work):
               f"{changed} with widths changed by gap_shadow")
 
 
+def read_extcap(path):
+    """Records of oracle/ref_extcap.c: every seed extension of a reference run."""
+    raw = open(path, "rb").read()
+    assert raw[:4] == b"EXCP"
+    o = 4
+    recs = []
+    while o < len(raw):
+        hdr = np.frombuffer(raw[o:o + 32], np.int32).copy()
+        o += 32
+        n = int(hdr[6])
+        opt = np.frombuffer(raw[o:o + 64], np.uint32).copy()
+        o += 64
+        aln_in = np.frombuffer(raw[o:o + 36], np.uint32).copy()
+        o += 36
+        seq = np.frombuffer(raw[o:o + n], np.uint8).copy()
+        o += n
+        bid = np.frombuffer(raw[o:o + 4 * n], np.int32).copy()
+        o += 4 * n
+        tail = np.frombuffer(raw[o:o + 8], np.int32).copy()
+        o += 8
+        aln_out = np.frombuffer(raw[o:o + 36], np.uint32).copy()
+        o += 36
+        recs.append(dict(hdr=hdr, opt=opt, aln_in=aln_in, seq=seq, bid=bid, tail=tail, aln_out=aln_out))
+    return recs
+
+
+def extcap_cases(work):
+    """The splice path's seed extensions (bwt_extend_foreward / bwt_extend_backward,
+    bwtgap.c:640-663 -> bwt_backtracing_search :346-511): every call the reference makes
+    on the drop-in splice read set, recorded by oracle/ref_extcap.c with the window of
+    sequence and widths each call reads."""
+    seqs = splice_reads()
+    rb = os.path.join(work, "ext_reads.bin")
+    synth.write_reads_bin(rb, seqs)
+    idx = os.path.join(GOLD, "index", "tiny.fa")
+    for name, args in (("extcap_default", []), ("extcap_n4o1", ["-n", "4", "-o", "1"])):
+        ob = os.path.join(work, name + ".bin")
+        r = subprocess.run([os.path.join(REF, "ref_extcap"), idx, rb, ob, *args], check=True, capture_output=True,
+                           text=True)
+        recs = read_extcap(ob)
+        out = dict(hdr=np.stack([x["hdr"] for x in recs]), opt=np.stack([x["opt"] for x in recs]),
+                   aln_in=np.stack([x["aln_in"] for x in recs]), seq=np.concatenate([x["seq"] for x in recs]),
+                   bid=np.concatenate([x["bid"] for x in recs]), tail=np.stack([x["tail"] for x in recs]),
+                   aln_out=np.stack([x["aln_out"] for x in recs]))
+        np.savez_compressed(os.path.join(GOLD, name + ".npz"), **out)
+        ret = out["tail"][:, 0]
+        print(f"{name}: {len(recs)} calls ({r.stderr.strip()}): {int((out['hdr'][:, 0] == 1).sum())} backward; "
+              f"ret 1: {int((ret == 1).sum())}, 2: {int((ret == 2).sum())}, -1: {int((ret == -1).sum())}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ecoli", action="store_true")
     ap.add_argument("--dropin", action="store_true")
     ap.add_argument("--sa", action="store_true")
     ap.add_argument("--mgcap", action="store_true")
+    ap.add_argument("--extcap", action="store_true")
     a = ap.parse_args()
     if not os.path.exists(os.path.join(REF, "ref_probe")):
         sys.exit("build oracle/_ref first: make -C oracle -f ref.mk")
@@ -499,6 +550,8 @@ def main():
             sa_cases(work)
         elif a.mgcap:
             mgcap_cases(work)
+        elif a.extcap:
+            extcap_cases(work)
         else:
             tiny_cases(work)
 
