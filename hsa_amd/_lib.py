@@ -29,7 +29,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "bwt_match_gap", "bwt_match_gap_batch", "hsa_splice_seeds_device", "hsa_pass_times",
     "hsa_cal_sa_reg_gap_multi", "hsa_index_create_device64", "hsa_index_is64", "hsa_occ4_batch64",
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
-    "hsa_build_bwt_index_device",
+    "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
 ]
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
@@ -85,6 +85,10 @@ JOB_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("max_diff", "<i4"), ("see
 # hsa_mg_job_t (include/hsa_gpu.h): one direct bwt_match_gap call's widths and strand
 MG_DTYPE = np.dtype([("wb_off", "<u8"), ("ws_off", "<u8"), ("strand", "<i4"), ("seed", "<i4")])
 SEED_NONE, SEED_OWN, SEED_ALIAS = 0, 1, 2
+# hsa_ext_job_t (include/hsa_gpu.h): one seed extension of the splice path
+EXT_DTYPE = np.dtype([("dir", "<i4"), ("len", "<i4"), ("max_pos", "<i4"), ("regime", "<i4"), ("lo", "<i4"),
+                      ("n", "<i4"), ("off", "<u8"), ("aln", "<u4", (9,)), ("pad", "<u4")])
+assert EXT_DTYPE.itemsize == 72
 
 
 def regime_of(opt: dict, n_stacks: int, max_diff: int) -> "Regime":
@@ -192,6 +196,9 @@ def lib():
     if hasattr(L, "hsa_build_bwt_index_device"):
         L.hsa_build_bwt_index_device.argtypes = [C.c_int, C.c_uint64, vp, vp, C.POINTER(C.c_uint64), u64, C.c_uint32,
                                                  vp]
+    if hasattr(L, "hsa_extend_batch"):
+        L.hsa_extend_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, C.c_int, u8, i32, C.c_size_t, i32, i32,
+                                       u32]
     f32 = np.ctypeslib.ndpointer(np.float32, flags="C")
     L.hsa_pass_times.argtypes = [vp, C.c_int, f32, f32]
     if hasattr(L, "hsa_cal_sa_reg_gap_multi"):      # (older A/B builds lack it)
@@ -375,6 +382,21 @@ class GpuIndex:
         tot = check(lib().hsa_search_batch(self.h, rg, len(regimes), jobs.ctypes.data, n, codes, len(codes), n_aln,
                                            flags, hoff, C.byref(hp), C.byref(st)))
         return n_aln, flags, hoff, _take_hits(hp, tot), st.as_dict()
+
+    def extend(self, regimes, jobs, codes, bids):
+        """hsa_extend_batch: jobs (EXT_DTYPE), the windows' codes / bids; returns
+        (ret, max_pos, aln (n, 9))."""
+        n = len(jobs)
+        rg = (Regime * len(regimes))(*regimes)
+        ret = np.zeros(n, np.int32)
+        mp = np.zeros(n, np.int32)
+        aln = np.zeros((n, 9), np.uint32)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        bids = np.ascontiguousarray(bids, np.int32)
+        check(lib().hsa_extend_batch(self.h, rg, len(regimes), np.ascontiguousarray(jobs).ctypes.data, n,
+                                     codes if len(codes) else np.zeros(1, np.uint8),
+                                     bids if len(bids) else np.zeros(1, np.int32), len(codes), ret, mp, aln))
+        return ret, mp, aln
 
     def match_gap(self, regimes, jobs, mg, codes, widths):
         """hsa_match_gap_batch: direct bwt_match_gap calls with caller widths.

@@ -30,6 +30,8 @@
 #pragma weak hsa_splice_prefetch
 #pragma weak hsa_splice_memo_clear
 #pragma weak hsa_splice_memo_stats
+#pragma weak hsa_splice_extend_active
+#pragma weak hsa_splice_run
 
 _Static_assert(sizeof(bwt_aln1_t) == 36, "bwt_aln1_t layout");
 _Static_assert(sizeof(gap_opt_t) == 64, "gap_opt_t layout");
@@ -522,6 +524,16 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
             free(fa); free(fp); free(fo); free(rc);
         }
     }
+    /* the host's splice path for the fallback reads: all of them at once as coroutines
+     * whose seed extensions run batched on the GPU, when the host calls our
+     * bwt_extend_* (bwtext_gpu.c); else one read at a time, as the reference */
+    const int batched = have_splice && hsa_splice_run && hsa_splice_extend_active && hsa_splice_extend_active();
+    hsa_splice_read_t *sr = NULL;
+    int *sr_idx = NULL, n_sr = 0;
+    if (batched) {
+        sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)n_seqs + 1));
+        sr_idx = (int *)malloc(sizeof(int) * ((size_t)n_seqs + 1));
+    }
     for (int i = 0; i < n_seqs; ++i) {
         bwa_seq_t *p = seqs + i;
         if (flags[i] & HSA_RF_NFILTER) continue;               /* untouched (:314-317) */
@@ -535,6 +547,14 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
             continue;
         }
         if (!(flags[i] & HSA_F_FALLBACK) || !have_splice) continue;
+        gap_opt_t lo = local;                                   /* aux->opt = &local_opt (:363) */
+        lo.max_diff = sp[2 * i];
+        lo.seed_len = sp[2 * i + 1];
+        if (batched) {
+            sr[n_sr].seq = p->seq; sr[n_sr].len = (int)p->len; sr[n_sr].opt = lo;
+            sr_idx[n_sr++] = i;
+            continue;
+        }
         if (!aux.stack) {
             aux.bi_bwt = (Idx2BWT *)bi_bwt;
             aux.arr = arr;
@@ -545,9 +565,6 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
             aux.rc_seq = (ubyte_t *)calloc(max_len + 1, 1);
             aux.stack = ref_stack_new(n_stacks);
         }
-        gap_opt_t lo = local;                                   /* aux->opt = &local_opt (:363) */
-        lo.max_diff = sp[2 * i];
-        lo.seed_len = sp[2 * i + 1];
         aux.opt = &lo;
         aux.seq = p->seq;
         aux.len = (int)p->len;
@@ -562,6 +579,22 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
         p->n_aln = na;
         if (na == 0) { free(p->aln); p->aln = NULL; }
     }
+    if (n_sr > 0) {
+        bwt_aln1_t **so = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)n_sr);
+        int *sn = (int *)malloc(sizeof(int) * (size_t)n_sr);
+        const long launches = hsa_splice_run(bi_bwt, arr, max_len, n_stacks, n_sr, sr, so, sn);
+        for (int k = 0; k < n_sr; ++k) {
+            bwa_seq_t *p = seqs + sr_idx[k];
+            p->aln = so[k];
+            p->n_aln = sn[k];
+            if (sn[k] == 0) { free(p->aln); p->aln = NULL; }
+        }
+        if (getenv("HSA_VERBOSE"))
+            fprintf(stderr, "[hsa] splice path: %d reads as coroutines, seed extensions in %ld GPU launches\n", n_sr,
+                    launches);
+        free(so); free(sn);
+    }
+    free(sr); free(sr_idx);
     if (aux.stack) {
         free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);
         ref_stack_free(aux.stack);

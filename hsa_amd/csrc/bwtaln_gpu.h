@@ -24,4 +24,15 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux);
 void hsa_splice_memo_clear(void);
 void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses);
 
+/* the splice path's seed extensions and its batched runner (bwtext_gpu.c; referred to
+ * weakly as well) */
+typedef struct {
+    const ubyte_t *seq;        /* the read (bwa_seq_t.seq) */
+    int len;
+    gap_opt_t opt;             /* local_opt as bwt_splice_match receives it for this read */
+} hsa_splice_read_t;
+int hsa_splice_extend_active(void);
+long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int n_stacks, int n,
+                    const hsa_splice_read_t *reads, bwt_aln1_t **out, int *n_out);
+
 #endif

@@ -1,0 +1,307 @@
+/*
+ * bwtext_gpu.c -- the splice path's seed extensions on the GPU, and the batched runner
+ * of the host's splice path that feeds them.
+ *
+ * bwt_extend_backward / bwt_extend_foreward (bwtgap.c:640-663, declared bwtgap.h) are
+ * what bwt_splice_match (bwtgap.c:748) calls to grow a mapped seed across the read:
+ * bwt_backtracing_search (:346-511), the splice path's costliest host step once its
+ * bwt_match_gap calls run on the GPU.  Each call depends on the previous one's result,
+ * so one read's calls cannot be batched; the calls of many reads can.  So the drop-in
+ * bwa_cal_sa_reg_gap runs bwt_splice_match -- the host's own code, unchanged -- for
+ * every fallback read of a batch as a coroutine (ucontext, one stack each, one host
+ * thread): a coroutine that calls bwt_extend_* parks its call and yields; when every
+ * running coroutine is parked or done, one hsa_extend_batch launch answers all parked
+ * calls and they resume.  bwt_splice_match is a function of its read alone (its
+ * splice-site record, bwt_array_t, is inert: bwt_array_insert and
+ * bwt_find_split_pos_by_record return at their first line, bwt_array.c:34, :77), so
+ * the reads' order does not change any result.
+ *
+ * Its own object: a host opts in by linking bwtext_gpu.o and weakening its own
+ * bwt_extend_backward / bwt_extend_foreward.
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <ucontext.h>
+
+#include "../../include/hsa_bwtaln.h"
+#include "bwtaln_gpu.h"
+
+#define CO_STACK (512u << 10)     /* C stack per coroutine (the host's splice code + ours) */
+#define CO_MAX 4096               /* coroutines alive at once */
+
+/* One parked extension call. */
+typedef struct {
+    int dir, len, max_pos;
+    hsa_regime_t rg;
+    int lo, n;
+    uint8_t *seq;                 /* window copies */
+    int32_t *bid;
+    bwt_aln1_t *aln;              /* the caller's, updated on resume */
+    int *max_pos_io;
+    int ret;
+} ext_req_t;
+
+typedef struct {
+    ucontext_t uc;
+    void *stack;
+    int read;                     /* index into the run's reads, -1 idle */
+    int state;                    /* 0 runnable, 1 parked, 2 done */
+    bwt_aux_t aux;
+    gap_opt_t opt;
+    int len;                      /* the read's length */
+    bwt_aln1_t *result;
+    int n_aln;
+    ext_req_t req;
+} co_t;
+
+static __thread co_t *tl_co;          /* the running coroutine, or NULL outside the runner */
+static __thread ucontext_t *tl_sched; /* the runner's context */
+
+static int imin(int a, int b) { return a < b ? a : b; }
+static int imax(int a, int b) { return a > b ? a : b; }
+
+/* The window of read positions a call reads (include/hsa_gpu.h, hsa_ext_job_t):
+ * backward [min(start - len, max_pos), max(start, max_pos + 1)], forward
+ * [min(end, max_pos - 1), max(end + len, max_pos)]; empty for a negative len without
+ * NONSTOP (the seed entry's score field is 2047 then: the search stops at its first
+ * pop).  Returns 0, or -1 when the reference's search would read undefined memory. */
+static int call_window(const bwt_aux_t *aux, const bwt_aln1_t *aln, int dir, int max_pos, int read_len, int *lo,
+                       int *n)
+{
+    const int len = aux->len;
+    if (len < 0 && !(aux->opt->mode & BWA_MODE_NONSTOP)) { *lo = 0; *n = 0; return 0; }
+    int l, h;
+    if (dir) { l = imin(aln->start - len, max_pos); h = imax(aln->start, max_pos + 1); }
+    else { l = imin(aln->end, max_pos - 1); h = imax(aln->end + len, max_pos); }
+    if (len < 0 || l < 0 || (read_len >= 0 && h > read_len)) return -1;
+    *lo = l;
+    *n = h - l + 1;
+    return 0;
+}
+
+static void fill_req(ext_req_t *q, bwt_aux_t *aux, bwt_aln1_t *aln, int *max_pos, int dir, int read_len)
+{
+    q->dir = dir;
+    q->len = aux->len;
+    q->max_pos = *max_pos;
+    q->rg = hsa_regime_of(aux->opt, aux->stack->n_stacks, aux->opt->max_diff);
+    q->rg.mode = aux->opt->mode & (BWA_MODE_GAPE | BWA_MODE_LOGGAP | BWA_MODE_NONSTOP);   /* as the search reads it */
+    q->rg.max_gapo = aux->opt->max_gapo;
+    q->rg.max_gape = aux->opt->max_gape;
+    if (call_window(aux, aln, dir, *max_pos, read_len, &q->lo, &q->n)) {
+        fprintf(stderr, "[bwt_extend_%s] extension of %d positions from [%d, %d] toward %d reads outside the read "
+                        "(undefined in the reference)\n", dir ? "backward" : "foreward", aux->len, aln->start, aln->end,
+                *max_pos);
+        exit(1);
+    }
+    const ubyte_t *seq = aux->strand == 0 ? aux->seq : aux->rc_seq;
+    const bwt_width_t *w = dir ? aux->width_back : aux->width_fore;
+    /* the sequence is read only at [start - len, start - 1] / [end + 1, end + len] */
+    const int s0 = dir ? aln->start - aux->len : aln->end + 1, s1 = dir ? aln->start - 1 : aln->end + aux->len;
+    q->seq = (uint8_t *)malloc((size_t)q->n + 1);
+    q->bid = (int32_t *)malloc(sizeof(int32_t) * ((size_t)q->n + 1));
+    for (int p = 0; p < q->n; ++p) {
+        const int pos = q->lo + p;
+        q->seq[p] = pos >= s0 && pos <= s1 ? seq[pos] : 4;
+        q->bid[p] = w[pos].bid;
+    }
+    q->aln = aln;
+    q->max_pos_io = max_pos;
+}
+
+/* Answer parked calls q[0..n) in one batch. */
+static void run_reqs(hsa_index_t *ix, ext_req_t *const *q, int n)
+{
+    if (n <= 0) return;
+    hsa_regime_t *rg = (hsa_regime_t *)calloc((size_t)n, sizeof(hsa_regime_t));
+    hsa_ext_job_t *jobs = (hsa_ext_job_t *)calloc((size_t)n, sizeof(hsa_ext_job_t));
+    size_t tot = 0;
+    for (int j = 0; j < n; ++j) tot += (size_t)q[j]->n;
+    uint8_t *codes = (uint8_t *)calloc(tot + 1, 1);
+    int32_t *bids = (int32_t *)calloc(tot + 1, sizeof(int32_t));
+    int nr = 0;
+    size_t off = 0;
+    for (int j = 0; j < n; ++j) {
+        int r = 0;
+        while (r < nr && memcmp(&rg[r], &q[j]->rg, sizeof(hsa_regime_t))) ++r;
+        if (r == nr) rg[nr++] = q[j]->rg;
+        hsa_ext_job_t *J = jobs + j;
+        J->dir = q[j]->dir; J->len = q[j]->len; J->max_pos = q[j]->max_pos; J->regime = r;
+        J->lo = q[j]->lo; J->n = q[j]->n; J->off = off;
+        memcpy(J->aln, q[j]->aln, sizeof(bwt_aln1_t));
+        memcpy(codes + off, q[j]->seq, (size_t)q[j]->n);
+        memcpy(bids + off, q[j]->bid, sizeof(int32_t) * (size_t)q[j]->n);
+        off += (size_t)q[j]->n;
+    }
+    int32_t *ret = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    int32_t *mp = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    uint32_t *aln = (uint32_t *)malloc(sizeof(bwt_aln1_t) * (size_t)n);
+    int rc = hsa_extend_batch(ix, rg, nr, jobs, n, codes, bids, tot, ret, mp, aln);
+    if (rc) hsa_gpu_fatal("GPU seed extension", rc);
+    for (int j = 0; j < n; ++j) {
+        memcpy(q[j]->aln, aln + 9 * (size_t)j, sizeof(bwt_aln1_t));
+        *q[j]->max_pos_io = mp[j];
+        q[j]->ret = ret[j];
+        free(q[j]->seq); free(q[j]->bid);
+        q[j]->seq = NULL; q[j]->bid = NULL;
+    }
+    free(rg); free(jobs); free(codes); free(bids); free(ret); free(mp); free(aln);
+}
+
+static int extend(bwt_aux_t *aux, bwt_aln1_t *aln, int *max_pos, int dir)
+{
+    co_t *me = tl_co;
+    if (me) {                             /* inside the runner: park the call and yield */
+        fill_req(&me->req, aux, aln, max_pos, dir, me->len);
+        me->state = 1;
+        swapcontext(&me->uc, tl_sched);
+        return me->req.ret;
+    }
+    ext_req_t q;                          /* a direct call: a batch of one */
+    fill_req(&q, aux, aln, max_pos, dir, -1);
+    ext_req_t *qp = &q;
+    run_reqs(hsa_gpu_index_of(aux->bi_bwt), &qp, 1);
+    return q.ret;
+}
+
+/* bwt_extend_backward (bwtgap.c:640-649): extend aln backward, at least to *_left. */
+int bwt_extend_backward(bwt_aux_t *aux, bwt_aln1_t *aln, int *_left) { return extend(aux, aln, _left, 1); }
+
+/* bwt_extend_foreward (bwtgap.c:654-663): extend aln forward, at least to *_right. */
+int bwt_extend_foreward(bwt_aux_t *aux, bwt_aln1_t *aln, int *_right) { return extend(aux, aln, _right, 0); }
+
+extern __typeof__(bwt_extend_backward) hsa_own_extend_backward
+    __attribute__((alias("bwt_extend_backward"), visibility("hidden")));
+
+/* Whether the host's bwt_splice_match calls these extensions (the host linked
+ * bwtext_gpu.o and weakened its own): only then does the batched runner pay. */
+int hsa_splice_extend_active(void)
+{
+    int (*volatile resolved)(bwt_aux_t *, bwt_aln1_t *, int *) = bwt_extend_backward;
+    return resolved == hsa_own_extend_backward;
+}
+
+/* gap_init_stack's layout (bwtgap.c:13-27): the host's splice code resets and reads it */
+static gap_stack_t *stack_new(int n_stacks)
+{
+    gap_stack_t *s = (gap_stack_t *)calloc(1, sizeof(gap_stack_t));
+    s->n_stacks = n_stacks;
+    s->stacks = (gap_stack1_t *)calloc((size_t)n_stacks, sizeof(gap_stack1_t));
+    for (int i = 0; i < n_stacks; ++i) {
+        s->stacks[i].m_entries = 4;
+        s->stacks[i].stack = (gap_entry_t *)calloc(4, sizeof(gap_entry_t));
+    }
+    return s;
+}
+
+static void stack_free(gap_stack_t *s)
+{
+    for (int i = 0; i < s->n_stacks; ++i) free(s->stacks[i].stack);
+    free(s->stacks);
+    free(s);
+}
+
+static void co_entry(void)
+{
+    co_t *me = tl_co;
+    me->result = bwt_splice_match(&me->aux, &me->n_aln);
+    me->state = 2;
+    /* returning resumes uc_link: the runner */
+}
+
+/* Start coroutine c on read r: the aux bwa_cal_sa_reg_gap hands bwt_splice_match
+ * (bwtaln.c:326-364: seq, len, rc_seq, strand 0, opt = local_opt of that read). */
+static void co_start(co_t *c, int r, const hsa_splice_read_t *rd)
+{
+    c->read = r;
+    c->state = 0;
+    c->opt = rd->opt;
+    c->len = rd->len;
+    c->aux.opt = &c->opt;
+    c->aux.seq = (ubyte_t *)rd->seq;
+    c->aux.len = rd->len;
+    c->aux.strand = 0;
+    memset(c->aux.rc_seq, 0, (size_t)c->aux.max_len);
+    for (int j = 0; j < rd->len; ++j) {
+        const ubyte_t x = rd->seq[rd->len - 1 - j];
+        c->aux.rc_seq[j] = x < 4 ? (ubyte_t)(3 - x) : x;
+    }
+    c->result = NULL;
+    c->n_aln = 0;
+    getcontext(&c->uc);
+    c->uc.uc_stack.ss_sp = c->stack;
+    c->uc.uc_stack.ss_size = CO_STACK;
+    c->uc.uc_link = tl_sched;
+    makecontext(&c->uc, co_entry, 0);
+}
+
+/* bwt_splice_match for reads[0..n) (see the file comment): out[r] / n_out[r] are what
+ * bwt_splice_match(aux of read r) returns.  Returns the number of GPU extension
+ * launches. */
+long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int n_stacks, int n,
+                    const hsa_splice_read_t *reads, bwt_aln1_t **out, int *n_out)
+{
+    if (n <= 0) return 0;
+    if (!bwt_splice_match) { for (int r = 0; r < n; ++r) { out[r] = NULL; n_out[r] = 0; } return 0; }
+    hsa_index_t *ix = hsa_gpu_index_of(bi);
+    const int W = n < CO_MAX ? n : CO_MAX;
+    co_t *co = (co_t *)calloc((size_t)W, sizeof(co_t));
+    ucontext_t sched;
+    tl_sched = &sched;
+    for (int k = 0; k < W; ++k) {
+        co_t *c = co + k;
+        c->stack = mmap(NULL, CO_STACK, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+        if (c->stack == MAP_FAILED) { fprintf(stderr, "[hsa_splice_run] cannot map a coroutine stack\n"); exit(1); }
+        c->aux.bi_bwt = (Idx2BWT *)bi;
+        c->aux.arr = arr;
+        c->aux.max_len = max_len;
+        c->aux.width_back = (bwt_width_t *)calloc((size_t)max_len + 1, sizeof(bwt_width_t));
+        c->aux.width_fore = (bwt_width_t *)calloc((size_t)max_len + 1, sizeof(bwt_width_t));
+        c->aux.width_seed = (bwt_width_t *)calloc((size_t)max_len + 1, sizeof(bwt_width_t));
+        c->aux.rc_seq = (ubyte_t *)calloc((size_t)max_len + 1, 1);
+        c->aux.stack = stack_new(n_stacks);
+        c->read = -1;
+    }
+    ext_req_t **pend = (ext_req_t **)malloc(sizeof(ext_req_t *) * (size_t)W);
+    int next = 0, live = 0;
+    long launches = 0;
+    for (int k = 0; k < W; ++k) { co_start(co + k, next, reads + next); ++next; ++live; }
+    while (live > 0) {
+        /* run every runnable coroutine until it parks or finishes; a finished one takes
+         * the next read at once */
+        for (int k = 0; k < W; ++k) {
+            co_t *c = co + k;
+            while (c->read >= 0 && c->state == 0) {
+                tl_co = c;
+                swapcontext(&sched, &c->uc);
+                tl_co = NULL;
+                if (c->state == 2) {
+                    out[c->read] = c->result;
+                    n_out[c->read] = c->n_aln;
+                    if (next < n) { co_start(c, next, reads + next); ++next; }
+                    else { c->read = -1; --live; }
+                }
+            }
+        }
+        int np = 0;
+        for (int k = 0; k < W; ++k)
+            if (co[k].read >= 0 && co[k].state == 1) pend[np++] = &co[k].req;
+        if (np == 0) continue;
+        run_reqs(ix, pend, np);
+        ++launches;
+        for (int k = 0; k < W; ++k)
+            if (co[k].read >= 0 && co[k].state == 1) co[k].state = 0;
+    }
+    for (int k = 0; k < W; ++k) {
+        co_t *c = co + k;
+        munmap(c->stack, CO_STACK);
+        free(c->aux.width_back); free(c->aux.width_fore); free(c->aux.width_seed); free(c->aux.rc_seq);
+        stack_free(c->aux.stack);
+    }
+    free(co); free(pend);
+    tl_sched = NULL;
+    return launches;
+}

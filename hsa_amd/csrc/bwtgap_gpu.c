@@ -247,7 +247,7 @@ static const memo_ent_t *memo_get(const bwt_aux_t *a)
 static void batch_into_memo(bwt_aux_t *calls, int c, bwt_width_t **win, int *n_out)
 {
     if (c <= 0) return;
-    bwt_aux_t **cp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)c);
+    bwt_aux_t **cp = (bwt_aux_t **)calloc((size_t)c, sizeof(bwt_aux_t *));
     bwt_aln1_t **out = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)c);
     for (int i = 0; i < c; ++i) cp[i] = calls + i;
     bwt_match_gap_batch(cp, c, out, n_out);

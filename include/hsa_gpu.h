@@ -23,6 +23,9 @@
  *                         (bwtgap.c:797-812) for every fallback read of a device batch.
  *   hsa_sa_position_*  -- BWTSaValue (BWT.c:1195) + BWTRetrievePositionFromSAIndex
  *                         (2BWT-Interface.c:329).
+ *   hsa_extend_batch   -- bwt_extend_backward / bwt_extend_foreward (bwtgap.c:640-663,
+ *                         bwt_backtracing_search :346-511): the splice path's seed
+ *                         extensions.
  *
  * Errors: every call returns 0 on success or a negative HSA_E* code and leaves a
  * message readable with hsa_last_error().  The library never falls back to a CPU
@@ -92,6 +95,38 @@ int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t *pos, uint
 int hsa_step_batch(hsa_index_t *ix, size_t n, const uint32_t *klrr, uint32_t *out16);
 int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
                     const uint8_t *codes, size_t codes_len, uint32_t *width_out /* 2*(len+1) words per read, packed */);
+
+/* One seed extension of the splice path: bwt_extend_backward (dir 1) or
+ * bwt_extend_foreward (dir 0), bwtgap.c:640-663 -> bwt_backtracing_search (:346-511).
+ * The call extends hit `aln` (bwt_aln1_t words, bwtaln.h:41-50) over `len` read
+ * positions toward max_pos (*_left / *_right).  It reads the strand sequence and the
+ * direction's width bids (width_back backward, width_fore forward) only inside the
+ * read-position window [lo, lo + n) -- backward [min(start - len, max_pos),
+ * max(start, max_pos + 1)], forward [min(end, max_pos - 1), max(end + len, max_pos)]
+ * (an empty window for a negative len without NONSTOP, whose seed entry stops the
+ * search at its first pop) -- given at codes[off .. off + n) and bids[off .. off + n).
+ * The regime holds aux->opt's fields with max_diff exact, and n_stacks =
+ * aux->stack->n_stacks. */
+typedef struct {
+    int32_t dir;
+    int32_t len;
+    int32_t max_pos;
+    int32_t regime;
+    int32_t lo, n;
+    uint64_t off;
+    uint32_t aln[9];
+    uint32_t pad;
+} hsa_ext_job_t;
+
+/* n extensions in one batch (one lane per call; stacks in HBM, grown in capacity
+ * passes up to the reference's max_entries bound).  Outputs per call: ret (1, 2 or -1
+ * as the reference), max_pos after, and the 9 words of the hit after.  A call whose
+ * search the reference leaves undefined (a score past the stack's buckets, a rank
+ * position past the text, a read position outside its window) fails the batch with
+ * HSA_E_ARG. */
+int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_ext_job_t *jobs, int n,
+                     const uint8_t *codes, const int32_t *bids, size_t win_len, int32_t *ret, int32_t *max_pos,
+                     uint32_t *aln_out);
 
 /* Search statistics (summed over the call). */
 typedef struct {

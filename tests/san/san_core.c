@@ -152,3 +152,26 @@ int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint3
     }
     return 0;
 }
+
+/* hsa_extend_batch = bwt_extend_backward / bwt_extend_foreward per call (or_extend). */
+int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_ext_job_t *jobs, int n,
+                     const uint8_t *codes, const int32_t *bids, size_t win_len, int32_t *ret, int32_t *max_pos,
+                     uint32_t *aln_out)
+{
+    (void)n_regimes; (void)win_len;
+    for (int j = 0; j < n; ++j) {
+        const hsa_ext_job_t *J = jobs + j;
+        const hsa_regime_t *R = regimes + J->regime;
+        or_opt_t o;
+        or_init_opt(&o);
+        o.s_mm = R->s_mm; o.s_gapo = R->s_gapo; o.s_gape = R->s_gape; o.mode = R->mode;
+        o.indel_end_skip = R->indel_end_skip; o.max_del_occ = R->max_del_occ; o.max_entries = R->max_entries;
+        o.max_gapo = R->max_gapo; o.max_gape = R->max_gape; o.max_diff = R->max_diff;
+        memcpy(aln_out + 9 * (size_t)j, J->aln, 36);
+        int mp = J->max_pos;
+        ret[j] = or_extend((const or_index_t *)ix, &o, R->n_stacks, J->dir, J->len, codes + J->off, bids + J->off,
+                           J->lo, J->n, aln_out + 9 * (size_t)j, &mp);
+        max_pos[j] = mp;
+    }
+    return 0;
+}
