@@ -22,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/hsa_bwtaln.h"
 #include "bwtaln_gpu.h"
@@ -32,6 +33,10 @@
 #pragma weak hsa_splice_memo_stats
 #pragma weak hsa_splice_extend_active
 #pragma weak hsa_splice_run
+#pragma weak hsa_splice_width_active
+#pragma weak hsa_splice_widths_prefetch
+#pragma weak hsa_splice_wmemo_clear
+#pragma weak hsa_splice_wmemo_stats
 
 _Static_assert(sizeof(bwt_aln1_t) == 36, "bwt_aln1_t layout");
 _Static_assert(sizeof(gap_opt_t) == 64, "gap_opt_t layout");
@@ -445,6 +450,13 @@ static void ref_stack_free(gap_stack_t *s)
     free(s);
 }
 
+double hsa_now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
 void hsa_gpu_fatal(const char *what, long rc)
 {
     /* the reference's convention for unrecoverable errors: message + exit(1) */
@@ -475,6 +487,7 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     int32_t *sp = (int32_t *)malloc(sizeof(int32_t) * 2 * ((size_t)n_seqs + 1));
     gap_opt_t local = *opt;                 /* local_opt as of :254, before the call mutates *opt */
     uint32_t *hits = NULL;
+    const double t0 = hsa_now();
     long nh = hsa_cal_sa_reg_gap_multi(slots, n_slots, opt, n_seqs, lens, offs, codes, tot, n_aln, flags, hoff, &hits, sp,
                                        NULL);
     if (nh < 0) hsa_gpu_fatal("GPU search", nh);
@@ -488,7 +501,9 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     const int n_stacks = hsa_aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
     /* the splice path's seed searches of every fallback read in one GPU batch, when
      * the host's bwt_splice_match calls our bwt_match_gap (bwtgap_gpu.c) */
-    int prefetched = 0;
+    int prefetched = 0, wprefetched = 0;
+    double t_pf = 0.0;
+    const double t1 = hsa_now();
     if (have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active()) {
         int nf = 0;
         for (int i = 0; i < n_seqs; ++i)
@@ -519,7 +534,15 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
                 fp[q] = fa + q;
                 ++q;
             }
+            t_pf = hsa_now();
             hsa_splice_prefetch(bi_bwt, nf, fp);
+            /* and the widths the splice path computes (bwtext_gpu.c), when the host calls
+             * our bwt_cal_width */
+            if (hsa_splice_width_active && hsa_splice_width_active()) {
+                hsa_splice_widths_prefetch(bi_bwt, nf, fp);
+                wprefetched = 1;
+            }
+            t_pf = hsa_now() - t_pf;
             prefetched = 1;
             free(fa); free(fp); free(fo); free(rc);
         }
@@ -579,6 +602,7 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
         p->n_aln = na;
         if (na == 0) { free(p->aln); p->aln = NULL; }
     }
+    const double t2 = hsa_now();
     if (n_sr > 0) {
         bwt_aln1_t **so = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)n_sr);
         int *sn = (int *)malloc(sizeof(int) * (size_t)n_sr);
@@ -595,6 +619,9 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
         free(so); free(sn);
     }
     free(sr); free(sr_idx);
+    if (getenv("HSA_VERBOSE"))
+        fprintf(stderr, "[hsa] batch of %d reads: search %.3f s, splice prefetch %.3f s, splice path %.3f s "
+                        "(%d fallback reads)\n", n_seqs, t1 - t0, t_pf, hsa_now() - t2 + (t2 - t1 - t_pf), n_sr);
     if (aux.stack) {
         free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);
         ref_stack_free(aux.stack);
@@ -607,6 +634,15 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
                     (unsigned long long)mh, (unsigned long long)mm);
         }
         hsa_splice_memo_clear();
+    }
+    if (wprefetched) {
+        if (getenv("HSA_VERBOSE")) {
+            uint64_t wh = 0, wm = 0;
+            hsa_splice_wmemo_stats(&wh, &wm);
+            fprintf(stderr, "[hsa] splice widths: %llu bwt_cal_width calls answered from the batch, %llu run alone\n",
+                    (unsigned long long)wh, (unsigned long long)wm);
+        }
+        hsa_splice_wmemo_clear();
     }
     hsa_free(hits);
     free(lens); free(offs); free(codes); free(n_aln); free(flags); free(hoff); free(sp);

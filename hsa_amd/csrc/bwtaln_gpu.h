@@ -12,6 +12,8 @@ hsa_index_t *const *hsa_gpu_slots_of(const Idx2BWT *bi, int *n);
 void hsa_gpu_set_error_text(const char *msg);
 /* the reference's convention for unrecoverable errors: message + exit(1) */
 void hsa_gpu_fatal(const char *what, long rc) __attribute__((noreturn));
+/* monotonic seconds (timing logs) */
+double hsa_now(void);
 /* aln_score (bwtgap.h) */
 int hsa_aln_score(const gap_opt_t *o, int m, int g, int e);
 /* the search options of one option block (the fields bwt_match_gap reads) */
@@ -32,6 +34,10 @@ typedef struct {
     gap_opt_t opt;             /* local_opt as bwt_splice_match receives it for this read */
 } hsa_splice_read_t;
 int hsa_splice_extend_active(void);
+int hsa_splice_width_active(void);
+int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux);
+void hsa_splice_wmemo_clear(void);
+void hsa_splice_wmemo_stats(uint64_t *hits, uint64_t *misses);
 long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int n_stacks, int n,
                     const hsa_splice_read_t *reads, bwt_aln1_t **out, int *n_out);
 

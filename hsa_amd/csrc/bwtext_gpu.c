@@ -16,10 +16,16 @@
  * bwt_find_split_pos_by_record return at their first line, bwt_array.c:34, :77), so
  * the reads' order does not change any result.
  *
+ * The same object answers the splice path's bwt_cal_width calls (bwtaln.c:73, called at
+ * bwtgap.c:807, :867-868, :871-872, :915) from a table the drop-in fills on the GPU
+ * ahead of the splice path (hsa_splice_widths_prefetch): every width array those calls
+ * can ask for, per fallback read and strand, keyed by (type, length, sequence).
+ *
  * Its own object: a host opts in by linking bwtext_gpu.o and weakening its own
- * bwt_extend_backward / bwt_extend_foreward.
+ * bwt_extend_backward / bwt_extend_foreward / bwt_cal_width.
  */
 #define _GNU_SOURCE
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -184,6 +190,198 @@ int hsa_splice_extend_active(void)
     return resolved == hsa_own_extend_backward;
 }
 
+/* ------------------------------------------------------------ width table
+ * bwt_cal_width(bi, len, str, width, type) depends on (type, len, str[0..len)) only
+ * (and the index).  Type 1 writes entries 0..len, type 0 entries 1..len (bwtaln.c:85-115);
+ * the table stores the written entries and the return value. */
+typedef struct {
+    uint64_t h;
+    uint8_t *key;            /* type, len, the sequence */
+    size_t key_len;
+    bwt_width_t *w;          /* entries 0..len (entry 0 unused for type 0) */
+    int len, type, ret;
+} wm_ent_t;
+
+static wm_ent_t *g_wm;
+static size_t g_wm_cap, g_wm_n;
+static uint64_t g_wm_hits, g_wm_misses;
+static pthread_mutex_t g_wm_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static size_t wkey(int type, int len, const ubyte_t *str, uint8_t *buf)
+{
+    buf[0] = (uint8_t)type;
+    memcpy(buf + 1, &len, 4);
+    memcpy(buf + 5, str, (size_t)len);
+    return 5 + (size_t)len;
+}
+
+static uint64_t wfnv(const uint8_t *p, size_t n)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return h | 1;
+}
+
+static void wm_put(int type, int len, const ubyte_t *str, const uint32_t *w, int ret)   /* caller holds g_wm_mu */
+{
+    if (2 * (g_wm_n + 1) > g_wm_cap) {
+        size_t cap = g_wm_cap ? g_wm_cap * 2 : 4096;
+        wm_ent_t *t = (wm_ent_t *)calloc(cap, sizeof(wm_ent_t));
+        for (size_t i = 0; i < g_wm_cap; ++i) {
+            if (!g_wm[i].h) continue;
+            size_t j = g_wm[i].h & (cap - 1);
+            while (t[j].h) j = (j + 1) & (cap - 1);
+            t[j] = g_wm[i];
+        }
+        free(g_wm);
+        g_wm = t;
+        g_wm_cap = cap;
+    }
+    uint8_t *key = (uint8_t *)malloc((size_t)len + 5);
+    const size_t kl = wkey(type, len, str, key);
+    const uint64_t h = wfnv(key, kl);
+    size_t j = h & (g_wm_cap - 1);
+    while (g_wm[j].h) {
+        if (g_wm[j].h == h && g_wm[j].key_len == kl && !memcmp(g_wm[j].key, key, kl)) { free(key); return; }
+        j = (j + 1) & (g_wm_cap - 1);
+    }
+    wm_ent_t *e = g_wm + j;
+    e->h = h; e->key = key; e->key_len = kl; e->len = len; e->type = type; e->ret = ret;
+    e->w = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)len + 1));
+    for (int i = 0; i <= len; ++i) { e->w[i].w = w[2 * i]; e->w[i].bid = (int)w[2 * i + 1]; }
+    ++g_wm_n;
+}
+
+void hsa_splice_wmemo_clear(void)
+{
+    pthread_mutex_lock(&g_wm_mu);
+    for (size_t i = 0; i < g_wm_cap; ++i)
+        if (g_wm[i].h) { free(g_wm[i].key); free(g_wm[i].w); }
+    free(g_wm);
+    g_wm = NULL;
+    g_wm_cap = g_wm_n = 0;
+    pthread_mutex_unlock(&g_wm_mu);
+}
+
+void hsa_splice_wmemo_stats(uint64_t *hits, uint64_t *misses)
+{
+    pthread_mutex_lock(&g_wm_mu);
+    *hits = g_wm_hits; *misses = g_wm_misses;
+    g_wm_hits = g_wm_misses = 0;
+    pthread_mutex_unlock(&g_wm_mu);
+}
+
+/* bwt_cal_width on the GPU for n sequences of one type; w: 2 * (len + 1) words each */
+static void widths_gpu(hsa_index_t *ix, int type, int n, const uint64_t *offs, const uint32_t *lens,
+                       const uint8_t *codes, size_t codes_len, uint32_t *w)
+{
+    const int rc = type == 1 ? hsa_width_batch(ix, (size_t)n, offs, lens, codes, codes_len, w)
+                             : hsa_width0_batch(ix, (size_t)n, offs, lens, codes, codes_len, w);
+    if (rc) hsa_gpu_fatal("GPU bwt_cal_width", rc);
+}
+
+/* bwt_cal_width (bwtaln.c:73-116): from the table, or one GPU call. */
+int bwt_cal_width(const Idx2BWT *bi_bwt, int len, const ubyte_t *str, bwt_width_t *width, int type)
+{
+    if (len < 0) len = 0;
+    uint8_t stackbuf[1024];
+    uint8_t *key = (size_t)len + 5 <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc((size_t)len + 5);
+    const size_t kl = wkey(type == 1, len, str, key);
+    const uint64_t h = wfnv(key, kl);
+    int found = 0, ret = 0;
+    pthread_mutex_lock(&g_wm_mu);
+    if (g_wm_n)
+        for (size_t j = h & (g_wm_cap - 1); g_wm[j].h; j = (j + 1) & (g_wm_cap - 1))
+            if (g_wm[j].h == h && g_wm[j].key_len == kl && !memcmp(g_wm[j].key, key, kl)) {
+                const wm_ent_t *e = g_wm + j;
+                memcpy(width + (type == 1 ? 0 : 1), e->w + (type == 1 ? 0 : 1),
+                       sizeof(bwt_width_t) * (size_t)(type == 1 ? len + 1 : len));
+                ret = e->ret;
+                found = 1;
+                break;
+            }
+    if (found) ++g_wm_hits;
+    else if (g_wm_n) ++g_wm_misses;
+    pthread_mutex_unlock(&g_wm_mu);
+    if (key != stackbuf) free(key);
+    if (found) return ret;
+    uint64_t off = 0;
+    uint32_t l32 = (uint32_t)len;
+    uint32_t *w = (uint32_t *)calloc(2 * ((size_t)len + 1), sizeof(uint32_t));
+    widths_gpu(hsa_gpu_index_of(bi_bwt), type == 1, 1, &off, &l32, str, (size_t)len, w);
+    for (int i = type == 1 ? 0 : 1; i <= len; ++i) { width[i].w = w[2 * i]; width[i].bid = (int)w[2 * i + 1]; }
+    ret = (int)w[2 * len + 1];
+    free(w);
+    return ret;
+}
+
+extern __typeof__(bwt_cal_width) hsa_own_cal_width __attribute__((alias("bwt_cal_width"), visibility("hidden")));
+
+int hsa_splice_width_active(void)
+{
+    int (*volatile resolved)(const Idx2BWT *, int, const ubyte_t *, bwt_width_t *, int) = bwt_cal_width;
+    return resolved == hsa_own_cal_width;
+}
+
+/* The widths bwt_splice_match can ask for, per fallback read (aux[r] as it receives
+ * it) and strand s (seq_s: the read or its reverse complement, length L, seed length
+ * sl = L / 3): type 1 of the prefixes of length sl and sl + L % 3 (the seed calls,
+ * bwtgap.c:807), of the whole read and of its last 12 bases (:867/:871, :915), and type
+ * 0 of the whole read (:868/:872).  Two GPU launches; the answers go to the table. */
+int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
+{
+    if (n <= 0) return 0;
+    hsa_index_t *ix = hsa_gpu_index_of(bi);
+    for (int type = 1; type >= 0; --type) {
+        const int per = type == 1 ? 4 : 1;
+        size_t nc = 0, nrow = 0;
+        for (int r = 0; r < n; ++r) {
+            const int L = aux[r]->len;
+            nrow += 2 * (size_t)per;
+            nc += 2 * (type == 1 ? (size_t)(2 * (L / 3) + L % 3 + L + (L >= 12 ? 12 : 0)) : (size_t)L);
+        }
+        uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * nrow);
+        uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * nrow);
+        const ubyte_t **src = (const ubyte_t **)malloc(sizeof(ubyte_t *) * nrow);
+        uint8_t *codes = (uint8_t *)malloc(nc + 1);
+        size_t co = 0, wo = 0, q = 0;
+        for (int r = 0; r < n; ++r) {
+            const int L = aux[r]->len, sl = L / 3;
+            for (int s = 0; s < 2; ++s) {
+                const ubyte_t *sq = s ? aux[r]->rc_seq : aux[r]->seq;
+                int rl[4], nr = 0;
+                const ubyte_t *rs[4];
+                if (type == 1) {
+                    rl[nr] = sl; rs[nr++] = sq;
+                    rl[nr] = sl + L % 3; rs[nr++] = sq;
+                    rl[nr] = L; rs[nr++] = sq;
+                    if (L >= 12) { rl[nr] = 12; rs[nr++] = sq + L - 12; }
+                } else {
+                    rl[nr] = L; rs[nr++] = sq;
+                }
+                for (int k = 0; k < nr; ++k) {
+                    offs[q] = co; lens[q] = (uint32_t)rl[k]; src[q] = rs[k];
+                    memcpy(codes + co, rs[k], (size_t)rl[k]);
+                    co += (size_t)rl[k];
+                    wo += 2 * ((size_t)rl[k] + 1);
+                    ++q;
+                }
+            }
+        }
+        uint32_t *w = (uint32_t *)calloc(wo + 2, sizeof(uint32_t));
+        widths_gpu(ix, type, (int)q, offs, lens, codes, co, w);
+        pthread_mutex_lock(&g_wm_mu);
+        size_t o = 0;
+        for (size_t j = 0; j < q; ++j) {
+            wm_put(type, (int)lens[j], src[j], w + o, (int)w[o + 2 * lens[j] + 1]);
+            o += 2 * ((size_t)lens[j] + 1);
+        }
+        pthread_mutex_unlock(&g_wm_mu);
+        free(offs); free(lens); free(src); free(codes); free(w);
+    }
+    return 0;
+}
+
 /* gap_init_stack's layout (bwtgap.c:13-27): the host's splice code resets and reads it */
 static gap_stack_t *stack_new(int n_stacks)
 {
@@ -267,7 +465,9 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     }
     ext_req_t **pend = (ext_req_t **)malloc(sizeof(ext_req_t *) * (size_t)W);
     int next = 0, live = 0;
-    long launches = 0;
+    long launches = 0, calls = 0;
+    double t_gpu = 0.0;
+    const double t_run = hsa_now();
     for (int k = 0; k < W; ++k) { co_start(co + k, next, reads + next); ++next; ++live; }
     while (live > 0) {
         /* run every runnable coroutine until it parks or finishes; a finished one takes
@@ -290,7 +490,10 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         for (int k = 0; k < W; ++k)
             if (co[k].read >= 0 && co[k].state == 1) pend[np++] = &co[k].req;
         if (np == 0) continue;
+        const double tg = hsa_now();
         run_reqs(ix, pend, np);
+        t_gpu += hsa_now() - tg;
+        calls += np;
         ++launches;
         for (int k = 0; k < W; ++k)
             if (co[k].read >= 0 && co[k].state == 1) co[k].state = 0;
@@ -303,5 +506,9 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     }
     free(co); free(pend);
     tl_sched = NULL;
+    if (getenv("HSA_VERBOSE"))
+        fprintf(stderr, "[hsa] splice runner: %d reads, %ld extension calls in %ld launches: %.3f s in the launches "
+                        "(copies included), %.3f s of host splice code\n", n, calls, launches, t_gpu,
+                hsa_now() - t_run - t_gpu);
     return launches;
 }

@@ -25,6 +25,7 @@
 #include "hsa_internal.h"
 
 #define EXT_NT 64
+#define EXT_LDS_NB 128     // buckets per lane kept in LDS: 64 lanes x 128 x 8 B = 64 KiB
 #define EXT_NIL 0xFFFFFFFFu
 #define MODE_GAPE 0x01
 #define MODE_LOGGAP 0x04
@@ -52,6 +53,7 @@ struct ExtArgs {
     uint4 *pool;                 // per lane: cap entries x 2 uint4
     uint32_t *heads, *cnt;       // per lane: nb each
     uint32_t cap, nb;
+    uint32_t lds;                // bucket heads and counts in LDS (nb <= EXT_LDS_NB), else in heads/cnt
     int32_t *ret, *mp_out;
     uint32_t *aln_out;           // 9 words per job
 };
@@ -80,10 +82,16 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
     const hsa_ext_job_t J = a.jobs[jb];
     const hsa_regime_t R = a.regimes[J.regime];
     uint4 *const P = a.pool + (size_t)t * a.cap * 2;
-    uint32_t *const H = a.heads + (size_t)t * a.nb;
-    uint32_t *const N = a.cnt + (size_t)t * a.nb;
+    // bucket heads and counts (gap_stack_t's per-score stacks): lane-interleaved in LDS,
+    // or per lane in HBM when there are too many buckets
+    extern __shared__ uint32_t s_hn[];
+    uint32_t *const Hb = a.lds ? s_hn + threadIdx.x : a.heads + (size_t)t * a.nb;
+    uint32_t *const Nb = a.lds ? s_hn + (size_t)a.nb * EXT_NT + threadIdx.x : a.cnt + (size_t)t * a.nb;
+    const uint32_t hs = a.lds ? EXT_NT : 1u;
+#define H(b) Hb[(uint32_t)(b) * hs]
+#define N(b) Nb[(uint32_t)(b) * hs]
     const int nst = R.n_stacks;
-    for (int b = 0; b < nst; ++b) N[b] = 0;
+    for (int b = 0; b < nst; ++b) N(b) = 0;
     int best = nst, n_ent = 0, err = 0;
     uint32_t top = 0, freel = EXT_NIL;
     const int len = J.len, bw = J.dir;
@@ -98,25 +106,41 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
         if (p < lo || p >= hi) { err = EXT_E_WIN; return 0; }
         return bd[p - lo];
     };
+    // The entry pushed last stays in registers ("pending") until the next push or pop:
+    // the next pop takes it whenever its score is <= the lowest non-empty bucket (it is
+    // the top of that bucket then, bwtgap.c:77-92), so a chain of expansions whose last
+    // child (the match, pushed last, bwtgap.c:493-502) is always the best never touches
+    // the stack in HBM.
+    bool pend = false;
+    uint4 pe0 = make_uint4(0, 0, 0, 0), pe1 = make_uint4(0, 0, 0, 0);
+    int pscore = 0;
+    auto flush = [&]() {                               // the pending entry into its bucket
+        pend = false;
+        uint32_t slot;
+        if (freel != EXT_NIL) { slot = freel; freel = P[(size_t)slot * 2 + 1].z; }
+        else if (top < a.cap) slot = top++;
+        else { err = EXT_E_CAP; return; }
+        pe1.z = N(pscore) ? H(pscore) : EXT_NIL;
+        P[(size_t)slot * 2] = pe0;
+        P[(size_t)slot * 2 + 1] = pe1;
+        H(pscore) = slot;
+        ++N(pscore);
+        if (best > pscore) best = pscore;
+    };
     // gap_push (bwtgap.c:46-75): info = score << 21 | i in 32 bits; last_diff_pos is
     // never read by the extension
     auto push = [&](int i, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl, int mm, int go, int ge, int st) {
         const int score = mm * R.s_mm + go * R.s_gapo + ge * R.s_gape;
         if (score < 0 || score >= nst) { err = EXT_E_SCORE; return; }
-        uint32_t slot;
-        if (freel != EXT_NIL) { slot = freel; freel = P[(size_t)slot * 2 + 1].z; }
-        else if (top < a.cap) slot = top++;
-        else { err = EXT_E_CAP; return; }
-        const uint32_t nx = N[score] ? H[score] : EXT_NIL;
-        P[(size_t)slot * 2] = make_uint4(k, l, rk, rl);
-        P[(size_t)slot * 2 + 1] = make_uint4((uint32_t)score << 21 | (uint32_t)i,
-                                             (uint32_t)(mm & 255) | (uint32_t)(go & 255) << 8 |
-                                                 (uint32_t)(ge & 255) << 16 | (uint32_t)(st & 3) << 24,
-                                             nx, 0u);
-        H[score] = slot;
-        ++N[score];
+        if (pend) flush();
+        pe0 = make_uint4(k, l, rk, rl);
+        pe1 = make_uint4((uint32_t)score << 21 | (uint32_t)i,
+                         (uint32_t)(mm & 255) | (uint32_t)(go & 255) << 8 | (uint32_t)(ge & 255) << 16 |
+                             (uint32_t)(st & 3) << 24,
+                         0u, 0u);
+        pscore = score;
+        pend = true;
         ++n_ent;
-        if (best > score) best = score;
     };
     // one bidirectional step, all four characters: backward on the forward BWT, or
     // forward on the reverse BWT with the forward C table
@@ -156,19 +180,27 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
     while (n_ent != 0 && !err) {
         if (n_ent > R.max_entries) break;
         // gap_pop (bwtgap.c:77-92)
-        const uint32_t slot = H[best];
-        const uint4 e0 = P[(size_t)slot * 2], e1 = P[(size_t)slot * 2 + 1];
-        H[best] = e1.z;
-        --N[best];
-        --n_ent;
-        P[(size_t)slot * 2 + 1].z = freel;
-        freel = slot;
-        if (N[best] == 0 && n_ent) {
-            int b = best + 1;
-            while (b < nst && N[b] == 0) ++b;
-            best = b;
-        } else if (n_ent == 0) {
-            best = nst;
+        uint4 e0, e1;
+        if (pend && pscore <= best) {
+            e0 = pe0; e1 = pe1;
+            pend = false;
+            --n_ent;
+        } else {
+            if (pend) { flush(); if (err) break; }
+            const uint32_t slot = H(best);
+            e0 = P[(size_t)slot * 2]; e1 = P[(size_t)slot * 2 + 1];
+            H(best) = e1.z;
+            --N(best);
+            --n_ent;
+            P[(size_t)slot * 2 + 1].z = freel;
+            freel = slot;
+            if (N(best) == 0 && n_ent > (pend ? 1 : 0)) {
+                int b = best + 1;
+                while (b < nst && N(b) == 0) ++b;
+                best = b;
+            } else if (N(best) == 0) {
+                best = nst;
+            }
         }
         uint32_t k = e0.x, l = e0.y, rk = e0.z, rl = e0.w;
         const uint32_t info = e1.x;
@@ -272,6 +304,8 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
     a.mp_out[jb] = max_pos;
 #pragma unroll
     for (int w = 0; w < 9; ++w) a.aln_out[(size_t)jb * 9 + w] = aln[w];
+#undef H
+#undef N
 }
 
 // Device scratch of one pass: lanes x (cap entries x 32 B + nb x 8 B).
@@ -365,7 +399,9 @@ extern "C" int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, in
             A.cap = cap;
             A.job_list = (const int32_t *)(din + o_list) + c0;
             A.n = (int)m;
-            hipLaunchKernelGGL(k_extend, dim3((unsigned)((m + EXT_NT - 1) / EXT_NT)), dim3(EXT_NT), 0, ix->stream, A);
+            A.lds = nb <= EXT_LDS_NB;
+            const size_t shm = A.lds ? (size_t)nb * EXT_NT * 8 : 0;
+            hipLaunchKernelGGL(k_extend, dim3((unsigned)((m + EXT_NT - 1) / EXT_NT)), dim3(EXT_NT), shm, ix->stream, A);
             HSA_HIP(hipGetLastError());
         }
         HSA_HIP(hipMemcpyAsync(ret, dout, (size_t)n * 4, hipMemcpyDeviceToHost, ix->stream));

@@ -472,8 +472,39 @@ __global__ void k_width(RankDir rev, uint32_t T, const uint32_t *C, const uint64
     o[2 * len + 1] = (uint32_t)(bid + 1);
 }
 
-extern "C" int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
-                               const uint8_t *codes, size_t codes_len, uint32_t *width_out)
+// bwt_cal_width type 0 (bwtaln.c:98-115): backward on the forward BWT
+// (BWTSARangeBackward, 2BWT-Interface.c:107-118) from the read's end; entries
+// [1, len) and [len] = {0, ++bid} are written, entry 0 never is (the reference's loop
+// stops at i > 0): it is left 0 here, and callers copy entries 1..len only.
+__global__ void k_width0(RankDir fwd, uint32_t T, const uint32_t *C, const uint64_t *offs, const uint32_t *lens,
+                         const uint64_t *woff, const uint8_t *codes, size_t n, uint32_t *w)
+{
+    size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint8_t *s = codes + offs[r];
+    const uint32_t len = lens[r];
+    uint32_t k = 0, l = T;
+    int bid = 0;
+    uint32_t *o = w + woff[r];
+    o[0] = 0; o[1] = 0;
+    for (uint32_t i = len - 1; i > 0 && len > 0; --i) {
+        const uint8_t c = s[i];
+        if (c < 4) {
+            uint32_t a, b;
+            hsa_occ1_pair(fwd, k, l + 1, c, a, b);
+            k = C[c] + a + 1;
+            l = C[c] + b;
+        }
+        if (k > l || c > 3) { k = 0; l = T; ++bid; }
+        o[2 * i] = l - k + 1;
+        o[2 * i + 1] = (uint32_t)bid;
+    }
+    o[2 * len] = 0;
+    o[2 * len + 1] = (uint32_t)(bid + 1);
+}
+
+static int width_batch(hsa_index_t *ix, int type, size_t n, const uint64_t *offs, const uint32_t *lens,
+                       const uint8_t *codes, size_t codes_len, uint32_t *width_out)
 {
     if (int rc0 = hsa_need32(ix)) return rc0;
     HSA_HIP(hipSetDevice(ix->device));
@@ -498,13 +529,28 @@ extern "C" int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, 
     HSA_HIP(hipMemcpyAsync(d_lens, lens, n * 4, hipMemcpyHostToDevice, ix->stream));
     HSA_HIP(hipMemcpyAsync(d_C, ix->C, 20, hipMemcpyHostToDevice, ix->stream));
     HSA_HIP(hipMemcpyAsync(d_codes, codes, codes_len, hipMemcpyHostToDevice, ix->stream));
-    RankDir rev{ix->blk[1], ix->risa0};
-    if (n) k_width<<<(unsigned)((n + 63) / 64), 64, 0, ix->stream>>>(rev, ix->T, d_C, d_offs, d_lens, d_woff, d_codes, n, (uint32_t *)ix->d_out);
+    RankDir rev{ix->blk[1], ix->risa0}, fwd{ix->blk[0], ix->isa0};
+    if (n && type == 1)
+        k_width<<<(unsigned)((n + 63) / 64), 64, 0, ix->stream>>>(rev, ix->T, d_C, d_offs, d_lens, d_woff, d_codes, n, (uint32_t *)ix->d_out);
+    else if (n)
+        k_width0<<<(unsigned)((n + 63) / 64), 64, 0, ix->stream>>>(fwd, ix->T, d_C, d_offs, d_lens, d_woff, d_codes, n, (uint32_t *)ix->d_out);
     HSA_HIP(hipGetLastError());
     HSA_HIP(hipMemcpyAsync(width_out, ix->d_out, tot * 4, hipMemcpyDeviceToHost, ix->stream));
     HSA_HIP(hipStreamSynchronize(ix->stream));
     free(woff);
     return 0;
+}
+
+extern "C" int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
+                               const uint8_t *codes, size_t codes_len, uint32_t *width_out)
+{
+    return width_batch(ix, 1, n, offs, lens, codes, codes_len, width_out);
+}
+
+extern "C" int hsa_width0_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
+                                const uint8_t *codes, size_t codes_len, uint32_t *width_out)
+{
+    return width_batch(ix, 0, n, offs, lens, codes, codes_len, width_out);
 }
 
 // ---------------------------------------------------------------- synthetic genome

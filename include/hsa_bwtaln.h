@@ -170,6 +170,16 @@ bwt_aln1_t *bwt_match_gap(bwt_aux_t *aux, int *_n_aln);
 int  bwt_match_gap_batch(bwt_aux_t *const *aux, int n, bwt_aln1_t **out, int *n_out);
 int  hsa_gpu_attach(const Idx2BWT *bi_bwt);
 void hsa_gpu_detach(const Idx2BWT *bi_bwt);
+/* bwt_extend_backward / bwt_extend_foreward: replace bwtgap.c:640 / :654 (declared
+ * bwtgap.h; -> bwt_backtracing_search :346-511).  Same effects on *aln and the bound.
+ * Called from the drop-in bwa_cal_sa_reg_gap's splice runner, a batch's calls run as
+ * GPU batches (hsa_extend_batch); called elsewhere, one GPU call each. */
+int  bwt_extend_backward(bwt_aux_t *aux, bwt_aln1_t *aln, int *_left);
+int  bwt_extend_foreward(bwt_aux_t *aux, bwt_aln1_t *aln, int *_right);
+/* bwt_cal_width: replaces bwtaln.c:73 (declared bwtaln.h).  Writes the entries the
+ * reference writes (type 1: 0..len, type 0: 1..len) and returns its value; the splice
+ * path's calls are answered from a table filled on the GPU per batch. */
+int  bwt_cal_width(const Idx2BWT *bi_bwt, int len, const ubyte_t *str, bwt_width_t *width, int type);
 /* Device slots: each bwa_cal_sa_reg_gap call splits its reads into n contiguous parts,
  * searched concurrently on slots 0..n-1 (slot k on device k % hsa_device_count(), one
  * host thread and one uploaded index per slot; several slots may share a device).

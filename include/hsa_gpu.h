@@ -11,7 +11,7 @@
  *                         rank blocks (3 x u32 counts + 16 two-bit codes).
  *   hsa_occ4_batch     -- BWTAllOccValue (BWT.c:793) for a batch of positions.
  *   hsa_step_batch     -- BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235).
- *   hsa_width_batch    -- bwt_cal_width type 1 (bwtaln.c:73-98).
+ *   hsa_width_batch    -- bwt_cal_width type 1 (bwtaln.c:73-98); hsa_width0_batch: type 0.
  *   hsa_search_batch   -- the per-read loop of bwa_cal_sa_reg_gap (bwtaln.c:303-373):
  *                         rc strand then forward strand, bwt_cal_width x2 and
  *                         bwt_match_gap (bwtgap.c:118-331) per strand (two kernels:
@@ -95,6 +95,10 @@ int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t *pos, uint
 int hsa_step_batch(hsa_index_t *ix, size_t n, const uint32_t *klrr, uint32_t *out16);
 int hsa_width_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
                     const uint8_t *codes, size_t codes_len, uint32_t *width_out /* 2*(len+1) words per read, packed */);
+/* bwt_cal_width type 0 (bwtaln.c:98-115, backward on the forward BWT): entries 1..len
+ * as the reference writes them; entry 0, which the reference never writes, is 0. */
+int hsa_width0_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens,
+                     const uint8_t *codes, size_t codes_len, uint32_t *width_out);
 
 /* One seed extension of the splice path: bwt_extend_backward (dir 1) or
  * bwt_extend_foreward (dir 0), bwtgap.c:640-663 -> bwt_backtracing_search (:346-511).

@@ -288,6 +288,33 @@ int OR(cal_width)(const or_index_t *ix, int len, const uint8_t *str, bw_t *width
     return cal_width((or_index_t *)ix, len, str, width);
 }
 
+/* bwt_cal_width, type 0 (bwtaln.c:98-115): backward extension on the FORWARD BWT
+ * (BWTSARangeBackward, 2BWT-Interface.c:107-118) from the end of str; entry 0 is never
+ * written (the loop stops at i > 0). */
+int OR(cal_width0)(const or_index_t *cix, int len, const uint8_t *str, bw_t *w)
+{
+    const or_index_t *ix = cix;
+    bw_t k = 0, l = ix->f.T;
+    int bid = 0;
+    for (int i = len - 1; i > 0; --i) {
+        uint8_t c = str[i];
+        if (c < 4) {
+            bw_t a[4], b[4];
+            occ4(&ix->f, k, a);
+            occ4(&ix->f, l + 1, b);
+            tl_queries += 2;
+            k = ix->f.C[c] + a[c] + 1;
+            l = ix->f.C[c] + b[c];
+        }
+        if (k > l || c > 3) { k = 0; l = ix->f.T; ++bid; }
+        w[2 * i] = l - k + 1;
+        w[2 * i + 1] = (bw_t)bid;
+    }
+    w[2 * len] = 0;
+    w[2 * len + 1] = (bw_t)++bid;
+    return bid;
+}
+
 void OR(init_opt)(or_opt_t *o)
 {
     memset(o, 0, sizeof *o);

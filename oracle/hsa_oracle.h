@@ -44,6 +44,8 @@ void or_step_all(const or_index_t *ix, uint32_t k, uint32_t l, uint32_t rk, uint
                  uint32_t ok[4], uint32_t ol[4], uint32_t ork[4], uint32_t orl[4]);
 /* bwt_cal_width type 1 (bwtaln.c:73-98); width is 2*(len+1) words {w, bid}. */
 int or_cal_width(const or_index_t *ix, int len, const uint8_t *str, uint32_t *width);
+/* bwt_cal_width type 0 (bwtaln.c:98-115): entries 1..len written, entry 0 untouched. */
+int or_cal_width0(const or_index_t *ix, int len, const uint8_t *str, uint32_t *width);
 
 /* BWTSaValue (BWT.c:1195) on the forward BWT; sa_values as BWTLoad holds them
  * (values[0] = -1). */
@@ -93,6 +95,7 @@ void or64_occ4(const or_index_t *ix, int dir, uint64_t i, uint64_t occ[4]);
 void or64_step_all(const or_index_t *ix, uint64_t k, uint64_t l, uint64_t rk, uint64_t rl,
                    uint64_t ok[4], uint64_t ol[4], uint64_t ork[4], uint64_t orl[4]);
 int or64_cal_width(const or_index_t *ix, int len, const uint8_t *str, uint64_t *width);
+int or64_cal_width0(const or_index_t *ix, int len, const uint8_t *str, uint64_t *width);
 void or64_init_opt(or_opt_t *o);
 int or64_cal_maxdiff(int l, double err, double thres);
 long or64_cal_sa_reg_gap(const or_index_t *ix, int n, const uint32_t *lens, const uint8_t *codes,

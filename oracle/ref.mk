@@ -99,18 +99,22 @@ $(OUT)/HSA_gpu_mg: $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPULIB)
 # (as HSA_gpu_mg), the splice path's seed extensions bwt_extend_backward /
 # bwt_extend_foreward (weakened in bwtgap.o too: hsa_amd/csrc/bwtext_gpu.c runs the
 # splice path of a batch's fallback reads as coroutines and their extensions as GPU
-# batches), and the SAM stage's bwa_cal_pac_pos, weakened in bwtse.o, so that
+# batches), bwt_cal_width (weakened in bwtaln.o: the splice path's widths from a table
+# filled on the GPU, bwtext_gpu.c), and the SAM stage's bwa_cal_pac_pos, weakened in bwtse.o, so that
 # generate_sam_se_core (bwtse.c:911) calls OUR bwa_cal_pac_pos (hsa_amd/csrc/bwtse_gpu.c:
 # the batch's SA -> position lookups on the GPU).
 $(OUT)/obj/bwtse_weak.o: $(OUT)/obj/bwtse.o
 	objcopy --weaken-symbol=bwa_cal_pac_pos $< $@
+
+$(OUT)/obj/bwtaln_weak_all.o: $(OUT)/obj/bwtaln.o
+	objcopy --weaken-symbol=bwa_cal_sa_reg_gap --weaken-symbol=bwt_cal_width $< $@
 
 $(OUT)/obj/bwtgap_weak_all.o: $(OUT)/obj/bwtgap.o
 	objcopy --weaken-symbol=bwt_match_gap --weaken-symbol=bwt_extend_foreward \
 	        --weaken-symbol=bwt_extend_backward $< $@
 
 ALLOBJS   = $(filter-out $(OUT)/obj/bwtaln.o $(OUT)/obj/bwtgap.o $(OUT)/obj/bwtse.o,$(OBJS)) \
-            $(OUT)/obj/bwtaln_weak.o $(OUT)/obj/bwtgap_weak_all.o $(OUT)/obj/bwtse_weak.o
+            $(OUT)/obj/bwtaln_weak_all.o $(OUT)/obj/bwtgap_weak_all.o $(OUT)/obj/bwtse_weak.o
 GPUOBJ_SA = $(CURDIR)/../hsa_amd/csrc/bwtse_gpu.o
 GPUOBJ_EX = $(CURDIR)/../hsa_amd/csrc/bwtext_gpu.o
 

@@ -17,6 +17,8 @@
  *       BWTAllSARangesBackward_Bidirection (2BWT-Interface.c:235) on (k,l,rk,rl).
  *   ref_probe width <prefix> <reads.bin> <out.bin>
  *       bwt_cal_width(type=1) (bwtaln.c:73) of every read: (len+1) x {u32 w, i32 bid}.
+ *   ref_probe width <prefix> <reads.bin> <out.bin> 0
+ *       the same with type 0 (backward; entry 0 is never written: stays 0 from calloc).
  *   ref_probe sa    <prefix> <idx.bin> <out.bin>
  *       BWTSaValue (BWT.c:1195) and BWTRetrievePositionFromSAIndex
  *       (2BWT-Interface.c:329) of each SA index: u32 sa, i32 seqId, u32 ori_pos,
@@ -191,7 +193,7 @@ static int cmd_width(int argc, char **argv)
     FILE *out = fopen(argv[3], "wb");
     for (uint32_t i = 0; i < r.n; ++i) {
         bwt_width_t *w = (bwt_width_t *)calloc(r.len[i] + 1, sizeof(bwt_width_t));
-        bwt_cal_width(bi, (int)r.len[i], r.seq[i], w, 1);
+        bwt_cal_width(bi, (int)r.len[i], r.seq[i], w, argc > 4 ? atoi(argv[4]) : 1);
         fwrite(w, sizeof(bwt_width_t), r.len[i] + 1, out);
         free(w);
     }

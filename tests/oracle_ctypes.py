@@ -50,6 +50,7 @@ def lib():
         L.or_occ4.argtypes = [C.c_void_p, C.c_int, C.c_uint32, u32p]
         L.or_step_all.argtypes = [C.c_void_p] + [C.c_uint32] * 4 + [u32p] * 4
         L.or_cal_width.argtypes = [C.c_void_p, C.c_int, np.ctypeslib.ndpointer(np.uint8, flags="C"), u32p]
+        L.or_cal_width0.argtypes = [C.c_void_p, C.c_int, np.ctypeslib.ndpointer(np.uint8, flags="C"), u32p]
         L.or_init_opt.argtypes = [C.POINTER(Opt)]
         L.or_cal_maxdiff.argtypes = [C.c_int, C.c_double, C.c_double]
         L.or_cal_sa_reg_gap.restype = C.c_long
@@ -158,6 +159,13 @@ class OracleIndex:
         seq = np.ascontiguousarray(seq, np.uint8)
         w = np.zeros(2 * (len(seq) + 1), np.uint32)
         lib().or_cal_width(self.h, len(seq), seq, w)
+        return w.reshape(-1, 2)
+
+    def cal_width0(self, seq):
+        """bwt_cal_width type 0; entry 0 (never written by the reference) is 0."""
+        seq = np.ascontiguousarray(seq, np.uint8)
+        w = np.zeros(2 * (len(seq) + 1), np.uint32)
+        lib().or_cal_width0(self.h, len(seq), seq, w)
         return w.reshape(-1, 2)
 
     def match_gap(self, opt: Opt, n_stacks, seq, strand, width, seed, width_seed=None):

@@ -175,3 +175,16 @@ int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes
     }
     return 0;
 }
+
+int hsa_width0_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint32_t *lens, const uint8_t *codes,
+                     size_t codes_len, uint32_t *width_out)
+{
+    (void)codes_len;
+    size_t o = 0;
+    for (size_t i = 0; i < n; ++i) {
+        width_out[o] = width_out[o + 1] = 0;
+        or_cal_width0((const or_index_t *)ix, (int)lens[i], codes + offs[i], width_out + o);
+        o += 2 * ((size_t)lens[i] + 1);
+    }
+    return 0;
+}

@@ -32,19 +32,21 @@ OBJ = os.path.join(ROOT, "oracle", "_ref", "obj")
 MAN = json.load(open(os.path.join(GOLD, "manifest_dropin.json")))
 COMMON = ["BWT", "BWTConstruct", "utils", "dictionary", "DNACount", "HSP", "iniparser", "inistrlib", "MemManager",
           "MiscUtilities", "QSufSort", "2BWT-Builder", "TextConverter", "Timing", "bamlite", "2BWT-Interface",
-          "bwaseqio", "r250", "cs2nt", "bwtse", "kstring", "stdaln", "bwt_array", "bwtaln_weak", "main"]
+          "bwaseqio", "r250", "cs2nt", "bwtse", "kstring", "stdaln", "bwt_array", "main"]
 # "mg": bwt_match_gap replaced (seeds and anchors from the prefetch table); "all": the
 # seed extensions too (bwtext_gpu.c: the splice path of the batch's fallback reads as
 # coroutines, their extensions batched)
-VARIANTS = {"mg": (COMMON + ["bwtgap_weak"], ["hsa_amd/csrc/bwtaln_gpu.c", "hsa_amd/csrc/bwtgap_gpu.c"]),
-            "all": (COMMON + ["bwtgap_weak_all"], ["hsa_amd/csrc/bwtaln_gpu.c", "hsa_amd/csrc/bwtgap_gpu.c",
+VARIANTS = {"mg": (COMMON + ["bwtaln_weak", "bwtgap_weak"], ["hsa_amd/csrc/bwtaln_gpu.c",
+                                                                "hsa_amd/csrc/bwtgap_gpu.c"]),
+            "all": (COMMON + ["bwtaln_weak_all", "bwtgap_weak_all"], ["hsa_amd/csrc/bwtaln_gpu.c", "hsa_amd/csrc/bwtgap_gpu.c",
                                                    "hsa_amd/csrc/bwtext_gpu.c"])}
 CORE = ["tests/san/san_core.c", "oracle/hsa_oracle.c"]
 FLAGS = ["-O1", "-g", "-std=gnu11", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
          "-fno-omit-frame-pointer"]
 
 needs_ref = pytest.mark.skipif(not all(os.path.exists(os.path.join(OBJ, o + ".o"))
-                                   for o in COMMON + ["bwtgap_weak", "bwtgap_weak_all"]) or not shutil.which("gcc"),
+                                   for o in COMMON + ["bwtaln_weak", "bwtgap_weak", "bwtaln_weak_all", "bwtgap_weak_all"])
+                               or not shutil.which("gcc"),
                                reason="reference objects not built here (make -C oracle)")
 _BINS = {}
 
@@ -98,3 +100,7 @@ def test_reference_hsa_with_dropin_host_c_prints_reference_sam(tmp_path_factory,
         if variant == "all":   # the extensions ran batched, from the coroutine runner
             m = re.findall(r"splice path: (\d+) reads as coroutines, seed extensions in (\d+) GPU launches", err)
             assert m and sum(int(a) for a, _ in m) > 0, err[-2000:]
+            # ... and every width the splice path computed came from the batched table
+            w = [(int(a), int(b)) for a, b in
+                 re.findall(r"splice widths: (\d+) bwt_cal_width calls answered from the batch, (\d+) run alone", err)]
+            assert w and sum(a for a, _ in w) > 0 and sum(b for _, b in w) == 0, w

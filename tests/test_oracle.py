@@ -206,3 +206,18 @@ def test_extension_matches_reference(name):
             bad += 1
     assert n > 3000
     assert bad == 0, f"{bad} of {n} extensions differ"
+
+
+def test_width_type0_matches_reference():
+    """bwt_cal_width type 0 (the splice path's width_fore, bwtgap.c:868/:872) against the
+    compiled reference's (tests/golden/tiny_width0.npz)."""
+    fwd, rev = index_io.read_index(INDEX["tiny"])
+    ox = OracleIndex(fwd, rev)
+    g = np.load(f"{GOLD}/tiny_width0.npz")
+    o = 0
+    exp = g["width"]
+    for L, off in zip(g["lens"].astype(int), np.concatenate([[0], np.cumsum(g["lens"].astype(int))[:-1]])):
+        off = int(off)
+        got = ox.cal_width0(g["codes"][off:off + L])
+        assert np.array_equal(got, exp[o:o + L + 1]), off
+        o += L + 1

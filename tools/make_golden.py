@@ -480,6 +480,23 @@ def mgcap_cases(work):
               f"{changed} with widths changed by gap_shadow")
 
 
+def width0_cases(work):
+    """bwt_cal_width type 0 (bwtaln.c:98-115; the splice path's width_fore, bwtgap.c:868,
+    :872) of the width reads and of the splice read set, on the tiny index."""
+    T, seed, nrec = 200003, 7, 3
+    g = synth.genome_codes(T, seed)
+    rec = synth.record_layout(T, nrec)
+    seqs = edge_reads(g, rec, 21)[:24] + splice_reads()[:200]
+    rb = os.path.join(work, "w0.bin")
+    synth.write_reads_bin(rb, seqs)
+    prefix = os.path.join(GOLD, "index", "tiny.fa")
+    sh(os.path.join(REF, "ref_probe"), "width", prefix, rb, os.path.join(work, "w0out.bin"), "0")
+    w = np.fromfile(os.path.join(work, "w0out.bin"), dtype=np.uint32).reshape(-1, 2)
+    lens, codes = pack_reads(seqs)
+    np.savez_compressed(os.path.join(GOLD, "tiny_width0.npz"), lens=lens, codes=codes, width=w)
+    print(f"tiny_width0: {len(seqs)} reads")
+
+
 def read_extcap(path):
     """Records of oracle/ref_extcap.c: every seed extension of a reference run."""
     raw = open(path, "rb").read()
@@ -537,6 +554,7 @@ def main():
     ap.add_argument("--sa", action="store_true")
     ap.add_argument("--mgcap", action="store_true")
     ap.add_argument("--extcap", action="store_true")
+    ap.add_argument("--width0", action="store_true")
     a = ap.parse_args()
     if not os.path.exists(os.path.join(REF, "ref_probe")):
         sys.exit("build oracle/_ref first: make -C oracle -f ref.mk")
@@ -552,6 +570,8 @@ def main():
             mgcap_cases(work)
         elif a.extcap:
             extcap_cases(work)
+        elif a.width0:
+            width0_cases(work)
         else:
             tiny_cases(work)
 

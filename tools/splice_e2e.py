@@ -43,7 +43,7 @@ def run(binary, args, prefix, fq, out, env=None, timeout=1800):
         raise SystemExit(f"{binary} printed no SAM lines:\n{err[-2000:]}")
     return {"wall_s": round(wall, 3), "sam_lines": lines, "search_cpu_s": round(sum(secs[0::2]), 3),
             "sam_cpu_s": round(sum(secs[1::2]), 3), "sha256": digest,
-            "log": [l for l in err.splitlines() if l.startswith("[hsa]")][-4:]}
+            "log": [l for l in err.splitlines() if l.startswith("[hsa]") and "launch:" not in l][-6:]}
 
 
 def main():
