@@ -30,6 +30,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_cal_sa_reg_gap_multi", "hsa_index_create_device64", "hsa_index_is64", "hsa_occ4_batch64",
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
+    "hsa_width0_batch", "bwt_cal_width",
 ]
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
@@ -171,6 +172,8 @@ def lib():
     L.hsa_occ4_batch.argtypes = [vp, C.c_int, C.c_size_t, u32, u32]
     L.hsa_step_batch.argtypes = [vp, C.c_size_t, u32, u32]
     L.hsa_width_batch.argtypes = [vp, C.c_size_t, u64, u32, u8, C.c_size_t, u32]
+    if hasattr(L, "hsa_width0_batch"):
+        L.hsa_width0_batch.argtypes = [vp, C.c_size_t, u64, u32, u8, C.c_size_t, u32]
     L.hsa_search_batch.restype = C.c_long
     L.hsa_search_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, C.c_int, u8, C.c_size_t, i32, u32, u64,
                                    C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(Stats)]
@@ -359,13 +362,16 @@ class GpuIndex:
         check(lib().hsa_step_batch(self.h, len(klrr), klrr, out))
         return out.reshape(-1, 4, 4)   # [n][k, l, rk, rl][c]
 
-    def widths(self, lens, codes):
+    def widths(self, lens, codes, type=1):
+        """bwt_cal_width of each sequence (type 1: hsa_width_batch, 0: hsa_width0_batch):
+        2 * (len + 1) words each, packed."""
         lens = np.ascontiguousarray(lens, np.uint32)
         offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
         tot = int(np.sum(2 * (lens.astype(np.int64) + 1)))
         out = np.zeros(tot, np.uint32)
         codes = np.ascontiguousarray(codes, np.uint8)
-        check(lib().hsa_width_batch(self.h, len(lens), offs, lens, codes, len(codes), out))
+        fn = lib().hsa_width_batch if type == 1 else lib().hsa_width0_batch
+        check(fn(self.h, len(lens), offs, lens, codes, len(codes), out))
         return out
 
     def search(self, regimes, jobs, codes):

@@ -44,6 +44,14 @@ def test_width_matches_reference():
     assert np.array_equal(ix.widths(g["lens"], g["codes"]), g["width"].reshape(-1))
 
 
+def test_width_type0_matches_reference():
+    """bwt_cal_width type 0 (the splice path's width_fore) on the GPU vs the compiled
+    reference's values; entry 0, which the reference never writes, is 0 on both."""
+    g = np.load(f"{GOLD}/tiny_width0.npz")
+    ix = gpu_index("tiny")
+    assert np.array_equal(ix.widths(g["lens"], g["codes"], type=0), g["width"].reshape(-1))
+
+
 def test_step_matches_oracle():
     from oracle_ctypes import OracleIndex
     fwd, rev = index_io.read_index(INDEX["tiny"])
