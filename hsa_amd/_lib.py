@@ -30,7 +30,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_cal_sa_reg_gap_multi", "hsa_index_create_device64", "hsa_index_is64", "hsa_occ4_batch64",
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
-    "hsa_width0_batch", "bwt_cal_width",
+    "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced",
 ]
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
@@ -202,6 +202,9 @@ def lib():
     if hasattr(L, "hsa_extend_batch"):
         L.hsa_extend_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, C.c_int, u8, i32, C.c_size_t, i32, i32,
                                        u32]
+    if hasattr(L, "hsa_extend_sliced"):
+        L.hsa_extend_sliced.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, i32, u8, C.c_int, u8, i32, C.c_size_t,
+                                        C.c_int, C.c_uint32, i32, i32, u32]
     f32 = np.ctypeslib.ndpointer(np.float32, flags="C")
     L.hsa_pass_times.argtypes = [vp, C.c_int, f32, f32]
     if hasattr(L, "hsa_cal_sa_reg_gap_multi"):      # (older A/B builds lack it)
@@ -402,6 +405,22 @@ class GpuIndex:
         check(lib().hsa_extend_batch(self.h, rg, len(regimes), np.ascontiguousarray(jobs).ctypes.data, n,
                                      codes if len(codes) else np.zeros(1, np.uint8),
                                      bids if len(bids) else np.zeros(1, np.int32), len(codes), ret, mp, aln))
+        return ret, mp, aln
+
+    def extend_sliced(self, regimes, jobs, codes, bids, slots, resume, n_slots, budget):
+        """One hsa_extend_sliced launch: returns (ret, max_pos, aln (n, 9))."""
+        n = len(jobs)
+        rg = (Regime * len(regimes))(*regimes)
+        ret = np.zeros(n, np.int32)
+        mp = np.zeros(n, np.int32)
+        aln = np.zeros((n, 9), np.uint32)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        bids = np.ascontiguousarray(bids, np.int32)
+        check(lib().hsa_extend_sliced(self.h, rg, len(regimes), np.ascontiguousarray(jobs).ctypes.data,
+                                      np.ascontiguousarray(slots, np.int32), np.ascontiguousarray(resume, np.uint8), n,
+                                      codes if len(codes) else np.zeros(1, np.uint8),
+                                      bids if len(bids) else np.zeros(1, np.int32), len(codes), int(n_slots),
+                                      int(budget), ret, mp, aln))
         return ret, mp, aln
 
     def match_gap(self, regimes, jobs, mg, codes, widths):

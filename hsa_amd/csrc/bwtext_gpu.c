@@ -37,6 +37,7 @@
 
 #define CO_STACK (512u << 10)     /* C stack per coroutine (the host's splice code + ours) */
 #define CO_MAX 4096               /* coroutines alive at once */
+#define SLICE_POPS 256u           /* pops per call per launch (hsa_extend_sliced) */
 
 /* One parked extension call. */
 typedef struct {
@@ -48,6 +49,7 @@ typedef struct {
     bwt_aln1_t *aln;              /* the caller's, updated on resume */
     int *max_pos_io;
     int ret;
+    int started;                  /* sliced: submitted before, its state is in its slot */
 } ext_req_t;
 
 typedef struct {
@@ -157,11 +159,69 @@ static void run_reqs(hsa_index_t *ix, ext_req_t *const *q, int n)
     free(rg); free(jobs); free(codes); free(bids); free(ret); free(mp); free(aln);
 }
 
+/* One sliced launch over the parked calls q[0..n) (slot[j]: the call's persistent slot):
+ * each runs for at most SLICE_POPS pops.  Returns the number finished; a finished call
+ * has its result applied and q[j]->started reset, an unfinished one stays parked. */
+static int run_slices(hsa_index_t *ix, ext_req_t *const *q, const int32_t *slot, int n, int n_slots, uint8_t *done)
+{
+    hsa_regime_t *rg = (hsa_regime_t *)calloc((size_t)n, sizeof(hsa_regime_t));
+    hsa_ext_job_t *jobs = (hsa_ext_job_t *)calloc((size_t)n, sizeof(hsa_ext_job_t));
+    uint8_t *res = (uint8_t *)calloc((size_t)n, 1);
+    size_t tot = 0;
+    for (int j = 0; j < n; ++j) tot += (size_t)q[j]->n;
+    uint8_t *codes = (uint8_t *)calloc(tot + 1, 1);
+    int32_t *bids = (int32_t *)calloc(tot + 1, sizeof(int32_t));
+    int nr = 0;
+    size_t off = 0;
+    for (int j = 0; j < n; ++j) {
+        int r = 0;
+        while (r < nr && memcmp(&rg[r], &q[j]->rg, sizeof(hsa_regime_t))) ++r;
+        if (r == nr) rg[nr++] = q[j]->rg;
+        hsa_ext_job_t *J = jobs + j;
+        J->dir = q[j]->dir; J->len = q[j]->len; J->max_pos = q[j]->max_pos; J->regime = r;
+        J->lo = q[j]->lo; J->n = q[j]->n; J->off = off;
+        memcpy(J->aln, q[j]->aln, sizeof(bwt_aln1_t));     /* the caller's hit, unchanged until done */
+        memcpy(codes + off, q[j]->seq, (size_t)q[j]->n);
+        memcpy(bids + off, q[j]->bid, sizeof(int32_t) * (size_t)q[j]->n);
+        off += (size_t)q[j]->n;
+        res[j] = (uint8_t)q[j]->started;
+    }
+    int32_t *ret = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    int32_t *mp = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    uint32_t *aln = (uint32_t *)malloc(sizeof(bwt_aln1_t) * (size_t)n);
+    int rc = hsa_extend_sliced(ix, rg, nr, jobs, slot, res, n, codes, bids, tot, n_slots, SLICE_POPS, ret, mp, aln);
+    if (rc) hsa_gpu_fatal("GPU seed extension", rc);
+    int nd = 0;
+    for (int j = 0; j < n; ++j) {
+        done[j] = 0;
+        if (ret[j] == HSA_EXT_CONT) { q[j]->started = 1; continue; }
+        if (ret[j] == HSA_EXT_E_CAP) {                 /* more stack than a slot holds: alone */
+            q[j]->started = 0;
+            ext_req_t *one = q[j];
+            run_reqs(ix, &one, 1);
+        } else if (ret[j] < -1) {
+            hsa_gpu_fatal("GPU seed extension (undefined in the reference)", ret[j]);
+        } else {
+            memcpy(q[j]->aln, aln + 9 * (size_t)j, sizeof(bwt_aln1_t));
+            *q[j]->max_pos_io = mp[j];
+            q[j]->ret = ret[j];
+            free(q[j]->seq); free(q[j]->bid);
+            q[j]->seq = NULL; q[j]->bid = NULL;
+        }
+        q[j]->started = 0;
+        done[j] = 1;
+        ++nd;
+    }
+    free(rg); free(jobs); free(res); free(codes); free(bids); free(ret); free(mp); free(aln);
+    return nd;
+}
+
 static int extend(bwt_aux_t *aux, bwt_aln1_t *aln, int *max_pos, int dir)
 {
     co_t *me = tl_co;
     if (me) {                             /* inside the runner: park the call and yield */
         fill_req(&me->req, aux, aln, max_pos, dir, me->len);
+        me->req.started = 0;
         me->state = 1;
         swapcontext(&me->uc, tl_sched);
         return me->req.ret;
@@ -464,6 +524,8 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         c->read = -1;
     }
     ext_req_t **pend = (ext_req_t **)malloc(sizeof(ext_req_t *) * (size_t)W);
+    int32_t *pslot = (int32_t *)malloc(sizeof(int32_t) * (size_t)W);
+    uint8_t *pdone = (uint8_t *)malloc((size_t)W);
     int next = 0, live = 0;
     long launches = 0, calls = 0;
     double t_gpu = 0.0;
@@ -486,17 +548,19 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
                 }
             }
         }
+        /* one sliced launch over every parked call (slot = its coroutine): the finished
+         * ones resume, the others stay parked with their state on the device */
         int np = 0;
         for (int k = 0; k < W; ++k)
-            if (co[k].read >= 0 && co[k].state == 1) pend[np++] = &co[k].req;
+            if (co[k].read >= 0 && co[k].state == 1) { pend[np] = &co[k].req; pslot[np++] = k; }
         if (np == 0) continue;
         const double tg = hsa_now();
-        run_reqs(ix, pend, np);
+        const int nd = run_slices(ix, pend, pslot, np, W, pdone);
         t_gpu += hsa_now() - tg;
-        calls += np;
+        calls += nd;
         ++launches;
-        for (int k = 0; k < W; ++k)
-            if (co[k].read >= 0 && co[k].state == 1) co[k].state = 0;
+        for (int j = 0; j < np; ++j)
+            if (pdone[j]) co[pslot[j]].state = 0;
     }
     for (int k = 0; k < W; ++k) {
         co_t *c = co + k;
@@ -504,7 +568,7 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         free(c->aux.width_back); free(c->aux.width_fore); free(c->aux.width_seed); free(c->aux.rc_seq);
         stack_free(c->aux.stack);
     }
-    free(co); free(pend);
+    free(co); free(pend); free(pslot); free(pdone);
     tl_sched = NULL;
     if (getenv("HSA_VERBOSE"))
         fprintf(stderr, "[hsa] splice runner: %d reads, %ld extension calls in %ld launches: %.3f s in the launches "

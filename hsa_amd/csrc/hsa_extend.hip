@@ -39,6 +39,8 @@
 #define EXT_E_SCORE 2      // an entry's score outside the stack's buckets (undefined in the reference)
 #define EXT_E_RANK 3       // a rank position past the text (undefined in the reference)
 #define EXT_E_WIN 4        // a read position outside the call's window
+#define EXT_CONT (-999)    // sliced mode: not finished, state saved in its slot
+#define EXT_STATE_U4 6     // saved state of a sliced call, in uint4
 
 struct ExtArgs {
     RankDir fwd, rev;
@@ -54,6 +56,13 @@ struct ExtArgs {
     uint32_t *heads, *cnt;       // per lane: nb each
     uint32_t cap, nb;
     uint32_t lds;                // bucket heads and counts in LDS (nb <= EXT_LDS_NB), else in heads/cnt
+    // sliced mode (hsa_extend_sliced): lane t works on persistent slot slots[t] (its stack
+    // and the state below stay in HBM between launches), resumes it when resume[t], and
+    // stops after `budget` pops with ret = EXT_CONT
+    const int32_t *slots;
+    const uint8_t *resume;
+    uint32_t budget;
+    uint4 *state;                // per slot: EXT_STATE_U4 uint4
     int32_t *ret, *mp_out;
     uint32_t *aln_out;           // 9 words per job
 };
@@ -81,17 +90,20 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
     const int jb = a.job_list ? a.job_list[t] : t;
     const hsa_ext_job_t J = a.jobs[jb];
     const hsa_regime_t R = a.regimes[J.regime];
-    uint4 *const P = a.pool + (size_t)t * a.cap * 2;
+    const size_t sl = a.slots ? (size_t)a.slots[t] : (size_t)t;   // the lane's stack region
+    const bool resume = a.resume && a.resume[t];
+    uint4 *const P = a.pool + sl * a.cap * 2;
     // bucket heads and counts (gap_stack_t's per-score stacks): lane-interleaved in LDS,
     // or per lane in HBM when there are too many buckets
     extern __shared__ uint32_t s_hn[];
-    uint32_t *const Hb = a.lds ? s_hn + threadIdx.x : a.heads + (size_t)t * a.nb;
-    uint32_t *const Nb = a.lds ? s_hn + (size_t)a.nb * EXT_NT + threadIdx.x : a.cnt + (size_t)t * a.nb;
+    uint32_t *const Hb = a.lds ? s_hn + threadIdx.x : a.heads + sl * a.nb;
+    uint32_t *const Nb = a.lds ? s_hn + (size_t)a.nb * EXT_NT + threadIdx.x : a.cnt + sl * a.nb;
     const uint32_t hs = a.lds ? EXT_NT : 1u;
 #define H(b) Hb[(uint32_t)(b) * hs]
 #define N(b) Nb[(uint32_t)(b) * hs]
     const int nst = R.n_stacks;
-    for (int b = 0; b < nst; ++b) N(b) = 0;
+    if (!resume)
+        for (int b = 0; b < nst; ++b) N(b) = 0;
     int best = nst, n_ent = 0, err = 0;
     uint32_t top = 0, freel = EXT_NIL;
     const int len = J.len, bw = J.dir;
@@ -171,13 +183,28 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
     uint32_t aln[9];
 #pragma unroll
     for (int w = 0; w < 9; ++w) aln[w] = J.aln[w];
-    push(len, aln[1], aln[2], aln[3], aln[4], (int)(aln[0] & 0xFFFFu), (int)((aln[0] >> 16) & 0xFFu), (int)(aln[0] >> 24),
-         ST_M);                                                   // bwtgap.c:644 / :658
     const int best_score = (R.max_diff + 1) * R.s_mm + (R.max_gapo + 1) * R.s_gapo + (R.max_gape + 1) * R.s_gape;
     const int max_diff = R.max_diff;
-    const int start = (int)aln[6], end = (int)aln[7];
+    const int start = (int)aln[6], end = (int)aln[7];    // the call's hit as given: fixed (bwtgap.c:365)
     int max_pos = J.max_pos, ret = 0;
+    uint4 *const S = a.state ? a.state + sl * EXT_STATE_U4 : nullptr;
+    if (resume) {                                         // a sliced call's saved state
+        const uint4 s0 = S[0], s1 = S[1];
+        best = (int)s0.x; n_ent = (int)s0.y; top = s0.z; freel = s0.w;
+        pend = s1.x != 0; pscore = (int)s1.y; max_pos = (int)s1.z;
+        pe0 = S[2]; pe1 = S[3];
+        const uint4 a0 = S[4], a1 = S[5];
+        aln[0] = a0.x; aln[1] = a0.y; aln[2] = a0.z; aln[3] = a0.w;
+        aln[4] = a1.x; aln[5] = a1.y; aln[6] = a1.z; aln[7] = a1.w; aln[8] = s1.w;
+    } else {
+        push(len, aln[1], aln[2], aln[3], aln[4], (int)(aln[0] & 0xFFFFu), (int)((aln[0] >> 16) & 0xFFu),
+             (int)(aln[0] >> 24), ST_M);                                    // bwtgap.c:644 / :658
+    }
+    uint32_t pops = 0;
+    bool cont = false;
     while (n_ent != 0 && !err) {
+        if (a.budget && pops == a.budget) { cont = true; break; }
+        ++pops;
         if (n_ent > R.max_entries) break;
         // gap_pop (bwtgap.c:77-92)
         uint4 e0, e1;
@@ -299,7 +326,14 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
         }
     }
     if (err) ret = EXT_ERR - err;
-    else if (ret != 1) ret = max_pos != J.max_pos ? 2 : -1;
+    else if (cont) {
+        ret = EXT_CONT;
+        S[0] = make_uint4((uint32_t)best, (uint32_t)n_ent, top, freel);
+        S[1] = make_uint4(pend ? 1u : 0u, (uint32_t)pscore, (uint32_t)max_pos, aln[8]);
+        S[2] = pe0; S[3] = pe1;
+        S[4] = make_uint4(aln[0], aln[1], aln[2], aln[3]);
+        S[5] = make_uint4(aln[4], aln[5], aln[6], aln[7]);
+    } else if (ret != 1) ret = max_pos != J.max_pos ? 2 : -1;
     a.ret[jb] = ret;
     a.mp_out[jb] = max_pos;
 #pragma unroll
@@ -380,6 +414,7 @@ extern "C" int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, in
     A.mp_out = (int32_t *)(dout + o_mp);
     A.aln_out = (uint32_t *)(dout + o_aln);
     A.nb = nb;
+    A.slots = nullptr; A.resume = nullptr; A.budget = 0; A.state = nullptr;
     // capacity passes: every call with a small stack, then the calls that overflowed it
     // with larger ones, up to what the reference's max_entries bound allows (live entries
     // <= max_entries + 9: the check precedes the pop, bwtgap.c:374)
@@ -424,5 +459,100 @@ extern "C" int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, in
                       e >= 1 && e <= 4 ? why[e] : "?");
         return HSA_E_ARG;
     }
+    return 0;
+}
+
+// ---------------------------------------------------------------- sliced mode
+// The splice runner's calls (bwtext_gpu.c) come in rounds from coroutines that wait on
+// them; one long search would hold every other read's next round.  So each launch runs
+// every call in flight for at most `budget` pops: a call that finishes returns its
+// result, one that does not keeps its stack and state in its slot (HBM, persistent
+// across launches) and is resumed by the next launch, while the coroutines whose calls
+// finished go on.  Slots hold EXT_SLICE_CAP entries and EXT_SLICE_NB buckets; a call
+// that needs more reports EXT_E_CAP / EXT_E_SCORE here and is re-run by the caller
+// through hsa_extend_batch.
+#define EXT_SLICE_CAP 2048u
+#define EXT_SLICE_NB 256u
+
+extern "C" int hsa_extend_sliced(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_ext_job_t *jobs,
+                                 const int32_t *slots, const uint8_t *resume, int n, const uint8_t *codes,
+                                 const int32_t *bids, size_t win_len, int n_slots, uint32_t budget, int32_t *ret,
+                                 int32_t *max_pos, uint32_t *aln_out)
+{
+    if (n < 0 || n_regimes < 1 || n_slots < 1 || (n > 0 && (!jobs || !regimes || !slots || !resume || !ret ||
+                                                           !max_pos || !aln_out))) {
+        hsa_set_error("hsa_extend_sliced: bad arguments");
+        return HSA_E_ARG;
+    }
+    if (n == 0) return 0;
+    if (int rc0 = hsa_need32(ix)) return rc0;
+    for (int r = 0; r < n_regimes; ++r)
+        if (regimes[r].n_stacks < 1 || regimes[r].n_stacks > (int)EXT_SLICE_NB) {
+            hsa_set_error("hsa_extend_sliced: regime %d: n_stacks %d outside 1..%u", r, regimes[r].n_stacks,
+                          EXT_SLICE_NB);
+            return HSA_E_ARG;
+        }
+    for (int j = 0; j < n; ++j) {
+        const hsa_ext_job_t &J = jobs[j];
+        if (J.regime < 0 || J.regime >= n_regimes || J.n < 0 || (J.n > 0 && J.off + (uint64_t)J.n > win_len) ||
+            (J.dir != 0 && J.dir != 1) || slots[j] < 0 || slots[j] >= n_slots) {
+            hsa_set_error("hsa_extend_sliced: call %d: bad job", j);
+            return HSA_E_ARG;
+        }
+    }
+    HSA_HIP(hipSetDevice(ix->device));
+    ix->staged_valid = 0;
+    // persistent slots: stacks, bucket heads and counts, state (grown, never shrunk:
+    // contents survive between calls with the same n_slots)
+    const size_t pb = (size_t)n_slots * EXT_SLICE_CAP * 32, hb = (size_t)n_slots * EXT_SLICE_NB * 4;
+    const size_t sb = (size_t)n_slots * EXT_STATE_U4 * 16;
+    int rc;
+    if ((rc = hsa_grow(&ix->d_slices, &ix->d_slices_cap, pb + 2 * hb + sb + 256))) return rc;
+    const size_t rb = (size_t)n_regimes * sizeof(hsa_regime_t), jbb = (size_t)n * sizeof(hsa_ext_job_t);
+    const size_t o_jobs = (rb + 255) / 256 * 256, o_codes = o_jobs + (jbb + 255) / 256 * 256;
+    const size_t o_bids = o_codes + (win_len + 255) / 256 * 256, o_slot = o_bids + (win_len * 4 + 255) / 256 * 256;
+    const size_t o_res = o_slot + ((size_t)n * 4 + 255) / 256 * 256, inb = o_res + (size_t)n + 256;
+    const size_t o_mp = ((size_t)n * 4 + 255) / 256 * 256, o_aln = o_mp + ((size_t)n * 4 + 255) / 256 * 256;
+    const size_t outb = o_aln + (size_t)n * 36 + 256;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, inb)) || (rc = hsa_grow(&ix->d_out, &ix->d_out_cap, outb))) return rc;
+    char *din = (char *)ix->d_in, *dout = (char *)ix->d_out;
+    HSA_HIP(hipMemcpyAsync(din, regimes, rb, hipMemcpyHostToDevice, ix->stream));
+    HSA_HIP(hipMemcpyAsync(din + o_jobs, jobs, jbb, hipMemcpyHostToDevice, ix->stream));
+    if (win_len) {
+        HSA_HIP(hipMemcpyAsync(din + o_codes, codes, win_len, hipMemcpyHostToDevice, ix->stream));
+        HSA_HIP(hipMemcpyAsync(din + o_bids, bids, win_len * 4, hipMemcpyHostToDevice, ix->stream));
+    }
+    HSA_HIP(hipMemcpyAsync(din + o_slot, slots, (size_t)n * 4, hipMemcpyHostToDevice, ix->stream));
+    HSA_HIP(hipMemcpyAsync(din + o_res, resume, (size_t)n, hipMemcpyHostToDevice, ix->stream));
+    ExtArgs A;
+    A.fwd = RankDir{ix->blk[0], ix->isa0};
+    A.rev = RankDir{ix->blk[1], ix->risa0};
+    A.T = ix->T; A.rT = ix->rT;
+    memcpy(A.C, ix->C, sizeof A.C);
+    A.regimes = (const hsa_regime_t *)din;
+    A.jobs = (const hsa_ext_job_t *)(din + o_jobs);
+    A.job_list = nullptr;
+    A.n = n;
+    A.codes = (const uint8_t *)(din + o_codes);
+    A.bids = (const int32_t *)(din + o_bids);
+    A.pool = (uint4 *)ix->d_slices;
+    A.heads = (uint32_t *)((char *)ix->d_slices + pb);
+    A.cnt = (uint32_t *)((char *)ix->d_slices + pb + hb);
+    A.state = (uint4 *)((char *)ix->d_slices + pb + 2 * hb);
+    A.cap = EXT_SLICE_CAP;
+    A.nb = EXT_SLICE_NB;
+    A.lds = 0;
+    A.slots = (const int32_t *)(din + o_slot);
+    A.resume = (const uint8_t *)(din + o_res);
+    A.budget = budget;
+    A.ret = (int32_t *)dout;
+    A.mp_out = (int32_t *)(dout + o_mp);
+    A.aln_out = (uint32_t *)(dout + o_aln);
+    hipLaunchKernelGGL(k_extend, dim3((unsigned)((n + EXT_NT - 1) / EXT_NT)), dim3(EXT_NT), 0, ix->stream, A);
+    HSA_HIP(hipGetLastError());
+    HSA_HIP(hipMemcpyAsync(ret, dout, (size_t)n * 4, hipMemcpyDeviceToHost, ix->stream));
+    HSA_HIP(hipMemcpyAsync(max_pos, dout + o_mp, (size_t)n * 4, hipMemcpyDeviceToHost, ix->stream));
+    HSA_HIP(hipMemcpyAsync(aln_out, dout + o_aln, (size_t)n * 36, hipMemcpyDeviceToHost, ix->stream));
+    HSA_HIP(hipStreamSynchronize(ix->stream));
     return 0;
 }

