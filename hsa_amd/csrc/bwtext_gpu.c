@@ -25,10 +25,13 @@
  * bwt_extend_backward / bwt_extend_foreward / bwt_cal_width.
  */
 #define _GNU_SOURCE
+/* coroutine switches _longjmp between stacks, which the fortified longjmp refuses */
+#undef _FORTIFY_SOURCE
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <setjmp.h>
 #include <sys/mman.h>
 #include <ucontext.h>
 
@@ -36,7 +39,7 @@
 #include "bwtaln_gpu.h"
 
 #define CO_STACK (512u << 10)     /* C stack per coroutine (the host's splice code + ours) */
-#define CO_MAX 4096               /* coroutines alive at once */
+#define CO_MAX 16384              /* coroutines alive at once (= extension slots) */
 #define SLICE_POPS 256u           /* pops per call per launch (hsa_extend_sliced) */
 
 /* One parked extension call. */
@@ -53,7 +56,10 @@ typedef struct {
 } ext_req_t;
 
 typedef struct {
-    ucontext_t uc;
+    ucontext_t uc;                /* the coroutine's first entry (makecontext) */
+    jmp_buf jb;                   /* where it parked (switches use _setjmp/_longjmp: no
+                                     signal-mask system calls, unlike swapcontext) */
+    int entered;
     void *stack;
     int read;                     /* index into the run's reads, -1 idle */
     int state;                    /* 0 runnable, 1 parked, 2 done */
@@ -66,7 +72,7 @@ typedef struct {
 } co_t;
 
 static __thread co_t *tl_co;          /* the running coroutine, or NULL outside the runner */
-static __thread ucontext_t *tl_sched; /* the runner's context */
+static __thread jmp_buf *tl_sched;    /* the runner's resume point */
 
 static int imin(int a, int b) { return a < b ? a : b; }
 static int imax(int a, int b) { return a > b ? a : b; }
@@ -223,7 +229,7 @@ static int extend(bwt_aux_t *aux, bwt_aln1_t *aln, int *max_pos, int dir)
         fill_req(&me->req, aux, aln, max_pos, dir, me->len);
         me->req.started = 0;
         me->state = 1;
-        swapcontext(&me->uc, tl_sched);
+        if (!_setjmp(me->jb)) _longjmp(*tl_sched, 1);
         return me->req.ret;
     }
     ext_req_t q;                          /* a direct call: a batch of one */
@@ -467,7 +473,7 @@ static void co_entry(void)
     co_t *me = tl_co;
     me->result = bwt_splice_match(&me->aux, &me->n_aln);
     me->state = 2;
-    /* returning resumes uc_link: the runner */
+    _longjmp(*tl_sched, 1);          /* never returns: the runner takes the next read */
 }
 
 /* Start coroutine c on read r: the aux bwa_cal_sa_reg_gap hands bwt_splice_match
@@ -492,8 +498,9 @@ static void co_start(co_t *c, int r, const hsa_splice_read_t *rd)
     getcontext(&c->uc);
     c->uc.uc_stack.ss_sp = c->stack;
     c->uc.uc_stack.ss_size = CO_STACK;
-    c->uc.uc_link = tl_sched;
+    c->uc.uc_link = NULL;
     makecontext(&c->uc, co_entry, 0);
+    c->entered = 0;
 }
 
 /* bwt_splice_match for reads[0..n) (see the file comment): out[r] / n_out[r] are what
@@ -507,7 +514,7 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     hsa_index_t *ix = hsa_gpu_index_of(bi);
     const int W = n < CO_MAX ? n : CO_MAX;
     co_t *co = (co_t *)calloc((size_t)W, sizeof(co_t));
-    ucontext_t sched;
+    jmp_buf sched;
     tl_sched = &sched;
     for (int k = 0; k < W; ++k) {
         co_t *c = co + k;
@@ -538,7 +545,10 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
             co_t *c = co + k;
             while (c->read >= 0 && c->state == 0) {
                 tl_co = c;
-                swapcontext(&sched, &c->uc);
+                if (!_setjmp(sched)) {
+                    if (!c->entered) { c->entered = 1; setcontext(&c->uc); }
+                    _longjmp(c->jb, 1);
+                }
                 tl_co = NULL;
                 if (c->state == 2) {
                     out[c->read] = c->result;
@@ -557,6 +567,9 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         const double tg = hsa_now();
         const int nd = run_slices(ix, pend, pslot, np, W, pdone);
         t_gpu += hsa_now() - tg;
+        if (getenv("HSA_EXT_TRACE"))
+            fprintf(stderr, "[hsa_splice_run] round %ld: %d parked, %d finished, %.3f ms\n", launches, np, nd,
+                    1e3 * (hsa_now() - tg));
         calls += nd;
         ++launches;
         for (int j = 0; j < np; ++j)

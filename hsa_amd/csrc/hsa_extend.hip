@@ -19,6 +19,8 @@
 // reads its read only inside the window [lo, lo + n) its arguments determine
 // (include/hsa_gpu.h); a read outside is reported, never performed.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "hsa_device.h"
@@ -56,6 +58,7 @@ struct ExtArgs {
     uint32_t *heads, *cnt;       // per lane: nb each
     uint32_t cap, nb;
     uint32_t lds;                // bucket heads and counts in LDS (nb <= EXT_LDS_NB), else in heads/cnt
+    uint32_t lnb;                // buckets per lane in the LDS layout
     // sliced mode (hsa_extend_sliced): lane t works on persistent slot slots[t] (its stack
     // and the state below stay in HBM between launches), resumes it when resume[t], and
     // stops after `budget` pops with ret = EXT_CONT
@@ -97,13 +100,19 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
     // or per lane in HBM when there are too many buckets
     extern __shared__ uint32_t s_hn[];
     uint32_t *const Hb = a.lds ? s_hn + threadIdx.x : a.heads + sl * a.nb;
-    uint32_t *const Nb = a.lds ? s_hn + (size_t)a.nb * EXT_NT + threadIdx.x : a.cnt + sl * a.nb;
+    uint32_t *const Nb = a.lds ? s_hn + (size_t)a.lnb * EXT_NT + threadIdx.x : a.cnt + sl * a.nb;
     const uint32_t hs = a.lds ? EXT_NT : 1u;
 #define H(b) Hb[(uint32_t)(b) * hs]
 #define N(b) Nb[(uint32_t)(b) * hs]
     const int nst = R.n_stacks;
-    if (!resume)
+    // sliced mode keeps the slot's heads and counts in HBM between launches; with the
+    // bookkeeping in LDS they are copied in on resume and out when the call pauses
+    uint32_t *const gH = a.heads + sl * a.nb, *const gN = a.cnt + sl * a.nb;
+    if (!resume) {
         for (int b = 0; b < nst; ++b) N(b) = 0;
+    } else if (a.lds) {
+        for (int b = 0; b < nst; ++b) { H(b) = gH[b]; N(b) = gN[b]; }
+    }
     int best = nst, n_ent = 0, err = 0;
     uint32_t top = 0, freel = EXT_NIL;
     const int len = J.len, bw = J.dir;
@@ -328,6 +337,8 @@ __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)
     if (err) ret = EXT_ERR - err;
     else if (cont) {
         ret = EXT_CONT;
+        if (a.lds)
+            for (int b = 0; b < nst; ++b) { gH[b] = H(b); gN[b] = N(b); }
         S[0] = make_uint4((uint32_t)best, (uint32_t)n_ent, top, freel);
         S[1] = make_uint4(pend ? 1u : 0u, (uint32_t)pscore, (uint32_t)max_pos, aln[8]);
         S[2] = pe0; S[3] = pe1;
@@ -435,6 +446,7 @@ extern "C" int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, in
             A.job_list = (const int32_t *)(din + o_list) + c0;
             A.n = (int)m;
             A.lds = nb <= EXT_LDS_NB;
+            A.lnb = nb;
             const size_t shm = A.lds ? (size_t)nb * EXT_NT * 8 : 0;
             hipLaunchKernelGGL(k_extend, dim3((unsigned)((m + EXT_NT - 1) / EXT_NT)), dim3(EXT_NT), shm, ix->stream, A);
             HSA_HIP(hipGetLastError());
@@ -541,15 +553,31 @@ extern "C" int hsa_extend_sliced(hsa_index_t *ix, const hsa_regime_t *regimes, i
     A.state = (uint4 *)((char *)ix->d_slices + pb + 2 * hb);
     A.cap = EXT_SLICE_CAP;
     A.nb = EXT_SLICE_NB;
-    A.lds = 0;
+    int nbmax = 1;
+    for (int r = 0; r < n_regimes; ++r) nbmax = regimes[r].n_stacks > nbmax ? regimes[r].n_stacks : nbmax;
+    A.lds = nbmax <= (int)EXT_LDS_NB;
+    A.lnb = (uint32_t)nbmax;
     A.slots = (const int32_t *)(din + o_slot);
     A.resume = (const uint8_t *)(din + o_res);
     A.budget = budget;
     A.ret = (int32_t *)dout;
     A.mp_out = (int32_t *)(dout + o_mp);
     A.aln_out = (uint32_t *)(dout + o_aln);
-    hipLaunchKernelGGL(k_extend, dim3((unsigned)((n + EXT_NT - 1) / EXT_NT)), dim3(EXT_NT), 0, ix->stream, A);
+    static const bool trace = getenv("HSA_EXT_TRACE") != nullptr;
+    if (trace) {
+        HSA_HIP(hipStreamSynchronize(ix->stream));
+        HSA_HIP(hipEventRecord(ix->ev0, ix->stream));
+    }
+    const size_t shm = A.lds ? (size_t)nbmax * EXT_NT * 8 : 0;
+    hipLaunchKernelGGL(k_extend, dim3((unsigned)((n + EXT_NT - 1) / EXT_NT)), dim3(EXT_NT), shm, ix->stream, A);
     HSA_HIP(hipGetLastError());
+    if (trace) {
+        HSA_HIP(hipEventRecord(ix->ev1, ix->stream));
+        HSA_HIP(hipEventSynchronize(ix->ev1));
+        float ms = 0.f;
+        HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+        fprintf(stderr, "[hsa_extend_sliced] %d calls, %zu window bytes, kernel %.3f ms\n", n, win_len, ms);
+    }
     HSA_HIP(hipMemcpyAsync(ret, dout, (size_t)n * 4, hipMemcpyDeviceToHost, ix->stream));
     HSA_HIP(hipMemcpyAsync(max_pos, dout + o_mp, (size_t)n * 4, hipMemcpyDeviceToHost, ix->stream));
     HSA_HIP(hipMemcpyAsync(aln_out, dout + o_aln, (size_t)n * 36, hipMemcpyDeviceToHost, ix->stream));

@@ -25,13 +25,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(binary, args, prefix, fq, out, env=None, timeout=1800):
+def run(binary, args, prefix, fq, out, env=None, timeout=1800, err_path=None):
     t0 = time.perf_counter()
     with open(out, "wb") as f:
         r = subprocess.run([binary, "aln", *args, prefix, fq], stdout=f, stderr=subprocess.PIPE, timeout=timeout,
                            env=env)
     wall = time.perf_counter() - t0
     err = r.stderr.decode(errors="replace")
+    if err_path:
+        with open(err_path, "w") as f:
+            f.write(err)
     if r.returncode:
         raise SystemExit(f"{binary} failed ({r.returncode}):\n{err[-2000:]}")
     secs = [float(x) for x in re.findall(r"^([0-9.]+) sec$", err, re.M)]
@@ -58,6 +61,7 @@ def main():
     ap.add_argument("--bins", nargs="+", default=["HSA", "HSA_gpu_mg", "HSA_gpu_all"])
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--out", default=None, help="JSON result file")
+    ap.add_argument("--stderr-dir", default=None, help="keep each program's stderr here")
     a = ap.parse_args()
 
     from hsa_amd import index_build, synth
@@ -83,7 +87,8 @@ def main():
     env = dict(os.environ, HSA_VERBOSE="1")
     for b in a.bins:
         path = os.path.join(ROOT, "oracle", "_ref", b)
-        r = run(path, a.args.split(), fa, fq, os.path.join(wd, f"{b}.sam"), env=env)
+        r = run(path, a.args.split(), fa, fq, os.path.join(wd, f"{b}.sam"), env=env,
+                err_path=os.path.join(a.stderr_dir, f"{b}.err") if a.stderr_dir else None)
         r["reads_per_s"] = round(a.reads / r["wall_s"], 1)
         res["runs"][b] = r
         print(f"[e2e] {b}: wall {r['wall_s']} s ({r['reads_per_s']} reads/s), search+splice {r['search_cpu_s']} "
