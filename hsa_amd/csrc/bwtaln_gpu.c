@@ -37,6 +37,10 @@
 #pragma weak hsa_splice_widths_prefetch
 #pragma weak hsa_splice_wmemo_clear
 #pragma weak hsa_splice_wmemo_stats
+#pragma weak hsa_splice_take_sa_list
+#pragma weak hsa_splice_sa_prefetch
+#pragma weak hsa_splice_sa_clear
+#pragma weak hsa_splice_sa_stats
 
 _Static_assert(sizeof(bwt_aln1_t) == 36, "bwt_aln1_t layout");
 _Static_assert(sizeof(gap_opt_t) == 64, "gap_opt_t layout");
@@ -501,7 +505,7 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     const int n_stacks = hsa_aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
     /* the splice path's seed searches of every fallback read in one GPU batch, when
      * the host's bwt_splice_match calls our bwt_match_gap (bwtgap_gpu.c) */
-    int prefetched = 0, wprefetched = 0;
+    int prefetched = 0, wprefetched = 0, saprefetched = 0;
     double t_pf = 0.0;
     const double t1 = hsa_now();
     if (have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active()) {
@@ -542,6 +546,15 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
                 hsa_splice_widths_prefetch(bi_bwt, nf, fp);
                 wprefetched = 1;
             }
+            /* and, with the whole splice path on the device (bwtext_gpu.c), the SA ->
+             * position lookups its correlation makes on the prefetched hits */
+            uint32_t *sal = NULL;
+            const size_t nsal = hsa_splice_take_sa_list ? hsa_splice_take_sa_list(&sal) : 0;
+            if (hsa_splice_sa_prefetch && hsa_splice_extend_active && hsa_splice_extend_active() && nsal) {
+                hsa_splice_sa_prefetch(bi_bwt, nsal, sal);
+                saprefetched = 1;
+            }
+            free(sal);
             t_pf = hsa_now() - t_pf;
             prefetched = 1;
             free(fa); free(fp); free(fo); free(rc);
@@ -643,6 +656,15 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
                     (unsigned long long)wh, (unsigned long long)wm);
         }
         hsa_splice_wmemo_clear();
+    }
+    if (saprefetched) {
+        if (getenv("HSA_VERBOSE")) {
+            uint64_t sh = 0, sm = 0;
+            hsa_splice_sa_stats(&sh, &sm);
+            fprintf(stderr, "[hsa] splice SA -> position: %llu lookups answered from the batch, %llu in the runner's "
+                            "rounds\n", (unsigned long long)sh, (unsigned long long)sm);
+        }
+        hsa_splice_sa_clear();
     }
     hsa_free(hits);
     free(lens); free(offs); free(codes); free(n_aln); free(flags); free(hoff); free(sp);

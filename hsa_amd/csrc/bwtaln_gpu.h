@@ -34,6 +34,12 @@ typedef struct {
     gap_opt_t opt;             /* local_opt as bwt_splice_match receives it for this read */
 } hsa_splice_read_t;
 int hsa_splice_extend_active(void);
+size_t hsa_splice_take_sa_list(uint32_t **idx);
+int hsa_splice_sa_prefetch(const Idx2BWT *bi, size_t n, const uint32_t *idx);
+void hsa_splice_sa_clear(void);
+void hsa_splice_sa_stats(uint64_t *hits, uint64_t *misses);
+void hsa_splice_sa_position(Idx2BWT *bi, unsigned int sa_index, unsigned int *seq_id, unsigned int *ori_pos,
+                            unsigned int *occ_pos);
 int hsa_splice_width_active(void);
 int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux);
 void hsa_splice_wmemo_clear(void);

@@ -53,6 +53,9 @@ typedef struct {
     int *max_pos_io;
     int ret;
     int started;                  /* sliced: submitted before, its state is in its slot */
+    int kind;                     /* 0 an extension, 1 an SA -> position lookup */
+    uint32_t sa;                  /* kind 1: the SA index, and where its answer goes */
+    unsigned int *sid_p, *ori_p, *occ_p;
 } ext_req_t;
 
 typedef struct {
@@ -228,6 +231,7 @@ static int extend(bwt_aux_t *aux, bwt_aln1_t *aln, int *max_pos, int dir)
     if (me) {                             /* inside the runner: park the call and yield */
         fill_req(&me->req, aux, aln, max_pos, dir, me->len);
         me->req.started = 0;
+        me->req.kind = 0;
         me->state = 1;
         if (!_setjmp(me->jb)) _longjmp(*tl_sched, 1);
         return me->req.ret;
@@ -448,6 +452,131 @@ int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
     return 0;
 }
 
+/* ------------------------------------------------------------ SA -> position
+ * The splice path's BWTRetrievePositionFromSAIndex calls (bwt_aln_corelate_check,
+ * bwtgap.c:699, :712; check_site_by_intron_end, :615), redirected to
+ * hsa_splice_sa_position by the host's link recipe (its bwtgap.o's reference renamed,
+ * INTEGRATION.md; the SAM stage keeps the host's own).  Answers come from a table filled
+ * on the GPU before the runner (the ranges the correlation reads of every prefetched
+ * seed and anchor hit); a lookup the table misses parks its coroutine, and each round's
+ * parked lookups are one GPU launch. */
+typedef struct { uint32_t key, sid, ori, occ; } sa_ent_t;   /* key = sa index + 1 (0: empty) */
+static sa_ent_t *g_sa;
+static size_t g_sa_cap2, g_sa_n2;
+static uint64_t g_sa_hits, g_sa_misses;
+static pthread_mutex_t g_sa_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static size_t sa_slot(uint32_t key, size_t cap)
+{
+    return (size_t)((key * 0x9E3779B97F4A7C15ull) >> 20) & (cap - 1);
+}
+
+static void sa_put(uint32_t idx, const uint32_t o4[4])      /* caller holds g_sa_mu */
+{
+    if (2 * (g_sa_n2 + 1) > g_sa_cap2) {
+        size_t cap = g_sa_cap2 ? 2 * g_sa_cap2 : 1u << 16;
+        sa_ent_t *t = (sa_ent_t *)calloc(cap, sizeof(sa_ent_t));
+        for (size_t i = 0; i < g_sa_cap2; ++i) {
+            if (!g_sa[i].key) continue;
+            size_t j = sa_slot(g_sa[i].key, cap);
+            while (t[j].key) j = (j + 1) & (cap - 1);
+            t[j] = g_sa[i];
+        }
+        free(g_sa);
+        g_sa = t;
+        g_sa_cap2 = cap;
+    }
+    const uint32_t key = idx + 1u;
+    size_t j = sa_slot(key, g_sa_cap2);
+    while (g_sa[j].key && g_sa[j].key != key) j = (j + 1) & (g_sa_cap2 - 1);
+    if (g_sa[j].key) return;
+    g_sa[j].key = key; g_sa[j].occ = o4[0]; g_sa[j].sid = o4[1]; g_sa[j].ori = o4[2];
+    ++g_sa_n2;
+}
+
+static const sa_ent_t *sa_get(uint32_t idx)                 /* caller holds g_sa_mu */
+{
+    if (!g_sa_n2) return NULL;
+    const uint32_t key = idx + 1u;
+    for (size_t j = sa_slot(key, g_sa_cap2); g_sa[j].key; j = (j + 1) & (g_sa_cap2 - 1))
+        if (g_sa[j].key == key) return g_sa + j;
+    return NULL;
+}
+
+/* BWTRetrievePositionFromSAIndex's outputs (2BWT-Interface.c:329-361): the packed
+ * position always, sequence id and 1-based position only when a block holds it. */
+static void sa_write(uint32_t occ, uint32_t sid, uint32_t ori, unsigned int *sid_p, unsigned int *ori_p,
+                     unsigned int *occ_p)
+{
+    *occ_p = occ;
+    if (sid != 0xFFFFFFFFu) { *sid_p = sid; *ori_p = ori; }
+}
+
+/* GPU lookups of idx[0..n) into the table (duplicates and known ones skipped). */
+int hsa_splice_sa_prefetch(const Idx2BWT *bi, size_t n, const uint32_t *idx)
+{
+    if (n == 0) return 0;
+    uint32_t *todo = (uint32_t *)malloc(sizeof(uint32_t) * n);
+    size_t m = 0;
+    pthread_mutex_lock(&g_sa_mu);
+    for (size_t i = 0; i < n; ++i) if (!sa_get(idx[i])) todo[m++] = idx[i];
+    pthread_mutex_unlock(&g_sa_mu);
+    if (m) {
+        uint32_t *o4 = (uint32_t *)malloc(sizeof(uint32_t) * 4 * m);
+        const int rc = hsa_sa_position_batch(hsa_gpu_index_of(bi), m, todo, o4);
+        if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
+        pthread_mutex_lock(&g_sa_mu);
+        for (size_t i = 0; i < m; ++i) sa_put(todo[i], o4 + 4 * i);
+        pthread_mutex_unlock(&g_sa_mu);
+        free(o4);
+    }
+    free(todo);
+    return 0;
+}
+
+void hsa_splice_sa_clear(void)
+{
+    pthread_mutex_lock(&g_sa_mu);
+    free(g_sa);
+    g_sa = NULL;
+    g_sa_cap2 = g_sa_n2 = 0;
+    pthread_mutex_unlock(&g_sa_mu);
+}
+
+void hsa_splice_sa_stats(uint64_t *hits, uint64_t *misses)
+{
+    pthread_mutex_lock(&g_sa_mu);
+    *hits = g_sa_hits; *misses = g_sa_misses;
+    g_sa_hits = g_sa_misses = 0;
+    pthread_mutex_unlock(&g_sa_mu);
+}
+
+/* BWTRetrievePositionFromSAIndex (2BWT-Interface.c:329) for the splice path. */
+void hsa_splice_sa_position(Idx2BWT *bi, unsigned int sa_index, unsigned int *seq_id, unsigned int *ori_pos,
+                            unsigned int *occ_pos)
+{
+    pthread_mutex_lock(&g_sa_mu);
+    const sa_ent_t *e = sa_get(sa_index);
+    sa_ent_t v = e ? *e : (sa_ent_t){0, 0, 0, 0};
+    if (e) ++g_sa_hits; else ++g_sa_misses;
+    pthread_mutex_unlock(&g_sa_mu);
+    if (e) { sa_write(v.occ, v.sid, v.ori, seq_id, ori_pos, occ_pos); return; }
+    co_t *me = tl_co;
+    if (me) {                             /* park; the round's lookups are one launch */
+        me->req.kind = 1;
+        me->req.sa = sa_index;
+        me->req.sid_p = seq_id; me->req.ori_p = ori_pos; me->req.occ_p = occ_pos;
+        me->state = 1;
+        if (!_setjmp(me->jb)) _longjmp(*tl_sched, 1);
+        return;
+    }
+    const uint32_t one = sa_index;
+    uint32_t o4[4];
+    const int rc = hsa_sa_position_batch(hsa_gpu_index_of(bi), 1, &one, o4);
+    if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
+    sa_write(o4[0], o4[1], o4[2], seq_id, ori_pos, occ_pos);
+}
+
 /* gap_init_stack's layout (bwtgap.c:13-27): the host's splice code resets and reads it */
 static gap_stack_t *stack_new(int n_stacks)
 {
@@ -531,6 +660,10 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         c->read = -1;
     }
     ext_req_t **pend = (ext_req_t **)malloc(sizeof(ext_req_t *) * (size_t)W);
+    uint32_t *sa_idx = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)W);
+    uint32_t *sa_o4 = (uint32_t *)malloc(sizeof(uint32_t) * 4 * (size_t)W);
+    int *sa_co = (int *)malloc(sizeof(int) * (size_t)W);
+    long sa_launches = 0;
     int32_t *pslot = (int32_t *)malloc(sizeof(int32_t) * (size_t)W);
     uint8_t *pdone = (uint8_t *)malloc((size_t)W);
     int next = 0, live = 0;
@@ -560,9 +693,27 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         }
         /* one sliced launch over every parked call (slot = its coroutine): the finished
          * ones resume, the others stay parked with their state on the device */
-        int np = 0;
+        int np = 0, nsa = 0;
         for (int k = 0; k < W; ++k)
-            if (co[k].read >= 0 && co[k].state == 1) { pend[np] = &co[k].req; pslot[np++] = k; }
+            if (co[k].read >= 0 && co[k].state == 1) {
+                if (co[k].req.kind == 1) { sa_idx[nsa] = co[k].req.sa; sa_co[nsa++] = k; }
+                else { pend[np] = &co[k].req; pslot[np++] = k; }
+            }
+        if (nsa > 0) {                    /* the round's SA -> position lookups: one launch */
+            const double ts = hsa_now();
+            const int rc = hsa_sa_position_batch(ix, (size_t)nsa, sa_idx, sa_o4);
+            if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
+            pthread_mutex_lock(&g_sa_mu);
+            for (int j = 0; j < nsa; ++j) {
+                ext_req_t *q = &co[sa_co[j]].req;
+                sa_write(sa_o4[4 * j], sa_o4[4 * j + 1], sa_o4[4 * j + 2], q->sid_p, q->ori_p, q->occ_p);
+                sa_put(sa_idx[j], sa_o4 + 4 * j);
+                co[sa_co[j]].state = 0;
+            }
+            pthread_mutex_unlock(&g_sa_mu);
+            t_gpu += hsa_now() - ts;
+            ++sa_launches;
+        }
         if (np == 0) continue;
         const double tg = hsa_now();
         const int nd = run_slices(ix, pend, pslot, np, W, pdone);
@@ -581,11 +732,11 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         free(c->aux.width_back); free(c->aux.width_fore); free(c->aux.width_seed); free(c->aux.rc_seq);
         stack_free(c->aux.stack);
     }
-    free(co); free(pend); free(pslot); free(pdone);
+    free(co); free(pend); free(pslot); free(pdone); free(sa_idx); free(sa_o4); free(sa_co);
     tl_sched = NULL;
     if (getenv("HSA_VERBOSE"))
-        fprintf(stderr, "[hsa] splice runner: %d reads, %ld extension calls in %ld launches: %.3f s in the launches "
-                        "(copies included), %.3f s of host splice code\n", n, calls, launches, t_gpu,
-                hsa_now() - t_run - t_gpu);
+        fprintf(stderr, "[hsa] splice runner: %d reads, %ld extension calls in %ld launches, %ld SA lookup launches: "
+                        "%.3f s in the launches (copies included), %.3f s of host splice code\n", n, calls, launches,
+                sa_launches, t_gpu, hsa_now() - t_run - t_gpu);
     return launches;
 }

@@ -240,6 +240,36 @@ static const memo_ent_t *memo_get(const bwt_aux_t *a)
     return hit;
 }
 
+/* The SA indices the splice path's correlation can look up for the prefetched hits
+ * (bwt_aln_corelate_check, bwtgap.c:698 and :711: k .. min(l, k + 49) of each hit),
+ * collected for the SA -> position prefetch (hsa_splice_take_sa_list). */
+static uint32_t *g_sa_list;
+static size_t g_sa_n, g_sa_cap;
+
+static void sa_list_add(const bwt_aln1_t *h, int n)     /* caller holds g_memo_mu */
+{
+    for (int x = 0; x < n; ++x)
+        for (uint64_t j = h[x].k; j <= h[x].l && j < (uint64_t)h[x].k + 50; ++j) {
+            if (g_sa_n == g_sa_cap) {
+                g_sa_cap = g_sa_cap ? 2 * g_sa_cap : 4096;
+                g_sa_list = (uint32_t *)realloc(g_sa_list, sizeof(uint32_t) * g_sa_cap);
+            }
+            g_sa_list[g_sa_n++] = (uint32_t)j;
+        }
+}
+
+/* The collected SA indices (ownership passes to the caller, who frees them). */
+size_t hsa_splice_take_sa_list(uint32_t **idx)
+{
+    pthread_mutex_lock(&g_memo_mu);
+    *idx = g_sa_list;
+    const size_t n = g_sa_n;
+    g_sa_list = NULL;
+    g_sa_n = g_sa_cap = 0;
+    pthread_mutex_unlock(&g_memo_mu);
+    return n;
+}
+
 /* Search calls[0..c) in one batch (bwt_match_gap_batch) and put every answer in the
  * table, keyed by the call's inputs: win[i] holds its width_back as it was before the
  * search (calls[i].width_back is a scratch copy the search rewrites; a width_seed
@@ -258,6 +288,7 @@ static void batch_into_memo(bwt_aux_t *calls, int c, bwt_width_t **win, int *n_o
         calls[i].width_back = win[i];
         if (alias) calls[i].width_seed = win[i];
         memo_put(calls + i, after, out[i], n_out[i]);
+        sa_list_add(out[i], n_out[i]);
         free(after); free(out[i]);
     }
     pthread_mutex_unlock(&g_memo_mu);

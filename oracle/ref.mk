@@ -100,7 +100,9 @@ $(OUT)/HSA_gpu_mg: $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPULIB)
 # bwt_extend_foreward (weakened in bwtgap.o too: hsa_amd/csrc/bwtext_gpu.c runs the
 # splice path of a batch's fallback reads as coroutines and their extensions as GPU
 # batches), bwt_cal_width (weakened in bwtaln.o: the splice path's widths from a table
-# filled on the GPU, bwtext_gpu.c), and the SAM stage's bwa_cal_pac_pos, weakened in bwtse.o, so that
+# filled on the GPU, bwtext_gpu.c), the splice path's SA -> position lookups (bwtgap.o's
+# reference to BWTRetrievePositionFromSAIndex renamed to hsa_splice_sa_position, so the
+# SAM stage keeps the host's own), and the SAM stage's bwa_cal_pac_pos, weakened in bwtse.o, so that
 # generate_sam_se_core (bwtse.c:911) calls OUR bwa_cal_pac_pos (hsa_amd/csrc/bwtse_gpu.c:
 # the batch's SA -> position lookups on the GPU).
 $(OUT)/obj/bwtse_weak.o: $(OUT)/obj/bwtse.o
@@ -111,7 +113,8 @@ $(OUT)/obj/bwtaln_weak_all.o: $(OUT)/obj/bwtaln.o
 
 $(OUT)/obj/bwtgap_weak_all.o: $(OUT)/obj/bwtgap.o
 	objcopy --weaken-symbol=bwt_match_gap --weaken-symbol=bwt_extend_foreward \
-	        --weaken-symbol=bwt_extend_backward $< $@
+	        --weaken-symbol=bwt_extend_backward \
+	        --redefine-sym BWTRetrievePositionFromSAIndex=hsa_splice_sa_position $< $@
 
 ALLOBJS   = $(filter-out $(OUT)/obj/bwtaln.o $(OUT)/obj/bwtgap.o $(OUT)/obj/bwtse.o,$(OBJS)) \
             $(OUT)/obj/bwtaln_weak_all.o $(OUT)/obj/bwtgap_weak_all.o $(OUT)/obj/bwtse_weak.o

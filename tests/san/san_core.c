@@ -34,10 +34,35 @@ int hsa_index_create(int device, uint32_t T, uint32_t isa0, const uint32_t C[5],
 
 void hsa_index_free(hsa_index_t *ix) { or_index_free((or_index_t *)ix); }
 
+/* the sampled SA and chromosome blocks of the (one) attached index */
+static uint32_t *g_sa_vals, *g_sa_blocks, g_sa_interval;
+static int g_sa_nblocks;
+
 int hsa_index_set_sa(hsa_index_t *ix, const uint32_t *sa, uint64_t n, uint32_t interval, const uint32_t *blocks,
                      int n_blocks)
 {
-    (void)ix; (void)sa; (void)n; (void)interval; (void)blocks; (void)n_blocks;
+    (void)ix;
+    free(g_sa_vals); free(g_sa_blocks);
+    g_sa_vals = (uint32_t *)malloc(n * 4);
+    memcpy(g_sa_vals, sa, n * 4);
+    g_sa_blocks = (uint32_t *)malloc((size_t)(n_blocks ? n_blocks : 1) * 16);
+    if (n_blocks) memcpy(g_sa_blocks, blocks, (size_t)n_blocks * 16);
+    g_sa_interval = interval;
+    g_sa_nblocks = n_blocks;
+    return 0;
+}
+
+/* hsa_sa_position_batch = BWTSaValue + BWTRetrievePositionFromSAIndex (or_sa_position):
+ * (occ, seq id, 1-based position, occ), id / position 0xFFFFFFFF when no block holds it. */
+int hsa_sa_position_batch(hsa_index_t *ix, size_t n, const uint32_t *sa_index, uint32_t *out4)
+{
+    if (!g_sa_vals) { hsa_gpu_set_error_text("no suffix array attached"); return HSA_E_ARG; }
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t sid = 0xFFFFFFFFu, ori = 0xFFFFFFFFu, occ = 0;
+        or_sa_position((const or_index_t *)ix, g_sa_vals, g_sa_interval, g_sa_blocks, g_sa_nblocks, sa_index[i], &sid,
+                       &ori, &occ);
+        out4[4 * i] = occ; out4[4 * i + 1] = sid; out4[4 * i + 2] = ori; out4[4 * i + 3] = occ;
+    }
     return 0;
 }
 
