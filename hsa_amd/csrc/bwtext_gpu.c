@@ -285,11 +285,20 @@ static size_t wkey(int type, int len, const ubyte_t *str, uint8_t *buf)
     return 5 + (size_t)len;
 }
 
-static uint64_t wfnv(const uint8_t *p, size_t n)
+static uint64_t key_hash(const uint8_t *p, size_t n)
 {
-    uint64_t h = 1469598103934665603ull;
-    for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
-    return h | 1;
+    /* 8 bytes per step (multiply-rotate), the tail byte by byte */
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+        h ^= h >> 29;
+    }
+    for (; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+    h ^= h >> 32;
+    return h | 1;                          /* 0 marks an empty slot */
 }
 
 static void wm_put(int type, int len, const ubyte_t *str, const uint32_t *w, int ret)   /* caller holds g_wm_mu */
@@ -309,7 +318,7 @@ static void wm_put(int type, int len, const ubyte_t *str, const uint32_t *w, int
     }
     uint8_t *key = (uint8_t *)malloc((size_t)len + 5);
     const size_t kl = wkey(type, len, str, key);
-    const uint64_t h = wfnv(key, kl);
+    const uint64_t h = key_hash(key, kl);
     size_t j = h & (g_wm_cap - 1);
     while (g_wm[j].h) {
         if (g_wm[j].h == h && g_wm[j].key_len == kl && !memcmp(g_wm[j].key, key, kl)) { free(key); return; }
@@ -357,7 +366,7 @@ int bwt_cal_width(const Idx2BWT *bi_bwt, int len, const ubyte_t *str, bwt_width_
     uint8_t stackbuf[1024];
     uint8_t *key = (size_t)len + 5 <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc((size_t)len + 5);
     const size_t kl = wkey(type == 1, len, str, key);
-    const uint64_t h = wfnv(key, kl);
+    const uint64_t h = key_hash(key, kl);
     int found = 0, ret = 0;
     pthread_mutex_lock(&g_wm_mu);
     if (g_wm_n)

@@ -174,10 +174,19 @@ static size_t key_of(const bwt_aux_t *a, uint8_t *buf)
     return o;
 }
 
-static uint64_t fnv1a(const uint8_t *p, size_t n)
+static uint64_t key_hash(const uint8_t *p, size_t n)
 {
-    uint64_t h = 1469598103934665603ull;
-    for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+    /* 8 bytes per step (multiply-rotate), the tail byte by byte */
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+        h ^= h >> 29;
+    }
+    for (; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+    h ^= h >> 32;
     return h | 1;                          /* 0 marks an empty slot */
 }
 
@@ -210,7 +219,7 @@ static void memo_put(const bwt_aux_t *in, const bwt_width_t *wout, const bwt_aln
     const size_t kl = key_of(in, NULL);
     uint8_t *key = (uint8_t *)malloc(kl);
     key_of(in, key);
-    const uint64_t h = fnv1a(key, kl);
+    const uint64_t h = key_hash(key, kl);
     size_t j = h & (g_memo_cap - 1);
     while (g_memo[j].h) {
         if (g_memo[j].h == h && g_memo[j].key_len == kl && !memcmp(g_memo[j].key, key, kl)) { free(key); return; }
@@ -232,7 +241,7 @@ static const memo_ent_t *memo_get(const bwt_aux_t *a)
     uint8_t stackbuf[4096];
     uint8_t *key = kl <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc(kl);
     key_of(a, key);
-    const uint64_t h = fnv1a(key, kl);
+    const uint64_t h = key_hash(key, kl);
     const memo_ent_t *hit = NULL;
     for (size_t j = h & (g_memo_cap - 1); g_memo[j].h; j = (j + 1) & (g_memo_cap - 1))
         if (g_memo[j].h == h && g_memo[j].key_len == kl && !memcmp(g_memo[j].key, key, kl)) { hit = g_memo + j; break; }
