@@ -2,6 +2,9 @@
  * bwtgap_gpu.c).  Not part of the public boundary (include/). */
 #ifndef BWTALN_GPU_H
 #define BWTALN_GPU_H
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "../../include/hsa_bwtaln.h"
 
 /* the device index of a loaded Idx2BWT (slot 0), attached on first use */
@@ -12,6 +15,29 @@ hsa_index_t *const *hsa_gpu_slots_of(const Idx2BWT *bi, int *n);
 void hsa_gpu_set_error_text(const char *msg);
 /* the reference's convention for unrecoverable errors: message + exit(1) */
 void hsa_gpu_fatal(const char *what, long rc) __attribute__((noreturn));
+/* A bump allocator for the per-batch splice tables: entries live until the table is
+ * cleared, so they come from 4 MiB blocks freed together. */
+typedef struct hsa_arena_blk { struct hsa_arena_blk *next; size_t used, cap; } hsa_arena_blk;
+typedef struct { hsa_arena_blk *head; } hsa_arena_t;
+static inline void *hsa_arena_alloc(hsa_arena_t *a, size_t n)
+{
+    n = (n + 15) & ~(size_t)15;
+    if (!a->head || a->head->used + n > a->head->cap) {
+        const size_t cap = n > ((size_t)4 << 20) ? n : ((size_t)4 << 20);
+        hsa_arena_blk *b = (hsa_arena_blk *)malloc(sizeof(hsa_arena_blk) + 16 + cap);
+        if (!b) { fprintf(stderr, "[hsa] out of host memory\n"); exit(1); }
+        b->next = a->head; b->used = 0; b->cap = cap;
+        a->head = b;
+    }
+    void *p = (char *)(a->head + 1) + 16 + a->head->used;
+    a->head->used += n;
+    return p;
+}
+static inline void hsa_arena_free(hsa_arena_t *a)
+{
+    while (a->head) { hsa_arena_blk *n = a->head->next; free(a->head); a->head = n; }
+}
+
 /* monotonic seconds (timing logs) */
 double hsa_now(void);
 /* aln_score (bwtgap.h) */

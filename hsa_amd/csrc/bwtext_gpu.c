@@ -47,8 +47,11 @@ typedef struct {
     int dir, len, max_pos;
     hsa_regime_t rg;
     int lo, n;
-    uint8_t *seq;                 /* window copies */
+    uint8_t *seq;                 /* window copies (in buf when owned == 0) */
     int32_t *bid;
+    int owned;                    /* seq / bid malloc'd by fill_req */
+    uint8_t *buf;                 /* the coroutine's window buffer, or NULL */
+    size_t buf_cap;
     bwt_aln1_t *aln;              /* the caller's, updated on resume */
     int *max_pos_io;
     int ret;
@@ -118,8 +121,16 @@ static void fill_req(ext_req_t *q, bwt_aux_t *aux, bwt_aln1_t *aln, int *max_pos
     const bwt_width_t *w = dir ? aux->width_back : aux->width_fore;
     /* the sequence is read only at [start - len, start - 1] / [end + 1, end + len] */
     const int s0 = dir ? aln->start - aux->len : aln->end + 1, s1 = dir ? aln->start - 1 : aln->end + aux->len;
-    q->seq = (uint8_t *)malloc((size_t)q->n + 1);
-    q->bid = (int32_t *)malloc(sizeof(int32_t) * ((size_t)q->n + 1));
+    const size_t need = 4 * ((size_t)q->n + 1) + (size_t)q->n + 1;
+    if (q->buf && need <= q->buf_cap) {
+        q->bid = (int32_t *)q->buf;
+        q->seq = q->buf + 4 * ((size_t)q->n + 1);
+        q->owned = 0;
+    } else {
+        q->seq = (uint8_t *)malloc((size_t)q->n + 1);
+        q->bid = (int32_t *)malloc(sizeof(int32_t) * ((size_t)q->n + 1));
+        q->owned = 1;
+    }
     for (int p = 0; p < q->n; ++p) {
         const int pos = q->lo + p;
         q->seq[p] = pos >= s0 && pos <= s1 ? seq[pos] : 4;
@@ -162,7 +173,7 @@ static void run_reqs(hsa_index_t *ix, ext_req_t *const *q, int n)
         memcpy(q[j]->aln, aln + 9 * (size_t)j, sizeof(bwt_aln1_t));
         *q[j]->max_pos_io = mp[j];
         q[j]->ret = ret[j];
-        free(q[j]->seq); free(q[j]->bid);
+        if (q[j]->owned) { free(q[j]->seq); free(q[j]->bid); }
         q[j]->seq = NULL; q[j]->bid = NULL;
     }
     free(rg); free(jobs); free(codes); free(bids); free(ret); free(mp); free(aln);
@@ -214,7 +225,7 @@ static int run_slices(hsa_index_t *ix, ext_req_t *const *q, const int32_t *slot,
             memcpy(q[j]->aln, aln + 9 * (size_t)j, sizeof(bwt_aln1_t));
             *q[j]->max_pos_io = mp[j];
             q[j]->ret = ret[j];
-            free(q[j]->seq); free(q[j]->bid);
+            if (q[j]->owned) { free(q[j]->seq); free(q[j]->bid); }
             q[j]->seq = NULL; q[j]->bid = NULL;
         }
         q[j]->started = 0;
@@ -237,6 +248,7 @@ static int extend(bwt_aux_t *aux, bwt_aln1_t *aln, int *max_pos, int dir)
         return me->req.ret;
     }
     ext_req_t q;                          /* a direct call: a batch of one */
+    memset(&q, 0, sizeof q);
     fill_req(&q, aux, aln, max_pos, dir, -1);
     ext_req_t *qp = &q;
     run_reqs(hsa_gpu_index_of(aux->bi_bwt), &qp, 1);
@@ -276,6 +288,7 @@ static wm_ent_t *g_wm;
 static size_t g_wm_cap, g_wm_n;
 static uint64_t g_wm_hits, g_wm_misses;
 static pthread_mutex_t g_wm_mu = PTHREAD_MUTEX_INITIALIZER;
+static hsa_arena_t g_wm_arena;          /* keys and widths of the entries */
 
 static size_t wkey(int type, int len, const ubyte_t *str, uint8_t *buf)
 {
@@ -316,17 +329,17 @@ static void wm_put(int type, int len, const ubyte_t *str, const uint32_t *w, int
         g_wm = t;
         g_wm_cap = cap;
     }
-    uint8_t *key = (uint8_t *)malloc((size_t)len + 5);
+    uint8_t *key = (uint8_t *)hsa_arena_alloc(&g_wm_arena, (size_t)len + 5);
     const size_t kl = wkey(type, len, str, key);
     const uint64_t h = key_hash(key, kl);
     size_t j = h & (g_wm_cap - 1);
     while (g_wm[j].h) {
-        if (g_wm[j].h == h && g_wm[j].key_len == kl && !memcmp(g_wm[j].key, key, kl)) { free(key); return; }
+        if (g_wm[j].h == h && g_wm[j].key_len == kl && !memcmp(g_wm[j].key, key, kl)) return;
         j = (j + 1) & (g_wm_cap - 1);
     }
     wm_ent_t *e = g_wm + j;
     e->h = h; e->key = key; e->key_len = kl; e->len = len; e->type = type; e->ret = ret;
-    e->w = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)len + 1));
+    e->w = (bwt_width_t *)hsa_arena_alloc(&g_wm_arena, sizeof(bwt_width_t) * ((size_t)len + 1));
     for (int i = 0; i <= len; ++i) { e->w[i].w = w[2 * i]; e->w[i].bid = (int)w[2 * i + 1]; }
     ++g_wm_n;
 }
@@ -334,8 +347,7 @@ static void wm_put(int type, int len, const ubyte_t *str, const uint32_t *w, int
 void hsa_splice_wmemo_clear(void)
 {
     pthread_mutex_lock(&g_wm_mu);
-    for (size_t i = 0; i < g_wm_cap; ++i)
-        if (g_wm[i].h) { free(g_wm[i].key); free(g_wm[i].w); }
+    hsa_arena_free(&g_wm_arena);
     free(g_wm);
     g_wm = NULL;
     g_wm_cap = g_wm_n = 0;
@@ -410,6 +422,8 @@ int hsa_splice_width_active(void)
 int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
 {
     if (n <= 0) return 0;
+    const double t_start = hsa_now();
+    double t_gpu = 0.0;
     hsa_index_t *ix = hsa_gpu_index_of(bi);
     for (int type = 1; type >= 0; --type) {
         const int per = type == 1 ? 4 : 1;
@@ -448,7 +462,9 @@ int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
             }
         }
         uint32_t *w = (uint32_t *)calloc(wo + 2, sizeof(uint32_t));
+        const double tg = hsa_now();
         widths_gpu(ix, type, (int)q, offs, lens, codes, co, w);
+        t_gpu += hsa_now() - tg;
         pthread_mutex_lock(&g_wm_mu);
         size_t o = 0;
         for (size_t j = 0; j < q; ++j) {
@@ -458,6 +474,8 @@ int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
         pthread_mutex_unlock(&g_wm_mu);
         free(offs); free(lens); free(src); free(codes); free(w);
     }
+    if (getenv("HSA_VERBOSE"))
+        fprintf(stderr, "[hsa] width prefetch: %.3f s (GPU %.3f s)\n", hsa_now() - t_start, t_gpu);
     return 0;
 }
 
@@ -525,6 +543,7 @@ static void sa_write(uint32_t occ, uint32_t sid, uint32_t ori, unsigned int *sid
 int hsa_splice_sa_prefetch(const Idx2BWT *bi, size_t n, const uint32_t *idx)
 {
     if (n == 0) return 0;
+    const double t_start = hsa_now();
     uint32_t *todo = (uint32_t *)malloc(sizeof(uint32_t) * n);
     size_t m = 0;
     pthread_mutex_lock(&g_sa_mu);
@@ -540,6 +559,8 @@ int hsa_splice_sa_prefetch(const Idx2BWT *bi, size_t n, const uint32_t *idx)
         free(o4);
     }
     free(todo);
+    if (getenv("HSA_VERBOSE"))
+        fprintf(stderr, "[hsa] SA prefetch: %zu indices, %zu looked up, %.3f s\n", n, m, hsa_now() - t_start);
     return 0;
 }
 
@@ -666,6 +687,8 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         c->aux.width_seed = (bwt_width_t *)calloc((size_t)max_len + 1, sizeof(bwt_width_t));
         c->aux.rc_seq = (ubyte_t *)calloc((size_t)max_len + 1, 1);
         c->aux.stack = stack_new(n_stacks);
+        c->req.buf_cap = 5 * ((size_t)max_len + 4);    /* the largest window: the read and both bounds */
+        c->req.buf = (uint8_t *)malloc(c->req.buf_cap);
         c->read = -1;
     }
     ext_req_t **pend = (ext_req_t **)malloc(sizeof(ext_req_t *) * (size_t)W);
@@ -740,6 +763,7 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         munmap(c->stack, CO_STACK);
         free(c->aux.width_back); free(c->aux.width_fore); free(c->aux.width_seed); free(c->aux.rc_seq);
         stack_free(c->aux.stack);
+        free(c->req.buf);
     }
     free(co); free(pend); free(pslot); free(pdone); free(sa_idx); free(sa_o4); free(sa_co);
     tl_sched = NULL;

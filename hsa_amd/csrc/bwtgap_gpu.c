@@ -156,6 +156,7 @@ static memo_ent_t *g_memo;
 static size_t g_memo_cap, g_memo_n;
 static uint64_t g_memo_hits, g_memo_misses;
 static pthread_mutex_t g_memo_mu = PTHREAD_MUTEX_INITIALIZER;
+static hsa_arena_t g_memo_arena;        /* keys, hits and widths of the entries */
 
 static size_t key_of(const bwt_aux_t *a, uint8_t *buf)
 {
@@ -193,8 +194,7 @@ static uint64_t key_hash(const uint8_t *p, size_t n)
 void hsa_splice_memo_clear(void)
 {
     pthread_mutex_lock(&g_memo_mu);
-    for (size_t i = 0; i < g_memo_cap; ++i)
-        if (g_memo[i].h) { free(g_memo[i].key); free(g_memo[i].hits); free(g_memo[i].wout); }
+    hsa_arena_free(&g_memo_arena);
     free(g_memo);
     g_memo = NULL;
     g_memo_cap = g_memo_n = 0;
@@ -217,19 +217,19 @@ static void memo_put(const bwt_aux_t *in, const bwt_width_t *wout, const bwt_aln
         g_memo_cap = cap;
     }
     const size_t kl = key_of(in, NULL);
-    uint8_t *key = (uint8_t *)malloc(kl);
+    uint8_t *key = (uint8_t *)hsa_arena_alloc(&g_memo_arena, kl);
     key_of(in, key);
     const uint64_t h = key_hash(key, kl);
     size_t j = h & (g_memo_cap - 1);
     while (g_memo[j].h) {
-        if (g_memo[j].h == h && g_memo[j].key_len == kl && !memcmp(g_memo[j].key, key, kl)) { free(key); return; }
+        if (g_memo[j].h == h && g_memo[j].key_len == kl && !memcmp(g_memo[j].key, key, kl)) return;
         j = (j + 1) & (g_memo_cap - 1);
     }
     memo_ent_t *e = g_memo + j;
     e->h = h; e->key = key; e->key_len = kl; e->n_aln = n_aln; e->len = in->len;
-    e->hits = (bwt_aln1_t *)malloc(sizeof(bwt_aln1_t) * (size_t)(n_aln > 0 ? n_aln : 1));
+    e->hits = (bwt_aln1_t *)hsa_arena_alloc(&g_memo_arena, sizeof(bwt_aln1_t) * (size_t)(n_aln > 0 ? n_aln : 1));
     if (n_aln > 0) memcpy(e->hits, hits, sizeof(bwt_aln1_t) * (size_t)n_aln);
-    e->wout = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)in->len + 1));
+    e->wout = (bwt_width_t *)hsa_arena_alloc(&g_memo_arena, sizeof(bwt_width_t) * ((size_t)in->len + 1));
     memcpy(e->wout, wout, sizeof(bwt_width_t) * ((size_t)in->len + 1));
     ++g_memo_n;
 }
@@ -283,13 +283,18 @@ size_t hsa_splice_take_sa_list(uint32_t **idx)
  * table, keyed by the call's inputs: win[i] holds its width_back as it was before the
  * search (calls[i].width_back is a scratch copy the search rewrites; a width_seed
  * aliased to it is re-aliased to win[i]).  n_out[i] receives the hit counts. */
+static double g_t_search, g_t_put;   /* prefetch timing (HSA_VERBOSE) */
+
 static void batch_into_memo(bwt_aux_t *calls, int c, bwt_width_t **win, int *n_out)
 {
     if (c <= 0) return;
     bwt_aux_t **cp = (bwt_aux_t **)calloc((size_t)c, sizeof(bwt_aux_t *));
     bwt_aln1_t **out = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)c);
     for (int i = 0; i < c; ++i) cp[i] = calls + i;
+    const double t0 = hsa_now();
     bwt_match_gap_batch(cp, c, out, n_out);
+    const double t1 = hsa_now();
+    g_t_search += t1 - t0;
     pthread_mutex_lock(&g_memo_mu);
     for (int i = 0; i < c; ++i) {
         bwt_width_t *after = calls[i].width_back;
@@ -301,6 +306,7 @@ static void batch_into_memo(bwt_aux_t *calls, int c, bwt_width_t **win, int *n_o
         free(after); free(out[i]);
     }
     pthread_mutex_unlock(&g_memo_mu);
+    g_t_put += hsa_now() - t1;
     free(cp); free(out);
 }
 
@@ -345,6 +351,8 @@ static bwt_aux_t *add_call(bwt_aux_t *calls, gap_opt_t *opts, bwt_width_t **win,
 int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
 {
     if (n <= 0) return 0;
+    const double t_start = hsa_now();
+    g_t_search = g_t_put = 0.0;
     hsa_index_t *ix = hsa_gpu_index_of(bi);
     /* widths: per read, strand s, the prefix of seed_len and of seed_len + len % 3 */
     int nw = 0;
@@ -476,6 +484,9 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
     for (int i = 0; i < c; ++i) free(win[i]);
     free(offs); free(lens); free(woff); free(codes); free(wout);
     free(calls); free(opts); free(win); free(n_out);
+    if (getenv("HSA_VERBOSE"))
+        fprintf(stderr, "[hsa] seed/anchor prefetch: %.3f s (GPU searches %.3f s, table %.3f s, the rest: set-up and "
+                        "widths)\n", hsa_now() - t_start, g_t_search, g_t_put);
     return 0;
 }
 
