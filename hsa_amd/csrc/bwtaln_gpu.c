@@ -94,18 +94,36 @@ typedef struct { int opt_max_diff, opt_seed, loc_max_diff, loc_seed; } optstate_
 
 enum { K_JOB = 0, K_NFILTER = 1, K_POLYAT = 2 };
 
+/* What the prologue's filters read of a read (bwtaln.c:314-325), computed once per
+ * read: its count of codes > 3 (N), and whether its first 15 codes are all 0 or all 3. */
+typedef struct { int32_t n_n; int8_t polyat; } readinfo_t;
+
+static readinfo_t read_info(const uint8_t *seq, int len)
+{
+    readinfo_t ri = {0, 0};
+    int j = 0;
+    /* 8 codes at a time: a code is > 3 iff one of its bits 2..7 is set */
+    for (; j + 8 <= len; j += 8) {
+        uint64_t w;
+        memcpy(&w, seq + j, 8);
+        const uint64_t t = (w >> 2) & 0x3F3F3F3F3F3F3F3Full;
+        ri.n_n += __builtin_popcountll(((t + 0x7F7F7F7F7F7F7F7Full) | t) & 0x8080808080808080ull);
+    }
+    for (; j < len; ++j) ri.n_n += seq[j] > 3;
+    if (len >= 15) {
+        int a = 1, t = 1;
+        for (int k = 0; k < 15; ++k) { a &= seq[k] == 0; t &= seq[k] == 3; }
+        ri.polyat = (int8_t)(a || t);
+    }
+    return ri;
+}
+
 /* One read of the bwtaln.c:303-337 prologue under regime `cur` (0 = A, 1 = B). */
-static int plan_read(const gap_opt_t *caller, int cur, optstate_t *st, const uint8_t *seq, int len,
+static int plan_read(const gap_opt_t *caller, int cur, optstate_t *st, const readinfo_t *ri, int len,
                      int32_t *max_diff, int32_t *seed_len)
 {
-    int nN = 0;
-    for (int j = 0; j < len; ++j) nN += seq[j] > 3;
-    if (nN > st->loc_max_diff) return K_NFILTER;                      /* :314-317 */
-    if (len >= 15) {                                                    /* :324-325 */
-        int a = 1, t = 1;
-        for (int j = 0; j < 15; ++j) { a &= seq[j] == 0; t &= seq[j] == 3; }
-        if (a || t) return K_POLYAT;
-    }
+    if (ri->n_n > st->loc_max_diff) return K_NFILTER;                  /* :314-317 */
+    if (ri->polyat) return K_POLYAT;                                    /* :324-325 */
     int *md = cur ? &st->loc_max_diff : &st->opt_max_diff;
     int *sl = cur ? &st->loc_seed : &st->opt_seed;
     if (caller->fnr > 0.0) *md = cal_maxdiff(len, BWA_AVG_ERR, caller->fnr);   /* :330-331 */
@@ -257,6 +275,8 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
     const int equivalent = same_len && memcmp(&rg[0], &rg[1], sizeof rg[0]) == 0;
 
     int8_t *kind = (int8_t *)malloc((size_t)n + 1);
+    readinfo_t *ri = (readinfo_t *)malloc(sizeof(readinfo_t) * ((size_t)n + 1));
+    for (int r = 0; r < n; ++r) ri[r] = read_info(codes + offs[r], (int)lens[r]);
     int32_t *jmd = (int32_t *)malloc(sizeof(int32_t) * ((size_t)n + 1));
     int32_t *jsl = (int32_t *)malloc(sizeof(int32_t) * ((size_t)n + 1));
     hitbuf_t hb = {NULL, 0, 0};
@@ -271,7 +291,7 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
             const int end = equivalent ? n : (pos + chunk < n ? pos + chunk : n);
             const optstate_t saved = st;
             for (int r = pos; r < end; ++r)
-                kind[r] = (int8_t)plan_read(opt, 0, &st, codes + offs[r], (int)lens[r], &jmd[r], &jsl[r]);
+                kind[r] = (int8_t)plan_read(opt, 0, &st, ri + r, (int)lens[r], &jmd[r], &jsl[r]);
             rc = search_range(ixs, n_ix, rg, pos, end, kind, jmd, jsl, 0, lens, offs, codes, codes_len, n_aln, flags,
                               hit_off, &hb, stats);
             if (rc) break;
@@ -283,13 +303,13 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
             /* regime switch after read f: reads (f, end) are searched again in regime B */
             st = saved;
             for (int r = pos; r <= f; ++r)
-                kind[r] = (int8_t)plan_read(opt, 0, &st, codes + offs[r], (int)lens[r], &jmd[r], &jsl[r]);
+                kind[r] = (int8_t)plan_read(opt, 0, &st, ri + r, (int)lens[r], &jmd[r], &jsl[r]);
             for (int r = f + 1; r < end; ++r) { n_aln[r] = 0; flags[r] = 0; hit_off[r] = 0; }
             cur = 1;
             pos = f + 1;
         } else {
             for (int r = pos; r < n; ++r)
-                kind[r] = (int8_t)plan_read(opt, 1, &st, codes + offs[r], (int)lens[r], &jmd[r], &jsl[r]);
+                kind[r] = (int8_t)plan_read(opt, 1, &st, ri + r, (int)lens[r], &jmd[r], &jsl[r]);
             rc = search_range(ixs, n_ix, rg, pos, n, kind, jmd, jsl, 1, lens, offs, codes, codes_len, n_aln, flags,
                               hit_off, &hb, stats);
             pos = n;
@@ -302,7 +322,7 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
         int c = 0;
         for (int r = 0; r < n; ++r) {
             int32_t a, b;
-            const int k = plan_read(opt, c, &s, codes + offs[r], (int)lens[r], &a, &b);
+            const int k = plan_read(opt, c, &s, ri + r, (int)lens[r], &a, &b);
             if (k == K_NFILTER) flags[r] = HSA_RF_NFILTER;
             else if (k == K_POLYAT) flags[r] = HSA_RF_POLYAT;
             if (splice_opt) { splice_opt[2 * r] = s.loc_max_diff; splice_opt[2 * r + 1] = s.loc_seed; }
@@ -314,7 +334,7 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
     } else {
         free(hb.h);
     }
-    free(kind); free(jmd); free(jsl);
+    free(kind); free(jmd); free(jsl); free(ri);
     return rc ? rc : (long)hb.n;
 }
 
