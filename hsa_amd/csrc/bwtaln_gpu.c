@@ -118,6 +118,33 @@ static readinfo_t read_info(const uint8_t *seq, int len)
     return ri;
 }
 
+/* read_info of reads [r0, r1), a host thread's share */
+typedef struct { const uint8_t *codes; const uint64_t *offs; const uint32_t *lens; readinfo_t *ri; int r0, r1; } ri_part_t;
+
+static void *ri_run(void *arg)
+{
+    ri_part_t *p = (ri_part_t *)arg;
+    for (int r = p->r0; r < p->r1; ++r) p->ri[r] = read_info(p->codes + p->offs[r], (int)p->lens[r]);
+    return NULL;
+}
+
+/* read_info of every read, on up to 8 host threads for large calls */
+static void read_infos(const uint8_t *codes, const uint64_t *offs, const uint32_t *lens, int n, readinfo_t *ri)
+{
+    enum { MAXT = 8 };
+    const int nt = n >= (1 << 16) ? MAXT : 1;
+    ri_part_t part[MAXT];
+    pthread_t th[MAXT];
+    int started[MAXT] = {0};
+    for (int k = 0; k < nt; ++k) {
+        part[k] = (ri_part_t){codes, offs, lens, ri, (int)((long)n * k / nt), (int)((long)n * (k + 1) / nt)};
+        if (k > 0) started[k] = pthread_create(&th[k], NULL, ri_run, &part[k]) == 0;
+        if (k > 0 && !started[k]) ri_run(&part[k]);
+    }
+    ri_run(&part[0]);
+    for (int k = 1; k < nt; ++k) if (started[k]) pthread_join(th[k], NULL);
+}
+
 /* One read of the bwtaln.c:303-337 prologue under regime `cur` (0 = A, 1 = B). */
 static int plan_read(const gap_opt_t *caller, int cur, optstate_t *st, const readinfo_t *ri, int len,
                      int32_t *max_diff, int32_t *seed_len)
@@ -227,7 +254,10 @@ static int search_range(hsa_index_t *const *ixs, int n_ix, const hsa_regime_t *r
     for (int k = 0; k < n_ix && rc == 0; ++k) {
         slot_part_t *p = &part[k];
         const size_t base = hb->n;
-        if (hb_append(hb, p->hits, (size_t)p->tot)) { rc = HSA_E_MEM; break; }
+        if (hb->n == 0 && !hb->h && n_ix == 1) {       /* the first part's hits: take the array itself */
+            hb->h = p->hits; hb->n = hb->cap = (size_t)p->tot;
+            p->hits = NULL;
+        } else if (hb_append(hb, p->hits, (size_t)p->tot)) { rc = HSA_E_MEM; break; }
         for (int j = 0; j < p->n; ++j) {
             const int r = map[(p->jobs - jobs) + j];
             n_aln[r] = p->na[j]; flags[r] = p->fl[j]; hit_off[r] = p->ho[j] + base;
@@ -275,8 +305,11 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
     const int equivalent = same_len && memcmp(&rg[0], &rg[1], sizeof rg[0]) == 0;
 
     int8_t *kind = (int8_t *)malloc((size_t)n + 1);
+    const double tm0 = hsa_now();
     readinfo_t *ri = (readinfo_t *)malloc(sizeof(readinfo_t) * ((size_t)n + 1));
-    for (int r = 0; r < n; ++r) ri[r] = read_info(codes + offs[r], (int)lens[r]);
+    read_infos(codes, offs, lens, n, ri);
+    const double tm1 = hsa_now();
+    double tm_search = 0.0;
     int32_t *jmd = (int32_t *)malloc(sizeof(int32_t) * ((size_t)n + 1));
     int32_t *jsl = (int32_t *)malloc(sizeof(int32_t) * ((size_t)n + 1));
     hitbuf_t hb = {NULL, 0, 0};
@@ -292,8 +325,10 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
             const optstate_t saved = st;
             for (int r = pos; r < end; ++r)
                 kind[r] = (int8_t)plan_read(opt, 0, &st, ri + r, (int)lens[r], &jmd[r], &jsl[r]);
+            const double ts = hsa_now();
             rc = search_range(ixs, n_ix, rg, pos, end, kind, jmd, jsl, 0, lens, offs, codes, codes_len, n_aln, flags,
                               hit_off, &hb, stats);
+            tm_search += hsa_now() - ts;
             if (rc) break;
             int f = -1;
             for (int r = pos; r < end; ++r)
@@ -331,6 +366,10 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
         opt->max_diff = s.opt_max_diff;
         opt->seed_len = s.opt_seed;
         *hits = hb.h ? hb.h : (uint32_t *)calloc(9, 4);
+        if (getenv("HSA_VERBOSE"))
+            fprintf(stderr, "[hsa] cal_sa_reg_gap of %d reads: filters %.1f ms, searches %.1f ms (kernels %.1f ms), "
+                            "total %.1f ms\n", n, 1e3 * (tm1 - tm0), 1e3 * tm_search, stats ? stats->kernel_ms : -1.0,
+                    1e3 * (hsa_now() - tm0));
     } else {
         free(hb.h);
     }

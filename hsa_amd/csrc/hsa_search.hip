@@ -171,6 +171,9 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     hipStream_t st = ix->stream;
     if (stats) memset(stats, 0, sizeof *stats);
     if (n_jobs == 0) { *hits_out = (uint32_t *)calloc(9, 4); return 0; }
+    static const bool verbose = getenv("HSA_VERBOSE") != nullptr;
+    const auto now = []() { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + 1e-9 * t.tv_nsec; };
+    const double tv0 = verbose ? now() : 0.0;
 
     // device staging: regimes+bmap | jobs | list | codes [| mg jobs | caller widths]
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
@@ -227,8 +230,12 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     float ms = 0;
     HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
     uint64_t total = ctr[1] < hit_cap ? ctr[1] : hit_cap;
+    const double tv1 = verbose ? now() : 0.0;
     uint32_t *h = (uint32_t *)malloc((total + 1) * 36);
     if (total) HSA_HIP(hipMemcpy(h, d_hits, total * 36, hipMemcpyDeviceToHost));
+    if (verbose)
+        fprintf(stderr, "[hsa] search of %d reads: copies in + kernels + result arrays out %.1f ms (kernels %.1f ms), "
+                        "hits out %.1f ms\n", n_jobs, 1e3 * (tv1 - tv0), ms, 1e3 * (now() - tv1));
     if (stats) {
         stats->rank_queries += ctr[2]; stats->blocks_loaded += ctr[3]; stats->pops += ctr[4];
         stats->kernel_ms += ms; stats->main_kernel_ms += ms; stats->main_launches += 1;
