@@ -216,6 +216,29 @@ static int search_range(hsa_index_t *const *ixs, int n_ix, const hsa_regime_t *r
     int n = 0;
     for (int r = r0; r < r1; ++r) n += kind[r] == K_JOB;
     if (n == 0) return 0;
+    if (n == r1 - r0 && n_ix == 1 && hb->n == 0 && !hb->h) {
+        /* every read is a job, one slot, no hits yet: the search writes the outputs in place */
+        hsa_job_t *jobs = (hsa_job_t *)malloc(sizeof(hsa_job_t) * (size_t)n);
+        for (int q = 0; q < n; ++q) {
+            const int r = r0 + q;
+            jobs[q].off = offs[r] - offs[r0]; jobs[q].len = lens[r]; jobs[q].max_diff = jmd[r]; jobs[q].seed_len = jsl[r];
+            jobs[q].regime = 0;
+        }
+        const uint64_t c1 = offs[r1 - 1] + lens[r1 - 1];
+        hsa_stats_t st;
+        uint32_t *h = NULL;
+        const long tot = hsa_search_batch(ixs[0], rg + regime, 1, jobs, n, codes + offs[r0], (size_t)(c1 - offs[r0]),
+                                          n_aln + r0, flags + r0, hit_off + r0, &h, &st);
+        free(jobs);
+        if (tot < 0) return (int)tot;
+        hb->h = h; hb->n = hb->cap = (size_t)tot;
+        if (stats) {
+            stats->rank_queries += st.rank_queries; stats->blocks_loaded += st.blocks_loaded; stats->pops += st.pops;
+            stats->overflow_reruns += st.overflow_reruns; stats->kernel_ms += st.kernel_ms;
+            stats->main_kernel_ms += st.main_kernel_ms; stats->main_launches += st.main_launches;
+        }
+        return 0;
+    }
     hsa_job_t *jobs = (hsa_job_t *)malloc(sizeof(hsa_job_t) * n);
     int *map = (int *)malloc(sizeof(int) * n);
     int32_t *na = (int32_t *)malloc(sizeof(int32_t) * n);
