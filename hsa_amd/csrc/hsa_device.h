@@ -121,38 +121,65 @@ __device__ __forceinline__ uint32_t hsa_occ1_pair(const RankDir d, uint32_t p1, 
 // ---------------------------------------------------------------- 64-bit texts
 // Texts of 2^32 characters or more (config 5; the reference's bwtint_t is 32-bit,
 // 2BWT-Interface.h:26).  The blocks are the same 16-byte blocks, their counts kept
-// modulo 2^32; a superblock table holds the exact 64-bit Occ(A), Occ(C), Occ(G) at
-// every 2^24-character boundary (4 x u64 per entry, the 4th unused).  Counts inside
-// one superblock differ by less than 2^24, so Occ = sup + (u32)(block - (u32)sup).
-#define HSA_SUPER_SHIFT 24u
+// modulo 2^32.  The high words come from the wrap table: a wrap of base c is the
+// first block whose count of c reaches a multiple of 2^32 (there the block's low word
+// drops below its predecessor's, since counts grow by <= 16 per block), so
+//   Occ(16 b, c) = (wraps of c at blocks <= b) 2^32 + block b's low word.
+// A text of i.i.d. bases passes 2^32 of one base only past ~17 Gbp, and a text under
+// 2^36 characters has at most 15 wraps per base (HSA_MAX_WRAPS).  The table is the
+// HSA_WRAP_HEAD bytes in front of block 0, read only when the index has a wrap at all
+// (`any`, a uniform branch): an index without one pays nothing over the 32-bit rank,
+// where a superblock table cost a cached load per rank query.
+#define HSA_MAX_WRAPS 15u
+#define HSA_WIDE_MAX_T (1ull << 36)
+#define HSA_WRAP_HEAD 512u               // bytes allocated in front of every block array
 
 struct RankDir64 {
     const uint4 *blk;
-    const uint64_t *sup;
     uint64_t isa0;
+    uint32_t any;                        // the index has a wrap
 };
 
-__device__ __forceinline__ void hsa_occ4_q64(const uint4 q, const uint64_t *__restrict__ sup, uint64_t p,
-                                             uint64_t o[4])
+// the wrap table in front of block 0: [0] = the number of wraps, then (block, base) pairs by
+// block from word 2
+__device__ __host__ __forceinline__ const uint32_t *hsa_wrap_table(const uint4 *blk)
 {
-    const uint64_t *s = sup + (p >> HSA_SUPER_SHIFT) * 4u;
-    const uint64_t sa = s[0], sc = s[1], sg = s[2];
+    return reinterpret_cast<const uint32_t *>(blk) - HSA_WRAP_HEAD / 4;
+}
+
+__device__ __forceinline__ void hsa_hi64(const uint32_t *__restrict__ wrap, uint32_t b, uint64_t o[3])
+{
+    // one loop over all wraps (<= 45), by block: entry j = (block, base) at [2j + 2]
+    const uint32_t n = wrap[0];
+#pragma unroll 1
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint2 e = reinterpret_cast<const uint2 *>(wrap)[j + 1];
+        if (b < e.x) break;
+        const uint32_t c = e.y;
+        o[0] += c == 0 ? 0x100000000ull : 0ull;
+        o[1] += c == 1 ? 0x100000000ull : 0ull;
+        o[2] += c == 2 ? 0x100000000ull : 0ull;
+    }
+}
+
+__device__ __forceinline__ void hsa_occ4_q64(const uint4 q, const RankDir64 &d, uint64_t p, uint64_t o[4])
+{
     const uint32_t r = (uint32_t)p & 15u;
     const uint32_t v = q.w & ((1u << (2u * r)) - 1u);
     const uint32_t lo = v & 0x55555555u, hi = (v >> 1) & 0x55555555u;
     const uint32_t n3 = __popc(lo & hi);
     const uint32_t n1 = __popc(lo) - n3, n2 = __popc(hi) - n3;
-    o[0] = sa + (uint32_t)(q.x - (uint32_t)sa) + (r - n1 - n2 - n3);
-    o[1] = sc + (uint32_t)(q.y - (uint32_t)sc) + n1;
-    o[2] = sg + (uint32_t)(q.z - (uint32_t)sg) + n2;
+    o[0] = (uint64_t)q.x + (r - n1 - n2 - n3);
+    o[1] = (uint64_t)q.y + n1;
+    o[2] = (uint64_t)q.z + n2;
+    if (d.any) hsa_hi64(hsa_wrap_table(d.blk), (uint32_t)(p >> 4), o);   // uniform: no wraps, no work
     o[3] = p - o[0] - o[1] - o[2];
 }
 
-__device__ __forceinline__ uint64_t hsa_occ1_q64(const uint4 q, const uint64_t *__restrict__ sup, uint64_t p,
-                                                 uint32_t c)
+__device__ __forceinline__ uint64_t hsa_occ1_q64(const uint4 q, const RankDir64 &d, uint64_t p, uint32_t c)
 {
     uint64_t o[4];
-    hsa_occ4_q64(q, sup, p, o);
+    hsa_occ4_q64(q, d, p, o);
     return c == 0 ? o[0] : c == 1 ? o[1] : c == 2 ? o[2] : o[3];
 }
 
@@ -180,8 +207,8 @@ __device__ __forceinline__ uint32_t occ_pair(const RankDir64 &d, uint64_t p1, ui
     uint4 q2r = make_uint4(0, 0, 0, 0);
     if (two) q2r = d.blk[b2];
     const uint4 q2 = two ? q2r : q1;
-    hsa_occ4_q64(q1, d.sup, p1, a);
-    hsa_occ4_q64(q2, d.sup, p2, b);
+    hsa_occ4_q64(q1, d, p1, a);
+    hsa_occ4_q64(q2, d, p2, b);
     return 1u + ((p1 >> 6) != (p2 >> 6));
 }
 
@@ -196,7 +223,7 @@ __device__ __forceinline__ uint32_t occ1_pair(const RankDir64 &d, uint64_t p1, u
     uint4 q2r = make_uint4(0, 0, 0, 0);
     if (two) q2r = d.blk[b2];
     const uint4 q2 = two ? q2r : q1;
-    a = hsa_occ1_q64(q1, d.sup, p1, c);
-    b = hsa_occ1_q64(q2, d.sup, p2, c);
+    a = hsa_occ1_q64(q1, d, p1, c);
+    b = hsa_occ1_q64(q2, d, p2, c);
     return 1u + ((p1 >> 6) != (p2 >> 6));
 }

@@ -141,8 +141,8 @@ struct WordCounts {
 };
 
 // block b = (Occ A, C, G over [0, 16b) from the scan, code word b).  The scan's u32
-// sums wrap past 2^32 characters: the counts are then kept modulo 2^32 and the
-// superblock table (build_super) supplies the high part.
+// sums wrap past 2^32 characters: the counts are then kept modulo 2^32 and the wrap
+// table (build_wraps) supplies the high part.
 __global__ void k_block_codes(const uint32_t *__restrict__ code, size_t nwords, size_t nblk, uint4 *__restrict__ blk)
 {
     const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -156,7 +156,9 @@ static int build_blocks(hsa_index *ix, int dir, uint64_t T, const uint32_t *d_co
     const size_t nblk = (size_t)T / HSA_BLK_CHARS + 2;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
-    HSA_HIP(hipMalloc(&ix->blk[dir], nblk * 16));
+    HSA_HIP(hipMalloc(&ix->blk_base[dir], nblk * 16 + HSA_WRAP_HEAD));
+    HSA_HIP(hipMemset(ix->blk_base[dir], 0, HSA_WRAP_HEAD));       // no wraps
+    ix->blk[dir] = reinterpret_cast<uint4 *>(static_cast<char *>(ix->blk_base[dir]) + HSA_WRAP_HEAD);
     ix->nblk[dir] = nblk;
     auto in = rocprim::make_transform_iterator(rocprim::make_counting_iterator<size_t>(0),
                                                WordCounts{d_code_lsb, nwords, T});
@@ -172,50 +174,61 @@ static int build_blocks(hsa_index *ix, int dir, uint64_t T, const uint32_t *d_co
     return 0;
 }
 
-// Superblock s (characters [s 2^24, (s+1) 2^24)): its A, C, G counts, one workgroup
-// per superblock; the host turns them into exact u64 prefix counts.
-__global__ void __launch_bounds__(256) k_super_counts(WordCounts wc, uint64_t words_per_sup, unsigned long long *out)
+// The wrap table of RankDir64: block b > 0 is a wrap of base c when its low count word
+// is below block b - 1's (counts grow by <= 16 per block).  At most HSA_MAX_WRAPS per
+// base under HSA_WIDE_MAX_T characters; the slots fill in any order and are sorted on
+// the host.
+__global__ void k_find_wraps(const uint4 *__restrict__ blk, size_t nblk, unsigned *cnt, unsigned *out)
 {
-    __shared__ unsigned long long red[3][256];
-    const uint64_t s = blockIdx.x;
-    unsigned long long a = 0, c = 0, g = 0;
-    for (uint64_t w = s * words_per_sup + threadIdx.x; w < (s + 1) * words_per_sup && w < wc.nwords; w += 256) {
-        const U4 v = wc(w);
-        a += v.a; c += v.b; g += v.c;
-    }
-    red[0][threadIdx.x] = a; red[1][threadIdx.x] = c; red[2][threadIdx.x] = g;
-    __syncthreads();
-    for (int h = 128; h > 0; h >>= 1) {
-        if ((int)threadIdx.x < h)
-            for (int j = 0; j < 3; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + h];
-        __syncthreads();
-    }
-    if (threadIdx.x < 3) out[s * 3 + threadIdx.x] = red[threadIdx.x][0];
+    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b == 0 || b >= nblk) return;
+    const uint4 x = blk[b - 1], y = blk[b];
+    const uint32_t lo[3][2] = {{x.x, y.x}, {x.y, y.y}, {x.z, y.z}};
+    for (int c = 0; c < 3; ++c)
+        if (lo[c][1] < lo[c][0]) {
+            const unsigned k = atomicAdd(&cnt[c], 1u);
+            if (k < HSA_MAX_WRAPS) out[c * HSA_MAX_WRAPS + k] = (unsigned)b;
+        }
 }
 
-// sup[s] = exact (Occ A, C, G, 0) at character s 2^24, s = 0 .. T >> 24 (RankDir64)
-static int build_super(hsa_index *ix, int dir, uint64_t T, const uint32_t *d_code_lsb, hipStream_t st)
+static int build_wraps(hsa_index *ix, int dir, hipStream_t st)
 {
-    const uint64_t nwords = (T + 15) / 16, wps = (uint64_t)1 << (HSA_SUPER_SHIFT - 4);
-    const size_t nsup = (size_t)(T >> HSA_SUPER_SHIFT) + 2;
-    unsigned long long *d_cnt = nullptr;
-    HSA_HIP(hipMalloc(&d_cnt, nsup * 3 * sizeof(unsigned long long)));
-    HSA_HIP(hipMemsetAsync(d_cnt, 0, nsup * 3 * sizeof(unsigned long long), st));
-    k_super_counts<<<(unsigned)nsup, 256, 0, st>>>(WordCounts{d_code_lsb, (size_t)nwords, T}, wps, d_cnt);
-    HSA_HIP(hipGetLastError());
-    unsigned long long *cnt = (unsigned long long *)malloc(nsup * 3 * sizeof(unsigned long long));
-    uint64_t *sup = (uint64_t *)calloc(nsup * 4, sizeof(uint64_t));
-    if (!cnt || !sup) { free(cnt); free(sup); (void)hipFree(d_cnt); hsa_set_error("host allocation"); return HSA_E_MEM; }
-    HSA_HIP(hipMemcpyAsync(cnt, d_cnt, nsup * 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-    HSA_HIP(hipStreamSynchronize(st));
-    for (size_t s = 1; s < nsup; ++s)
-        for (int j = 0; j < 3; ++j) sup[s * 4 + j] = sup[(s - 1) * 4 + j] + cnt[(s - 1) * 3 + j];
-    int rc = 0;
-    if (hipMalloc(&ix->sup[dir], nsup * 32) != hipSuccess) { hsa_set_error("hipMalloc(sup)"); rc = HSA_E_MEM; }
-    else if (hipMemcpy(ix->sup[dir], sup, nsup * 32, hipMemcpyHostToDevice) != hipSuccess) { hsa_set_error("sup copy"); rc = HSA_E_HIP; }
-    ix->nsup[dir] = nsup;
-    free(cnt); free(sup); (void)hipFree(d_cnt);
-    return rc;
+    unsigned *d = nullptr;
+    const size_t words = 3 + 3 * HSA_MAX_WRAPS;
+    HSA_HIP(hipMalloc(&d, words * 4));
+    HSA_HIP(hipMemsetAsync(d, 0, words * 4, st));
+    const size_t nblk = ix->nblk[dir];
+    k_find_wraps<<<(unsigned)((nblk + 255) / 256), 256, 0, st>>>(ix->blk[dir], nblk, d, d + 3);
+    unsigned h[3 + 3 * HSA_MAX_WRAPS];
+    const hipError_t e1 = hipGetLastError();
+    const hipError_t e2 = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, st);
+    const hipError_t e3 = hipStreamSynchronize(st);
+    (void)hipFree(d);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) { hsa_set_error("wrap table"); return HSA_E_HIP; }
+    uint32_t tab[HSA_WRAP_HEAD / 4] = {};
+    uint32_t n = 0;
+    for (uint32_t c = 0; c < 3; ++c) {
+        if (h[c] > HSA_MAX_WRAPS) { hsa_set_error("more than %u count wraps", HSA_MAX_WRAPS); return HSA_E_ARG; }
+        for (uint32_t k = 0; k < h[c]; ++k, ++n) {
+            tab[2 + 2 * n] = h[3 + c * HSA_MAX_WRAPS + k];
+            tab[3 + 2 * n] = c;
+        }
+    }
+    for (uint32_t i = 1; i < n; ++i)                 // insertion sort by block, <= 45 entries
+        for (uint32_t j = i; j > 0 && tab[2 + 2 * j] < tab[2 * j]; --j) {
+            uint32_t *x = tab + 2 + 2 * j, *y = tab + 2 * j;
+            const uint32_t t0 = x[0], t1 = x[1];
+            x[0] = y[0]; x[1] = y[1]; y[0] = t0; y[1] = t1;
+        }
+    tab[0] = n;
+    ix->any_wrap[dir] = n > 0;
+    HSA_HIP(hipMemcpy((void *)hsa_wrap_table(ix->blk[dir]), tab, sizeof tab, hipMemcpyHostToDevice));
+    return 0;
+}
+
+RankDir64 hsa_rank_dir64(const hsa_index *ix, int dir)
+{
+    return RankDir64{ix->blk[dir], dir ? ix->risa0_64 : ix->isa0_64, ix->any_wrap[dir] ? 1u : 0u};
 }
 
 int hsa_need32(const hsa_index *ix)
@@ -276,11 +289,11 @@ extern "C" int hsa_index_create_device64(int device, uint64_t T, uint64_t isa0, 
         hsa_set_error("inconsistent lengths (C[4] must equal T, isa0 <= T)");
         return HSA_E_ARG;
     }
-    if ((T >> 4) + 2 >= (1ull << 40)) { hsa_set_error("text too long"); return HSA_E_ARG; }
+    if (T >= HSA_WIDE_MAX_T || rT >= HSA_WIDE_MAX_T) { hsa_set_error("text of 2^36 characters or more"); return HSA_E_ARG; }
     hsa_index *ix = nullptr;
     int rc = index_init(device, &ix);
     if (rc) return rc;
-    ix->has_sup = true;
+    ix->wide = true;
     ix->is64 = T > 0xFFFFFFFFull - 1 || rT > 0xFFFFFFFFull - 1;
     ix->T64 = T; ix->isa0_64 = isa0; memcpy(ix->C64, C, sizeof ix->C64);
     ix->rT64 = rT; ix->risa0_64 = risa0; memcpy(ix->rC64, rC, sizeof ix->rC64);
@@ -289,7 +302,7 @@ extern "C" int hsa_index_create_device64(int device, uint64_t T, uint64_t isa0, 
         for (int c = 0; c < 5; ++c) { ix->C[c] = (uint32_t)C[c]; ix->rC[c] = (uint32_t)rC[c]; }
     }
     if ((rc = build_blocks(ix, 0, T, d_code_lsb, ix->stream)) || (rc = build_blocks(ix, 1, rT, d_rcode_lsb, ix->stream)) ||
-        (rc = build_super(ix, 0, T, d_code_lsb, ix->stream)) || (rc = build_super(ix, 1, rT, d_rcode_lsb, ix->stream))) {
+        (rc = build_wraps(ix, 0, ix->stream)) || (rc = build_wraps(ix, 1, ix->stream))) {
         hsa_index_free(ix);
         return rc;
     }
@@ -325,8 +338,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
 {
     if (!ix) return;
     (void)hipSetDevice(ix->device);
-    (void)hipFree(ix->blk[0]); (void)hipFree(ix->blk[1]);
-    (void)hipFree(ix->sup[0]); (void)hipFree(ix->sup[1]);
+    (void)hipFree(ix->blk_base[0]); (void)hipFree(ix->blk_base[1]);
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big); hsa_scratch_free(ix->huge);
     if (ix->d_ovf2) (void)hipFree(ix->d_ovf2);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
@@ -343,7 +355,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
 
 extern "C" size_t hsa_index_bytes(const hsa_index_t *ix)
 {
-    return (ix->nblk[0] + ix->nblk[1]) * 16 + (ix->nsup[0] + ix->nsup[1]) * 32;
+    return (ix->nblk[0] + ix->nblk[1]) * 16;
 }
 extern "C" int hsa_index_is64(const hsa_index_t *ix) { return ix->is64 ? 1 : 0; }
 extern "C" int hsa_index_device(const hsa_index_t *ix) { return ix->device; }
@@ -371,7 +383,7 @@ __global__ void k_occ4_64(RankDir64 d, const uint64_t *pos, size_t n, uint64_t *
 extern "C" int hsa_occ4_batch64(hsa_index_t *ix, int dir, size_t n, const uint64_t *pos, uint64_t *occ)
 {
     if (dir < 0 || dir > 1) { hsa_set_error("dir"); return HSA_E_ARG; }
-    if (!ix->has_sup) { hsa_set_error("not a 64-bit index (hsa_index_create_device64)"); return HSA_E_ARG; }
+    if (!ix->wide) { hsa_set_error("not a 64-bit index (hsa_index_create_device64)"); return HSA_E_ARG; }
     const uint64_t T = dir ? ix->rT64 : ix->T64;
     for (size_t i = 0; i < n; ++i)
         if (pos[i] > T + 1) { hsa_set_error("position %llu > T + 1", (unsigned long long)pos[i]); return HSA_E_ARG; }
@@ -381,7 +393,7 @@ extern "C" int hsa_occ4_batch64(hsa_index_t *ix, int dir, size_t n, const uint64
     if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, n * 8 + 16)) || (rc = hsa_grow(&ix->d_out, &ix->d_out_cap, n * 32 + 16)))
         return rc;
     HSA_HIP(hipMemcpyAsync(ix->d_in, pos, n * 8, hipMemcpyHostToDevice, ix->stream));
-    RankDir64 d{ix->blk[dir], ix->sup[dir], dir ? ix->risa0_64 : ix->isa0_64};
+    const RankDir64 d = hsa_rank_dir64(ix, dir);
     if (n) k_occ4_64<<<(unsigned)((n + 255) / 256), 256, 0, ix->stream>>>(d, (const uint64_t *)ix->d_in, n, (uint64_t *)ix->d_out);
     HSA_HIP(hipGetLastError());
     HSA_HIP(hipMemcpyAsync(occ, ix->d_out, n * 32, hipMemcpyDeviceToHost, ix->stream));

@@ -5,6 +5,7 @@
 #include <string>
 
 #include "../../include/hsa_gpu.h"
+#include "hsa_device.h"
 
 void hsa_set_error(const char *fmt, ...);
 
@@ -33,16 +34,16 @@ struct hsa_index {
     int device = 0;
     uint32_t T = 0, isa0 = 0, C[5] = {0, 0, 0, 0, 0};
     uint32_t rT = 0, risa0 = 0, rC[5] = {0, 0, 0, 0, 0};
-    uint4 *blk[2] = {nullptr, nullptr};
+    uint4 *blk[2] = {nullptr, nullptr};        // HSA_WRAP_HEAD bytes into blk_base
+    void *blk_base[2] = {nullptr, nullptr};
     size_t nblk[2] = {0, 0};
     // 64-bit interval index (hsa_index_create_device64): exact lengths / counts and the
-    // superblock tables of RankDir64 (hsa_device.h).  is64: a text of 2^32 characters
-    // or more, which only the *64 entry points accept.
-    bool has_sup = false, is64 = false;
+    // wrap tables of RankDir64 (hsa_device.h).  is64: a text of 2^32 characters or
+    // more, which only the *64 entry points accept.
+    bool wide = false, is64 = false;
     uint64_t T64 = 0, isa0_64 = 0, C64[5] = {0, 0, 0, 0, 0};
     uint64_t rT64 = 0, risa0_64 = 0, rC64[5] = {0, 0, 0, 0, 0};
-    uint64_t *sup[2] = {nullptr, nullptr};
-    size_t nsup[2] = {0, 0};
+    bool any_wrap[2] = {false, false};         // a wrap table entry (RankDir64)
     hipStream_t stream = nullptr;
     int n_cu = 0;
     SearchScratch main, big, huge;
@@ -79,6 +80,7 @@ int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap
 void hsa_scratch_free(SearchScratch &s);
 // HSA_E_ARG unless the index fits the 32-bit entry points (bwtint_t, 2BWT-Interface.h:26)
 int hsa_need32(const hsa_index *ix);
+RankDir64 hsa_rank_dir64(const hsa_index *ix, int dir);   // the wrap-table rank of a wide index
 
 // Knobs (hsa_configure).
 extern int g_waves_per_cu;

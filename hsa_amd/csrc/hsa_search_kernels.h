@@ -1316,8 +1316,8 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.rev = RankDir{ix->blk[1], ix->risa0};
     A.T = ix->T;
     memcpy(A.C, ix->C, sizeof A.C);
-    A.fwd64 = RankDir64{ix->blk[0], ix->sup[0], ix->isa0_64};
-    A.rev64 = RankDir64{ix->blk[1], ix->sup[1], ix->risa0_64};
+    A.fwd64 = hsa_rank_dir64(ix, 0);
+    A.rev64 = hsa_rank_dir64(ix, 1);
     A.T64 = ix->T64;
     memcpy(A.C64, ix->C64, sizeof A.C64);
     A.regimes = d_regimes; A.bmap = d_bmap; A.jobs = d_jobs; A.job_list = d_list; A.n_jobs = n; A.codes = d_codes;
@@ -1458,7 +1458,7 @@ static int search_device_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
 {
     // regimes: host array; staged into the index's staging area
     if (n_regimes < 1 || n_regimes > 2) { hsa_set_error("1 or 2 regimes"); return HSA_E_ARG; }
-    if (sizeof(IT) == 8 && !ix->has_sup) { hsa_set_error("not a 64-bit index (hsa_index_create_device64)"); return HSA_E_ARG; }
+    if (sizeof(IT) == 8 && !ix->wide) { hsa_set_error("not a 64-bit index (hsa_index_create_device64)"); return HSA_E_ARG; }
     int rc = check_regimes(regimes, n_regimes);
     if (rc) return rc;
     if (b->max_len < 1 || b->max_len > 1023 || b->max_seed < 0 || b->max_seed > 1023) {

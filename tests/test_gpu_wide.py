@@ -194,6 +194,63 @@ def test_rank_past_2_32_matches_oracle():
     gi.close()
 
 
+def test_rank_count_wraps_match_oracle():
+    """Occ past a count wrap: base counts above 2^32 (the blocks keep them modulo 2^32 and
+    the index's wrap table adds the high words).  Forward: A everywhere but 1 in 2 000
+    code words random, so Occ(A) passes 2^32 near the end; reverse: the same with C.
+    Positions around each wrap block, random ones and the usual edges."""
+    import torch
+    from hsa_amd._lib import GpuIndex, check, lib
+    from oracle_ctypes import OracleIndex64
+    T = BIG_T
+    nw = (T + 15) // 16
+    d, host, Cs, wraps = [], [], [], []
+    for fill, seed in ((0x00000000, 31), (0x55555555, 32)):
+        t = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
+        check(lib().hsa_synth_genome_device(0, T, seed, t.data_ptr()))
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        keep = torch.rand(nw + 8, device="cuda", generator=g) < 1.0 / 2000
+        t = torch.where(keep, t, torch.tensor(np.int32(np.uint32(fill).view(np.int32)), device="cuda"))
+        if T % 16:                                   # no codes past T in the last word
+            last = int(np.uint32(t[nw - 1].item() & 0xFFFFFFFF)) & ((1 << (2 * (T % 16))) - 1)
+            t[nw - 1] = int(np.uint32(last).view(np.int32))
+        t[nw:] = 0
+        torch.cuda.synchronize()
+        w = t[:nw].cpu().numpy().view(np.uint32)
+        cnt = _counts_lsb(w, T)
+        Cs.append(np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64))
+        base = 0 if fill == 0 else 1
+        assert cnt[base] > (1 << 32)
+        # the character position where the count of `base` reaches 2^32
+        lo = w & np.uint32(0x55555555)
+        hi = (w >> np.uint32(1)) & np.uint32(0x55555555)
+        per = (np.bitwise_count(lo & ~hi & np.uint32(0x55555555)) if base == 1 else
+               16 - np.bitwise_count((lo | hi) & np.uint32(0x55555555))).astype(np.int64)
+        if base == 0:
+            per[-1] -= 16 - (T - 16 * (nw - 1))    # padding codes are not characters
+        word = int(np.searchsorted(np.cumsum(per), 1 << 32))
+        wraps.append(16 * word)
+        d.append(t)
+        host.append(w)
+    isa0 = (T // 5 + 3, (1 << 32) + 77)
+    gi = GpuIndex.from_device_codes64(T, isa0[0], Cs[0], d[0].data_ptr(), T, isa0[1], Cs[1], d[1].data_ptr())
+    ox = OracleIndex64(T, isa0[0], Cs[0], host[0], T, isa0[1], Cs[1], host[1])
+    rng = np.random.default_rng(9)
+    for d_ in (0, 1):
+        w0 = wraps[d_]
+        near = [w0 + e for e in range(-40, 41)] + [w0 + 16 * k for k in (-3, -2, -1, 1, 2, 3, 1000)]
+        pos = np.concatenate([rng.integers(0, T + 2, 3000, dtype=np.uint64),
+                              rng.integers(w0 - 100000, w0 + 100000, 1000, dtype=np.uint64),
+                              np.array(near + [0, 1, 16, (1 << 32) - 1, 1 << 32, T - 1, T, T + 1,
+                                               isa0[d_] - 1, isa0[d_], isa0[d_] + 1], np.uint64)])
+        got = gi.occ4_64(d_, pos)
+        exp = np.stack([ox.occ4(d_, int(p)) for p in pos])
+        bad = np.flatnonzero((got != exp).any(axis=1))
+        assert len(bad) == 0, f"dir {d_}: {len(bad)} positions differ, first {int(pos[bad[0]])}: {got[bad[0]]} vs {exp[bad[0]]}"
+        assert int(exp[:, d_].max()) > (1 << 32)     # the wrap was crossed
+    gi.close()
+
+
 def test_search_past_2_32_matches_oracle():
     """A 4.3 Gbp synthetic text, its forward and reverse BWTs built on the device
     (hsa_build_bwt_device64: u64 suffix positions), 2 000 reads of 100 bp from the

@@ -1,10 +1,10 @@
 #!/bin/bash
 # resource usage of the search kernels (device-only compile): SGPR/VGPR counts and
 # spills per instantiation.  usage: tools/kres.sh [source.hip] [regex]
-SRC=${1:-hsa_amd/csrc/hsa_search.hip}
+SRC=${1:-hsa_amd/csrc/hsa_search.hip}; X=${KRES_FLAGS:-}   # KRES_FLAGS: extra -D flags
 RE=${2:-k_search|k_widths}
 cd "$(dirname "$0")/.." || exit 1
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only -S "$SRC" -o /tmp/kres.s 2>/dev/null || exit 1
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only $X -S "$SRC" -o /tmp/kres.s 2>/dev/null || exit 1
 python3 - "$RE" <<'PY'
 import re, sys
 s = open('/tmp/kres.s').read()
