@@ -1,10 +1,10 @@
 #!/bin/bash
 # Round-2 closing validation on the GPU box: every GPU test, smoke, bench configs 2/3/4,
 # the spliced-read drop-in end to end, and the kernel-trace stats of the default bench.
-# usage: tools/gpu_final_r02.sh      outputs under gpurun_out/final2/
+# usage: [FINAL_DIR=name] tools/gpu_final_r02.sh      outputs under gpurun_out/${FINAL_DIR:-final2}/
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/final2
+OUT=$R/gpurun_out/${FINAL_DIR:-final2}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
