@@ -213,7 +213,9 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     LaunchPlan P;
     const bool gaps = any_gaps(regimes, n_regimes);
     const bool wide = need_wide(regimes, n_regimes);
-    if ((rc = plan_launch(ix, n_jobs, max_len, max_seed, nb, gaps, wide, PASS_MAIN, P))) return rc;
+    bool nib_ok = !mgpp && nib_exact(regimes, n_regimes);
+    for (int j = 0; j < n_jobs && nib_ok; ++j) nib_ok = jobs[j].max_diff <= 6;
+    if ((rc = plan_launch(ix, n_jobs, max_len, max_seed, nb, gaps, wide, PASS_MAIN, P, 0, 16, nib_ok))) return rc;
     HSA_HIP(hipEventRecord(ix->ev0, st));
     if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, (const hsa_job_t *)(din + o_jobs), nullptr, n_jobs,
                           max_len, max_seed, (const uint8_t *)(din + o_codes), d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, st,
@@ -252,7 +254,7 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
         int max_entries = 0;
         for (int r = 0; r < n_regimes; ++r) max_entries = regimes[r].max_entries > max_entries ? regimes[r].max_entries : max_entries;
         const int mode = round == 0 ? PASS_BIG : PASS_HUGE;
-        if ((rc = plan_launch(ix, n_over, max_len, max_seed, nb, gaps, wide, mode, B, max_entries))) {
+        if ((rc = plan_launch(ix, n_over, max_len, max_seed, nb, gaps, wide, mode, B, max_entries, 16, nib_ok))) {
             free(list); free(h); return rc;
         }
         uint64_t cap2 = (uint64_t)n_over * 256 * (round + 1) + 65536;

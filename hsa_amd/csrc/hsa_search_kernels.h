@@ -266,6 +266,7 @@ template <> struct BMask<2> {
 // The base code keeps exactly what bwt_match_gap derives from it: c > 3 (N) and
 // (c + j) & 3 (bwtgap.c:305-306).
 template <typename WT> struct WFmt {
+    static constexpr bool NIB = false;
     static constexpr uint32_t BIDB = sizeof(WT) == 1 ? 4u : 8u;
     static constexpr uint32_t BIDM = (1u << BIDB) - 1u;
     static constexpr uint32_t EQ = 1u << BIDB;
@@ -275,6 +276,28 @@ template <typename WT> struct WFmt {
     __device__ static uint32_t code_bits(uint32_t c) { return (c & 3u) << CSH | (c > 3 ? 4u : 0u) << CSH; }
     __device__ static uint32_t code(uint32_t v) { return (v >> CSH) & 7u; }   // 0..3, or 4..7 for N
 };
+
+// 4-bit elements for long reads (k_search only): min(bid, 7) | eq << 3, eight per LDS
+// word, exact while max(max_diff, max_seed_diff) <= 6.  k_widths still writes the
+// 8-bit rows to HBM; k_search packs them into LDS at each strand start and reads the
+// base codes from the HBM row (L2-resident), so a 250 bp read needs 126 B of LDS per
+// lane instead of 252 B and the CU holds twice the waves.
+struct WNib { uint8_t v; };
+template <> struct WFmt<WNib> {
+    static constexpr bool NIB = true;
+    static constexpr uint32_t BIDB = 3u, BIDM = 7u, EQ = 8u, EB = 4u, EPW = 8u;
+};
+
+// four 8-bit elements (WFmt<uint8_t>) -> four 4-bit ones in the low 16 bits
+__device__ __forceinline__ uint32_t nib4(uint32_t x)
+{
+    uint32_t b = x & 0x0F0F0F0Fu;                                   // bids, <= 15 per byte
+    const uint32_t ge7 = ((b + 0x09090909u) >> 4) & 0x01010101u;     // bid >= 7
+    b = (b & ~(ge7 * 0x0Fu)) | ge7 * 7u;
+    uint32_t n = b | ((x >> 4) & 0x01010101u) << 3;                   // | eq << 3
+    n = (n | n >> 4) & 0x00FF00FFu;
+    return (n | n >> 8) & 0xFFFFu;
+}
 
 #ifdef HSA_DIAG
 // Diagnostic build only (-DHSA_DIAG, never the product library): per-workgroup
@@ -499,8 +522,11 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         reinterpret_cast<uint32_t *>(s_reg)[tid] = reinterpret_cast<const uint32_t *>(a.regimes)[tid];
     __syncthreads();
     LT *const s_heads = reinterpret_cast<LT *>(s_lds + a.off_heads);
-    WT *const s_wb = reinterpret_cast<WT *>(s_lds + a.off_wb);
-    WT *const s_ws = reinterpret_cast<WT *>(s_lds + a.off_ws);
+    using WTL = typename std::conditional<F::NIB, uint8_t, WT>::type;     // LDS element (8/16-bit formats)
+    WTL *const s_wb = reinterpret_cast<WTL *>(s_lds + a.off_wb);
+    WTL *const s_ws = reinterpret_cast<WTL *>(s_lds + a.off_ws);
+    uint32_t *const s_nb = reinterpret_cast<uint32_t *>(s_lds + a.off_wb);   // 4-bit format: word q * NT + tid
+    uint32_t *const s_ns = reinterpret_cast<uint32_t *>(s_lds + a.off_ws);
     // per-lane HBM scratch, wave-interleaved: element e of lane l of wave w at
     // (w * cap + e) * 64 + l, so one wave's accesses stay inside one small region
     // (few pages) and lanes at equal e coalesce
@@ -554,8 +580,33 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 #define R_MAXGE ((int)(rmode >> 16))
 #define SCORE(mm, go, ge) ((mm) * S_MM + (go) * S_GO + (ge) * S_GE)
 
-    // base of the current strand's sequence at p (from the LDS element, see WFmt)
-    auto getc = [&](int p) -> uint32_t { return F::code(WB(p)); };
+    // pruning elements of the read row / seed row at p (WFmt), and the element write of gap_shadow
+    auto wbg = [&](int p) -> uint32_t {
+        if constexpr (F::NIB) return (s_nb[((uint32_t)p >> 3) * NT + tid] >> (((uint32_t)p & 7u) * 4u)) & 15u;
+        else return WB(p);
+    };
+    auto wsg = [&](int p) -> uint32_t {
+        if constexpr (F::NIB) return (s_ns[((uint32_t)p >> 3) * NT + tid] >> (((uint32_t)p & 7u) * 4u)) & 15u;
+        else return WS(p);
+    };
+    auto wbs = [&](int p, uint32_t v) {
+        if constexpr (F::NIB) {
+            uint32_t &w = s_nb[((uint32_t)p >> 3) * NT + tid];
+            const uint32_t sh = ((uint32_t)p & 7u) * 4u;
+            w = (w & ~(15u << sh)) | v << sh;
+        } else {
+            WB(p) = (WTL)v;
+        }
+    };
+    // 4-bit format: the strand's 8-bit HBM row (base codes), and the base the next
+    // step needs, loaded in the control phase so that its latency overlaps the rank load
+    const uint8_t *rowp = nullptr;
+    uint32_t cur_c = 0;
+    // base of the current strand's sequence at p (from the LDS element, or the HBM row)
+    auto getc = [&](int p) -> uint32_t {
+        if constexpr (F::NIB) return WFmt<uint8_t>::code(rowp[((uint32_t)p >> 2) * 256u + ((uint32_t)p & 3u)]);
+        else return F::code(WB(p));
+    };
     // stack bucket of an entry: dense index of its score (bwtgap.c:46-75)
     auto bucket_of = [&](uint32_t m) -> int {
         if (!GAPS && a.mm_buckets) return M_MM(m);
@@ -609,8 +660,26 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         // the whole row is in flight at once and one wait covers it
         const ColdArgs r = cold_args();
         const uint32_t *src = reinterpret_cast<const uint32_t *>(r->wb) + row_base(r->rb / 4);
-        uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + (tid & ~63u);
         const uint32_t nwb = r->rb / 4;                // row capacity in words (uniform)
+        if constexpr (F::NIB) {
+            // two 8-bit words per LDS word, eight loads in flight
+            rowp = reinterpret_cast<const uint8_t *>(src);
+            auto pack = [&](const uint32_t *row, uint32_t nw, uint32_t *dst) {
+                const uint32_t nn = (nw + 1u) / 2u;
+                for (uint32_t j = 0; j < nn; j += 4) {
+                    uint32_t w[8];
+#pragma unroll
+                    for (uint32_t u = 0; u < 8; ++u) w[u] = 2u * j + u < nw ? row[(2u * j + u) * 64u] : 0u;
+#pragma unroll
+                    for (uint32_t u = 0; u < 4; ++u)
+                        if (j + u < nn) dst[(j + u) * NT + tid] = nib4(w[2u * u]) | nib4(w[2u * u + 1u]) << 16;
+                }
+            };
+            pack(src, nwb, s_nb);
+            if (C_SEED(ctl) && !C_ALIAS(ctl))
+                pack(reinterpret_cast<const uint32_t *>(r->ws) + row_base(r->rs / 4), r->rs / 4, s_ns);
+        } else {
+        uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + (tid & ~63u);
         for (uint32_t q = 0; q < nwb; ++q)
             __builtin_amdgcn_global_load_lds(src + q * 64, db + q * NT, 4, 0, 0);
         if (C_SEED(ctl) && !C_ALIAS(ctl)) {
@@ -619,6 +688,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             const uint32_t nws = r->rs / 4;
             for (uint32_t q = 0; q < nws; ++q)
                 __builtin_amdgcn_global_load_lds(ss + q * 64, ds + q * NT, 4, 0, 0);
+        }
         }
 #ifdef HSA_EXTRA_LOADS
         // experiment only: HSA_EXTRA_LOADS random 16-byte rank-table loads per strand
@@ -744,7 +814,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                     IT w = WG(p);
                     if (w > x) { w -= x; WG(p) = w; }
                     else if (w == x) {
-                        WB(p) = (WT)((WB(p) & ~F::BIDM) | 1u);
+                        wbs(p, (wbg(p) & ~F::BIDM) | 1u);
                         WG(p) = TT - (++jj);
                         if (wd) wd[(uint32_t)p * 64] = 1;
                     }
@@ -752,7 +822,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 IT wnext = WG(ldp);
                 for (int p = ldp - 1; p >= 0; --p) {
                     const IT w = WG(p);
-                    WB(p) = (WT)((WB(p) & ~F::EQ) | (w == wnext ? F::EQ : 0u));
+                    wbs(p, (wbg(p) & ~F::EQ) | (w == wnext ? F::EQ : 0u));
                     wnext = w;
                 }
 #undef WG
@@ -871,6 +941,12 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             }
             const uint32_t ph = C_PH(ctl);
             if (ph == PH_EXACT) {
+                if constexpr (F::NIB) {
+                    // the rank step goes out with the base load; an N (c > 3) drops it in (D)
+                    cur_c = getc((int)pos);
+                    req = 1; rp1 = ik; rp2 = il + 1u;
+                    break;
+                }
                 const uint32_t c = getc((int)pos);
                 if (c > 3) { SET_PH(ctl, PH_POP); continue; }              // 2BWT-Interface.c:377
                 req = 1; rp1 = ik; rp2 = il + 1u;
@@ -905,7 +981,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             const int em = m_of(m);
             if (em < 0) continue;
             const int ei = M_I(m);
-            if (ei > 0 && em < (int)(WB(ei - 1) & F::BIDM)) continue;
+            if (ei > 0 && em < (int)(wbg(ei - 1) & F::BIDM)) continue;
             if (ei == 0) {
                 if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
                 continue;
@@ -916,6 +992,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 continue;
             }
             req = 1; rp1 = e.x; rp2 = e.y + 1u;
+            if constexpr (F::NIB) cur_c = getc(ei - 1);                  // the expansion's base (D)
             SET_PH(ctl, PH_EXPAND);
         }
 #if !HSA_CTL_LOOP
@@ -946,9 +1023,12 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 #endif
         // ---------------- (D) apply
         const uint32_t ph = C_PH(ctl);
-        if (req && ph == PH_EXACT) {
+        if (F::NIB && req && ph == PH_EXACT && cur_c > 3) {
+            st_q -= 2u; st_b -= 1u + two;                                // not a step (2BWT-Interface.c:377)
+            SET_PH(ctl, PH_POP);
+        } else if (req && ph == PH_EXACT) {
             // BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170), one character
-            const uint32_t c = getc((int)pos);
+            const uint32_t c = F::NIB ? cur_c : getc((int)pos);
             IT oc = 0;
 #pragma unroll
             for (uint32_t d = 1; d < 4; ++d) oc += d > c ? ob[d] - oa[d] : (IT)0;
@@ -989,7 +1069,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             int allow_diff = 1, allow_M = 1;
             if (i > 0) {
                 // width[i-1].bid, width[i].bid and w[i-1] == w[i] (bwtgap.c:256-258)
-                const uint32_t w1 = WB(i - 1), w0 = WB(i);
+                const uint32_t w1 = wbg(i - 1), w0 = wbg(i);
                 const int b1 = (int)(w1 & F::BIDM), b0 = (int)(w0 & F::BIDM);
                 if (b1 > em - 1) allow_diff = 0;
                 else if (b1 == em - 1 && b0 == em - 1 && (w1 & F::EQ)) allow_M = 0;
@@ -998,8 +1078,8 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                     int ems = RG(max_seed_diff) - (emm + ego);
                     if (R_MODE & MODE_GAPE) ems -= ege;
                     // width_seed aliased to width_back (bwtgap.c:809): the same LDS row
-                    const uint32_t s1 = C_ALIAS(ctl) ? (uint32_t)WB(ii - 1) : (uint32_t)WS(ii - 1);
-                    const uint32_t s0 = C_ALIAS(ctl) ? (uint32_t)WB(ii) : (uint32_t)WS(ii);
+                    const uint32_t s1 = C_ALIAS(ctl) ? wbg(ii - 1) : wsg(ii - 1);
+                    const uint32_t s0 = C_ALIAS(ctl) ? wbg(ii) : wsg(ii);
                     const int c1 = (int)(s1 & F::BIDM), c0 = (int)(s0 & F::BIDM);
                     if (c1 > ems - 1) allow_diff = 0;
                     else if (c1 == ems - 1 && c0 == ems - 1 && (s1 & F::EQ)) allow_M = 0;
@@ -1009,7 +1089,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             // bit 0 insertion, bits 1-4 deletion with child j = bit-1, bits 5-8
             // match/mismatch with child (seq[i] + bit-4) & 3.  All but the last go to the
             // pool in order; the last becomes the virtual top when it is the next pop.
-            const uint32_t sc = getc(i);
+            const uint32_t sc = F::NIB ? cur_c : getc(i);
             uint32_t cand = 0;
             if (GAPS && allow_diff && (R_MAXGO > 0 || ego > 0)) {
                 const int ies = RG(indel_end_skip);
@@ -1162,6 +1242,7 @@ struct LaunchPlan {
     uint32_t nt;                     // lanes per workgroup of k_search (256 or 64)
     uint32_t pcap, hcap, nb;
     bool gaps, wide;                 // gap opens possible; 16-bit pruning elements (WFmt)
+    bool nib;                        // 4-bit pruning elements in LDS (WFmt<WNib>)
     uint32_t off_heads, off_wb, off_ws;
     size_t lds;
     bool huge;                       // PASS_HUGE: 32-bit links, reused slots
@@ -1174,7 +1255,7 @@ struct LaunchPlan {
 enum { PASS_MAIN = 0, PASS_BIG = 1, PASS_HUGE = 2 };
 
 static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int nb, bool gaps, bool wide, int mode,
-                       LaunchPlan &P, int max_entries = 0, uint32_t ent_bytes = 16)
+                       LaunchPlan &P, int max_entries = 0, uint32_t ent_bytes = 16, bool nib_ok = false)
 {
     const bool big = mode == PASS_BIG;
     P.huge = mode == PASS_HUGE;
@@ -1183,7 +1264,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     P.gaps = gaps;
     P.wide = wide;
     const uint32_t esz = wide ? 2u : 1u;
-    const uint32_t epw = 4u / esz;                       // elements per LDS word (WFmt::EPW)
+    P.nib = false;
     // Resident workgroups per CU, from gfx950's own limits: 160 KiB of LDS per CU, at
     // most 16 waves (__launch_bounds__(NT, 4) caps VGPRs at 4 waves per SIMD).  The
     // per-lane LDS (bucket heads, pruning rows) decides between 256-lane workgroups
@@ -1193,6 +1274,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     // HIP runtime the process loaded first it assumed 64 KiB of LDS and halved the
     // grid -- measured 512 instead of 1024 workgroups, 1.5x slower.)
     auto layout = [&](uint32_t nt) {
+        const uint32_t epw = P.nib ? 8u : 4u / esz;      // elements per LDS word (WFmt::EPW)
         P.nt = nt;
         P.off_heads = 2 * P.ntab + 128;   // score tables, then the two regimes
         P.off_wb = P.off_heads + (uint32_t)nb * nt * (P.huge ? 4u : 2u);
@@ -1206,11 +1288,27 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
         return per_cu;
     };
     static const int force256 = getenv("HSA_WG256") != nullptr;   // A/B runs only
-    int per_cu = layout(P.huge ? 64 : 256);
-    if (per_cu < 4 && !force256 && !P.huge) {
-        const int p64 = layout(64);
-        if (p64 > per_cu * 4) per_cu = p64;
-        else per_cu = layout(256);
+    auto best = [&]() {
+        int per_cu = layout(P.huge ? 64 : 256);
+        if (per_cu < 4 && !force256 && !P.huge) {
+            const int p64 = layout(64);
+            if (p64 > per_cu * 4) per_cu = p64;
+            else per_cu = layout(256);
+        }
+        return per_cu;
+    };
+    int per_cu = best();
+    // long reads: 4-bit elements when the 8-bit rows leave the CU short of 16 waves
+    // (HSA_WFMT=nib forces them where exact, =byte keeps 8-bit; tests and A/B runs)
+    const char *wf = getenv("HSA_WFMT");
+    const bool force_nib = wf && !strcmp(wf, "nib"), no_nib = wf && !strcmp(wf, "byte");
+    if (nib_ok && !wide && !P.huge && !no_nib && (force_nib || per_cu * (int)(P.nt / 64) < 16)) {
+        const int waves8 = per_cu * (int)(P.nt / 64);
+        const LaunchPlan keep = P;
+        P.nib = true;
+        const int per_nib = best();
+        if (!force_nib && per_nib * (int)(P.nt / 64) <= waves8) { P = keep; }
+        else per_cu = per_nib;
     }
     if (P.lds > 160 * 1024) { hsa_set_error("reads too long for the LDS budget (%zu bytes)", P.lds); return HSA_E_ARG; }
     if (per_cu < 1) { hsa_set_error("search kernel does not fit (LDS %zu)", P.lds); return HSA_E_ARG; }
@@ -1235,7 +1333,8 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
         int occ = 0;
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_search<1, true, uint8_t, 256>, 256, P.lds);
         fprintf(stderr, "[hsa] launch: %d CUs x %d workgroups of %u lanes (runtime occupancy query says %d), "
-                "LDS %zu B, %zu workgroups, %d buckets\n", ix->n_cu, per_cu, P.nt, occ, P.lds, blocks, nb);
+                "LDS %zu B, %zu workgroups, %d buckets%s\n", ix->n_cu, per_cu, P.nt, occ, P.lds, blocks, nb,
+                P.nib ? ", 4-bit rows" : "");
     }
     // pool slots are not reused within a search: gapped searches push many more.  A
     // deeper main-pass pool keeps the long gapped searches inside the main pass, where
@@ -1281,6 +1380,13 @@ static void launch_search_nt(const LaunchPlan &P, const SearchArgs &A, hipStream
 template <typename WT, typename IT>
 static void launch_search(const LaunchPlan &P, const SearchArgs &A, hipStream_t st)
 {
+    if constexpr (!std::is_same<WT, WNib>::value) {
+        if (P.nib) {                                 // never a HUGE pass (plan_launch)
+            if (P.nt == 64) launch_search_nt<WNib, 64, IT>(P, A, st);
+            else launch_search_nt<WNib, 256, IT>(P, A, st);
+            return;
+        }
+    }
     if (P.huge) {
         const dim3 g((unsigned)P.blocks), b(64);
         if (P.gaps) hipLaunchKernelGGL((k_search<2, true, WT, 64, true, IT>), g, b, P.lds, st, A);
@@ -1410,6 +1516,15 @@ static bool need_wide(const hsa_regime_t *rg, int n)
     return false;
 }
 
+// 4-bit pruning elements are exact while every bid comparison bound is <= 6 (WFmt<WNib>);
+// a job's max_diff never exceeds its regime's
+static bool nib_exact(const hsa_regime_t *rg, int n)
+{
+    for (int r = 0; r < n; ++r)
+        if (rg[r].max_diff > 6 || rg[r].max_seed_diff > 6) return false;
+    return true;
+}
+
 static int jobs_limits(const hsa_job_t *jobs, int n, int &max_len, int &max_seed)
 {
     max_len = 0; max_seed = 0;
@@ -1476,8 +1591,9 @@ static int search_device_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     const bool gaps = any_gaps(regimes, n_regimes), wide = need_wide(regimes, n_regimes);
     int max_entries = 0;
     for (int r = 0; r < n_regimes; ++r) max_entries = regimes[r].max_entries > max_entries ? regimes[r].max_entries : max_entries;
-    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_MAIN, P, 0, EB)) ||
-        (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_BIG, B, 0, EB)) ||
+    const bool nib_ok = nib_exact(regimes, n_regimes);
+    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_MAIN, P, 0, EB, nib_ok)) ||
+        (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_BIG, B, 0, EB, nib_ok)) ||
         (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_HUGE, H, max_entries, EB)))
         return rc;
     if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, (size_t)b->n_jobs * 4 + 64)) ||
