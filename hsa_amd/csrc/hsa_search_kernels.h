@@ -1298,11 +1298,14 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
         return per_cu;
     };
     int per_cu = best();
-    // long reads: 4-bit elements when the 8-bit rows leave the CU short of 16 waves
-    // (HSA_WFMT=nib forces them where exact, =byte keeps 8-bit; tests and A/B runs)
+    // long reads: 4-bit elements when the 8-bit rows leave the CU short of 16 waves, in
+    // ungapped searches, which are latency-bound: config 5's k_search 45.6 -> 38.4 ms.
+    // Gapped ones are issue-bound and lose more to the unpacking and the base loads
+    // than they gain in waves (config 4: 1 988 -> 2 147 ms; config 3: equal).
+    // HSA_WFMT=nib forces them where exact, =byte keeps 8-bit (tests and A/B runs).
     const char *wf = getenv("HSA_WFMT");
     const bool force_nib = wf && !strcmp(wf, "nib"), no_nib = wf && !strcmp(wf, "byte");
-    if (nib_ok && !wide && !P.huge && !no_nib && (force_nib || per_cu * (int)(P.nt / 64) < 16)) {
+    if (nib_ok && !wide && !P.huge && !no_nib && (force_nib || (!gaps && per_cu * (int)(P.nt / 64) < 16))) {
         const int waves8 = per_cu * (int)(P.nt / 64);
         const LaunchPlan keep = P;
         P.nib = true;
