@@ -114,9 +114,10 @@ def main():
                      "vmem_rd_wave_insts": med(sq, "SQ_INSTS_VMEM_RD"),
                      "waves": med(sq, "SQ_WAVES"),
                      "grbm_gui_active_per_xcd": med(sq, "GRBM_GUI_ACTIVE") / 8}
-    tcc, _ = counters(os.path.join(src, "pmc_tcc"), "k_search")
-    h, m = med(tcc, "TCC_HIT_sum"), med(tcc, "TCC_MISS_sum")
-    out["tcc"] = {"hit_rate": h / (h + m), "ea_rdreq": med(tcc, "TCC_EA0_RDREQ_sum")}
+    if os.path.isdir(os.path.join(src, "pmc_tcc")):
+        tcc, _ = counters(os.path.join(src, "pmc_tcc"), "k_search")
+        h, m = med(tcc, "TCC_HIT_sum"), med(tcc, "TCC_MISS_sum")
+        out["tcc"] = {"hit_rate": h / (h + m), "ea_rdreq": med(tcc, "TCC_EA0_RDREQ_sum")}
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
