@@ -1330,9 +1330,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     if (blocks < 1) blocks = 1;
     P.blocks = blocks;
     P.lanes = blocks * NTB;
-    static int verbose = -1;
-    if (verbose < 0) verbose = getenv("HSA_VERBOSE") != nullptr;
-    if (verbose) {
+    if (getenv("HSA_VERBOSE")) {                   // read per plan: tests switch it on mid-process
         int occ = 0;
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_search<1, true, uint8_t, 256>, 256, P.lds);
         fprintf(stderr, "[hsa] launch: %d CUs x %d workgroups of %u lanes (runtime occupancy query says %d), "
