@@ -293,9 +293,10 @@ int hsa_probe_gather(int device, uint64_t table_bytes, int per_sector, double *g
  * points run the same search with 64-bit SA intervals.
  *
  * hsa_index_create_device64: as hsa_index_create_device, with 64-bit lengths, '$'
- * rows and C tables.  The rank blocks keep their counts modulo 2^32 and a superblock
- * table (exact u64 Occ every 2^24 characters, 32 bytes per entry) restores the high
- * part.  An index under 2^32 characters also serves every 32-bit entry point; a
+ * rows and C tables, T and rT under 2^36 (HSA_E_ARG otherwise).  The rank blocks keep
+ * their counts modulo 2^32 and a wrap table (the blocks where a base count passes a
+ * multiple of 2^32, found at creation, 512 bytes in front of the blocks) restores the
+ * high part.  An index under 2^32 characters also serves every 32-bit entry point; a
  * longer one only the *64 ones (the others return HSA_E_ARG). */
 int hsa_index_create_device64(int device, uint64_t T, uint64_t isa0, const uint64_t C[5], const uint32_t *d_code_lsb,
                               uint64_t rT, uint64_t risa0, const uint64_t rC[5], const uint32_t *d_rcode_lsb,
