@@ -90,6 +90,7 @@ struct SearchArgs {
     uint32_t *hbuf;
     uint32_t pcap, hcap, nb;
     uint32_t off_heads, off_wb, off_ws;   // LDS byte offsets
+    uint32_t nib_wb, nib_ws;              // 4-bit layout: LDS words per lane of the read / seed row
     uint32_t mm_buckets;           // 1: the bucket of every score is its n_mm (no gap opens, s_mm > 0)
     // device-side overflow re-run: the main pass appends reads that exceeded their
     // lane's capacity to ovf_list (count in ctr[8]); the re-run pass takes its read
@@ -664,8 +665,8 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         if constexpr (F::NIB) {
             // two 8-bit words per LDS word, eight loads in flight
             rowp = reinterpret_cast<const uint8_t *>(src);
-            auto pack = [&](const uint32_t *row, uint32_t nw, uint32_t *dst) {
-                const uint32_t nn = (nw + 1u) / 2u;
+            auto pack = [&](const uint32_t *row, uint32_t nw, uint32_t *dst, uint32_t cap) {
+                const uint32_t nn = (nw + 1u) / 2u < cap ? (nw + 1u) / 2u : cap;   // LDS words of the row
                 for (uint32_t j = 0; j < nn; j += 4) {
                     uint32_t w[8];
 #pragma unroll
@@ -675,9 +676,9 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                         if (j + u < nn) dst[(j + u) * NT + tid] = nib4(w[2u * u]) | nib4(w[2u * u + 1u]) << 16;
                 }
             };
-            pack(src, nwb, s_nb);
+            pack(src, nwb, s_nb, r->nib_wb);
             if (C_SEED(ctl) && !C_ALIAS(ctl))
-                pack(reinterpret_cast<const uint32_t *>(r->ws) + row_base(r->rs / 4), r->rs / 4, s_ns);
+                pack(reinterpret_cast<const uint32_t *>(r->ws) + row_base(r->rs / 4), r->rs / 4, s_ns, r->nib_ws);
         } else {
         uint32_t *const db = reinterpret_cast<uint32_t *>(s_wb) + (tid & ~63u);
         for (uint32_t q = 0; q < nwb; ++q)
@@ -1244,6 +1245,7 @@ struct LaunchPlan {
     bool gaps, wide;                 // gap opens possible; 16-bit pruning elements (WFmt)
     bool nib;                        // 4-bit pruning elements in LDS (WFmt<WNib>)
     uint32_t off_heads, off_wb, off_ws;
+    uint32_t nib_wb, nib_ws;         // 4-bit rows: LDS words per lane (SearchArgs)
     size_t lds;
     bool huge;                       // PASS_HUGE: 32-bit links, reused slots
     uint32_t ntab;                   // score table entries per regime in LDS
@@ -1278,8 +1280,16 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
         P.nt = nt;
         P.off_heads = 2 * P.ntab + 128;   // score tables, then the two regimes
         P.off_wb = P.off_heads + (uint32_t)nb * nt * (P.huge ? 4u : 2u);
-        P.off_ws = P.off_wb + ((uint32_t)max_len / epw + 1u) * nt * 4u;
-        P.lds = ((size_t)P.off_ws + ((size_t)max_seed / epw + 1u) * nt * 4u + 15) / 16 * 16;
+        // k_search reads elements 0 .. len - 1 of a row (pops of position i read i - 1,
+        // expansions i - 1 and i < len; seed rows ii - 1 and ii < seed_len): the 4-bit
+        // rows keep just those, which takes config 5's 64-lane workgroups from 15 to 16
+        // per CU; the 8-bit rows keep element len too (the LDS-DMA copies whole words)
+        P.nib_wb = ((uint32_t)max_len + 7u) / 8u;
+        P.nib_ws = ((uint32_t)max_seed + 7u) / 8u;
+        const uint32_t wbw = P.nib ? P.nib_wb : (uint32_t)max_len / epw + 1u;
+        const uint32_t wsw = P.nib ? P.nib_ws : (uint32_t)max_seed / epw + 1u;
+        P.off_ws = P.off_wb + wbw * nt * 4u;
+        P.lds = ((size_t)P.off_ws + (size_t)wsw * nt * 4u + 15) / 16 * 16;
         int per_cu = (int)((160u * 1024u) / P.lds);
         const int cap = 16 / (int)(nt / 64);                 // 16 waves per CU
         const int want = g_waves_per_cu / (int)(nt / 64);
@@ -1434,6 +1444,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.pool = S.pool; A.nxt = S.nxt; A.hbuf = S.hbuf;
     A.pcap = P.pcap; A.hcap = P.hcap;        // the planned capacities (the scratch may be larger)
     A.nb = P.nb; A.off_heads = P.off_heads; A.off_wb = P.off_wb; A.off_ws = P.off_ws;
+    A.nib_wb = P.nib_wb; A.nib_ws = P.nib_ws;
     A.mm_buckets = ix->staged_mmb ? 1u : 0u;
     A.ntab = P.ntab;
     A.batch_k = (uint32_t)g_batch_k;
