@@ -16,9 +16,20 @@ synthetic ~15 Gbp plant-scale text, which the reference's 32-bit bwtint_t cannot
 index: the 64-bit interval instantiation (hsa_search_device64, hsa_aln64_t hits) over
 a device-built 64-bit index, parity against the 64-bit restatement (liboracle64.so).
 
-Multi-GPU (torch.distributed.run, one rank per GPU): every rank holds the whole
-index, searches its own K batches of reads (weak scaling, no collective on the data
-path), and the per-rank hit lists are gathered to rank 0 over RCCL after timing.
+Multi-GPU (one rank per GPU): under torch.distributed.run (WORLD_SIZE set), or with
+`--gpus N` alone, which starts the N ranks itself (before anything touches the GPU).
+Every rank holds the whole index, searches its own K batches of reads (weak scaling,
+no collective on the data path), checks a sample of its timed reads against the CPU
+restatement, and the per-rank hit lists of every timed read set are gathered to rank 0
+over RCCL after timing; rank 0 re-checks the gathered lists against per-rank digests.
+
+Baselines beside the GPU figure (rank 0 at N=1, configs 2 and 3): the restatement on
+the box's CPU share (the whole timed batch, also the parity check), and the
+REFERENCE's own bwa_cal_sa_reg_gap (oracle/_ref/ref_probe, compiled from its sources
+in the build container) on index files written from the device-built BWTs, one process
+per core of the share.  The drop-in end to end: the reference's driver linked with
+every drop-in entry point of ours (oracle/_ref/ref_probe_gpu) on bwa_seq_t batches of
+100 000 reads, splice fallback included, its hits compared with the reference's.
 """
 import argparse
 import ctypes as C
@@ -32,8 +43,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-
-import hsa_amd  # noqa: E402,F401  (loads libhsa_gpu.so before torch: hsa_amd/_lib.py)
+# hsa_amd (which loads libhsa_gpu.so, before torch: hsa_amd/_lib.py) is imported in
+# main(), after `--gpus N` has started its ranks: the parent never loads the library.
+REF_DIR = os.path.join(ROOT, "oracle", "_ref")
 
 GENOME_T = 3_000_000_005
 GENOME5_T = 15_000_000_003  # config 5: plant-scale, past 2^32
@@ -45,13 +57,18 @@ DISTINCT = 3            # distinct read sets the steps cycle over
 METRIC = "aligned reads/sec, 100bp synthetic vs hg19-sized 2BWT, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_QUERY = 64    # one 64-byte HBM sector per Occ query
+SA_INTERVAL = 8         # the .sa sampling of `HSA index` (2BWT-Builder.c:97)
+REF_BATCH = 100_000     # bwa_aln_core's batch (bwtaln.c:477)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_index(T, seed, device):
+def build_index(T, seed, device, with_files=False):
+    """The hg19-sized index on the device.  with_files: also keep the text (packed) and
+    the forward direction's every-8th SA values (hsa_build_bwt_index_device, the same
+    sort), for the reference's index files (reference_files)."""
     import torch
     from hsa_amd import _lib
     L = _lib.lib()
@@ -59,18 +76,33 @@ def build_index(T, seed, device):
     text = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
     _lib.check(L.hsa_synth_genome_device(device, T, seed, text.data_ptr()))
     res = {}
+    extra = {}
     for rev in (0, 1):
         bw = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
         isa0 = C.c_uint32()
         Cc = np.zeros(5, np.uint32)
         t0 = time.time()
-        _lib.check(L.hsa_build_bwt_device(device, T, text.data_ptr(), rev, bw.data_ptr(), C.byref(isa0), Cc))
+        if with_files and rev == 0:
+            i64 = C.c_uint64()
+            C64 = np.zeros(5, np.uint64)
+            ns = (T + SA_INTERVAL) // SA_INTERVAL
+            sa = torch.zeros(ns, dtype=torch.int32, device="cuda")
+            _lib.check(L.hsa_build_bwt_index_device(device, T, text.data_ptr(), bw.data_ptr(), C.byref(i64), C64,
+                                                    SA_INTERVAL, sa.data_ptr()))
+            isa0.value = int(i64.value)
+            Cc[:] = C64.astype(np.uint32)
+            extra["sa"] = sa.cpu().numpy().view(np.uint32)
+            del sa
+        else:
+            _lib.check(L.hsa_build_bwt_device(device, T, text.data_ptr(), rev, bw.data_ptr(), C.byref(isa0), Cc))
         log(f"[bench] BWT{' (reverse)' if rev else ''} of {T} bp built on the device in {time.time() - t0:.1f} s")
         res[rev] = (bw, int(isa0.value), Cc)
+    if with_files:
+        extra["text"] = text[:nw].cpu().numpy().view(np.uint32)
     del text
     gi = _lib.GpuIndex.from_device_codes(T, res[0][1], res[0][2], res[0][0].data_ptr(), T, res[1][1], res[1][2],
                                          res[1][0].data_ptr(), device=device)
-    return gi, res
+    return gi, res, extra
 
 
 def build_index64(T, seed, device):
@@ -95,7 +127,7 @@ def build_index64(T, seed, device):
     torch.cuda.empty_cache()
     gi = _lib.GpuIndex.from_device_codes64(T, res[0][1], res[0][2], res[0][0].data_ptr(), T, res[1][1], res[1][2],
                                            res[1][0].data_ptr(), device=device)
-    return gi, res
+    return gi, res, {}
 
 
 def host_oracle_index64(res, T):
@@ -243,6 +275,215 @@ def compare_batch(g_n, g_f, g_o, g_h, o_n, o_f, o_h):
     nb = int(bad.sum())
     return nb, (int(np.flatnonzero(bad)[0]) if nb else None)
 
+# ---------------------------------------------------------------- N ranks from --gpus N
+def spawn_ranks(n, argv, script=None):
+    """`bench.py --gpus N` without a launcher: start N ranks of this script (RANK,
+    LOCAL_RANK = GPU, WORLD_SIZE, MASTER_* on 127.0.0.1), relay rank 0's JSON line and
+    return the worst exit status.  The parent imports neither torch nor hsa_amd, so no
+    process here has touched the GPU before its ranks start."""
+    import socket
+    import subprocess
+    import tempfile
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs, outs = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = tempfile.TemporaryFile() if r == 0 else subprocess.DEVNULL
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=out))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0:
+                rc = rc or c
+                log(f"[bench] rank {r} exited with {c}: stopping the others")
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.2)
+    outs[0].seek(0)
+    sys.stdout.write(outs[0].read().decode())
+    sys.stdout.flush()
+    return rc
+
+
+def hits_in_read_order(n_aln, hit_off, hits):
+    """A batch's hit records in read order (the kernel appends each read's hits
+    wherever its atomic lands): the gather's and the digests' layout."""
+    cnt = np.maximum(np.asarray(n_aln, np.int64), 0)
+    if cnt.sum() == 0:
+        return np.zeros((0, hits.shape[1]), np.uint32)
+    starts = np.asarray(hit_off, np.int64)
+    idx = np.repeat(starts - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt) + np.arange(int(cnt.sum()))
+    return np.ascontiguousarray(hits[idx], np.uint32)
+
+
+def batch_digest(n_aln, flags, hits_ordered):
+    """SHA-256 of one batch's results (n_aln, fallback flags, hits in read order)."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(n_aln, np.int32).tobytes())
+    h.update((np.asarray(flags, np.uint32) & 1).astype(np.uint32).tobytes())
+    h.update(np.ascontiguousarray(hits_ordered, np.uint32).tobytes())
+    return h.hexdigest()
+
+
+# ---------------------------------------------------------------- the reference's own path
+def write_reads_bin(path, reads):
+    """ref_probe's reads.bin: u32 n, u32 len[n], then the codes."""
+    reads = np.ascontiguousarray(reads, np.uint8)
+    with open(path, "wb") as f:
+        f.write(np.array([len(reads)], np.uint32).tobytes())
+        f.write(np.full(len(reads), reads.shape[1], np.uint32).tobytes())
+        f.write(reads.tobytes())
+
+
+def read_probe_out(path):
+    """ref_probe's out.bin -> (n_aln, hits of every read concatenated (n, 9))."""
+    b = np.fromfile(path, np.uint32)
+    assert b[0] == 0x48415348, "bad ref_probe output"
+    n = int(b[1])
+    n_aln = np.zeros(n, np.int32)
+    hits = []
+    i = 2
+    for r in range(n):
+        na = int(np.int32(b[i]))
+        i += 2
+        n_aln[r] = na
+        if na > 0:
+            hits.append(b[i:i + 9 * na].reshape(na, 9))
+            i += 9 * na
+    return n_aln, (np.concatenate(hits) if hits else np.zeros((0, 9), np.uint32))
+
+
+def reference_files(d, T, res, extra):
+    """The hg19-sized index as `HSA index` files under d (prefix d/g): .bwt / .rev.bwt
+    from the device-built BWTs (MSB-first words, BWTConstruct.c:1209-1224), .fmv /
+    .rev.fmv by the reference's own BWTGenerateOccValueFromBwt (ref_probe mkfmv), .sa
+    from the device sort's samples (BWTConstruct.c:1373-1392), .pac / .ann from the
+    synthetic text and its record layout (HSP.c:313-337)."""
+    import subprocess
+
+    from hsa_amd import index_build, synth
+    prefix = os.path.join(d, "g")
+    nw = (T + 15) // 16
+    for rev, suf in ((0, ""), (1, ".rev")):
+        bw, isa0, Cc = res[rev]
+        x = bw[:nw].cpu().numpy().view(np.uint32).copy()       # LSB-first -> MSB-first codes
+        x = (x >> 16) | (x << 16)
+        x = ((x & 0xFF00FF00) >> 8) | ((x & 0x00FF00FF) << 8)
+        x = ((x & 0xF0F0F0F0) >> 4) | ((x & 0x0F0F0F0F) << 4)
+        x = ((x & 0xCCCCCCCC) >> 2) | ((x & 0x33333333) << 2)
+        with open(f"{prefix}.index{suf}.bwt", "wb") as f:
+            f.write(np.concatenate([[isa0], np.asarray(Cc, np.uint32)[1:5]]).astype(np.uint32).tobytes())
+            f.write(x.astype(np.uint32).tobytes())
+        del x
+        subprocess.run([os.path.join(REF_DIR, "ref_probe"), "mkfmv", f"{prefix}.index{suf}.bwt",
+                        f"{prefix}.index{suf}.fmv"], check=True, timeout=600)
+    index_build.write_sa(prefix, T, res[0][1], res[0][2], SA_INTERVAL, extra["sa"])
+    # .pac: 4 codes per byte, first code in the high bits (text words are LSB-first)
+    b = extra["text"].view(np.uint8)
+    b = ((b & 3) << 6) | ((b & 12) << 2) | ((b >> 2) & 12) | (b >> 6)
+    nb = (T + 3) // 4
+    body = b[:nb].copy()
+    if T % 4:
+        body[-1] &= np.uint8((0xFF << (8 - 2 * (T % 4))) & 0xFF)
+    with open(f"{prefix}.index.pac", "wb") as f:
+        f.write(body.tobytes())
+        f.write((b"\x00" if T % 4 == 0 else b"") + bytes([T % 4]))
+    recs = synth.record_layout(T, RECORDS)
+    ann = [(f"chr{r + 1}", [(s0, s0 + n - 1, 0)]) for r, (s0, n) in enumerate(recs)]
+    with open(f"{prefix}.index.ann", "w") as f:
+        f.write(index_build.ann_text(ann, T))
+    return prefix
+
+
+def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
+    """The reference's own bwa_cal_sa_reg_gap on the box's cores, and the drop-in end to
+    end (ref_probe_gpu), on the same index files; returns the bench fields."""
+    import shutil
+    import subprocess
+    import tempfile
+    probe, probe_gpu = os.path.join(REF_DIR, "ref_probe"), os.path.join(REF_DIR, "ref_probe_gpu")
+    if not (os.path.exists(probe) and os.path.exists(probe_gpu)):
+        return {"skipped": "oracle/_ref/ref_probe(_gpu) not built"}
+    d = tempfile.mkdtemp(prefix="hsa_ref_")
+    try:
+        t0 = time.time()
+        prefix = reference_files(d, T, res, extra)
+        log(f"[bench] reference index files written in {time.time() - t0:.1f} s")
+        # the reference: `procs` processes (one core each; it is single-threaded,
+        # bwtaln.c:307-311), each one batch of n_ref / procs reads
+        per = max(1, n_ref // procs)
+        jobs = []
+        for k in range(procs):
+            rb = os.path.join(d, f"ref_reads{k}.bin")
+            write_reads_bin(rb, reads_all[k * per:(k + 1) * per])
+            jobs.append(subprocess.Popen([probe, "aln", prefix, rb, os.path.join(d, f"ref_out{k}.bin"), *opt_args,
+                                          "-B", str(REF_BATCH)], stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+        ts = []
+        for k, j in enumerate(jobs):
+            o, e = j.communicate(timeout=900)
+            if j.returncode != 0:
+                raise RuntimeError(f"ref_probe rank {k}: {e.decode()[-500:]}")
+            ts.append(float(o.decode().split()[-1]))
+        ref = {"value": round(per * procs / max(ts), 1), "unit": "reads/s", "cores": procs, "kind": "reference",
+               "value_1core": round(per / float(np.median(ts)), 1),
+               "sample": f"the reference's own bwa_cal_sa_reg_gap (oracle/_ref/ref_probe, gcc -O3 from its sources) "
+                         f"on {procs} processes x {per} reads of the timed batch, one core each (the reference is "
+                         f"single-threaded), index files from the device-built BWTs; search seconds per process "
+                         f"{min(ts):.1f}-{max(ts):.1f} (index load excluded)"}
+        log(f"[bench] reference CPU path: {ref['value']:.0f} reads/s on {procs} cores ({ref['value_1core']:.0f} per core)")
+        # the drop-in end to end on the same files: bwa_seq_t batches of 100 000 reads
+        rb = os.path.join(d, "e2e_reads.bin")
+        write_reads_bin(rb, reads_all[:e2e_reads])
+        env = dict(os.environ, HSA_VERBOSE="1")
+        j = subprocess.run([probe_gpu, "aln", prefix, rb, os.path.join(d, "gpu_out.bin"), *opt_args, "-B",
+                            str(REF_BATCH)], capture_output=True, timeout=900, env=env)
+        if j.returncode != 0:
+            raise RuntimeError(f"ref_probe_gpu: {j.stderr.decode()[-800:]}")
+        t_gpu = float(j.stdout.decode().split()[-1])
+        err = j.stderr.decode()
+        splice_s, n_fb = 0.0, 0
+        for ln in err.splitlines():
+            if ln.startswith("[hsa] batch of"):
+                parts = ln.replace(",", "").split()
+                splice_s += float(parts[parts.index("path") + 1])
+                n_fb += int(ln.split("(")[-1].split()[0])
+        # parity through the real entry point: rank 0's reads are a prefix of the first
+        # 100 000-read batch in both runs, so their hits (splice path's included) agree
+        g_n, g_h = read_probe_out(os.path.join(d, "gpu_out.bin"))
+        r_n, r_h = read_probe_out(os.path.join(d, "ref_out0.bin"))
+        m = len(r_n)
+        go = np.concatenate([[0], np.cumsum(np.maximum(g_n, 0).astype(np.int64))])
+        ro = np.concatenate([[0], np.cumsum(np.maximum(r_n, 0).astype(np.int64))])
+        bad = [i for i in range(m) if g_n[i] != r_n[i] or not np.array_equal(g_h[go[i]:go[i + 1]], r_h[ro[i]:ro[i + 1]])]
+        e2e = {"reads": e2e_reads, "reads_per_call": REF_BATCH, "value": round(e2e_reads / t_gpu, 1), "unit": "reads/s",
+               "seconds": round(t_gpu, 3), "splice_fallback_reads": n_fb, "splice_path_s": round(splice_s, 3),
+               "splice_path_us_per_fallback_read": round(1e6 * splice_s / n_fb, 1) if n_fb else None,
+               "what": "the reference's driver (ref_probe.c) linked with every drop-in entry point of ours "
+                       "(oracle/_ref/ref_probe_gpu, as HSA_gpu_all): bwa_cal_sa_reg_gap on bwa_seq_t batches from "
+                       "host memory, the reference's bwt_splice_match for the fallback reads with our seed searches, "
+                       "extensions, widths and SA lookups inside; wall time of the calls",
+               "parity_vs_reference": {"reads": m, "mismatching_reads": len(bad), "first_mismatch": bad[0] if bad else None,
+                                       "fields": "n_aln and every bwt_aln1_t field of every hit, splice-path hits "
+                                                 "included, hit order"}}
+        log(f"[bench] drop-in end to end: {e2e['value']:.0f} reads/s ({e2e_reads} reads in calls of {REF_BATCH}, "
+            f"{n_fb} fallback reads, splice path {splice_s:.3f} s); {len(bad)} of {m} reads differ from the reference")
+        return {"reference": ref, "dropin_e2e": e2e}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,8 +505,19 @@ def main():
                          "and 32 with config 5's reads on one are A/B runs of the two instantiations")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0)
+    ap.add_argument("--ref-sample", type=int, default=-1,
+                    help="reads the REFERENCE's own CPU path (oracle/_ref/ref_probe) searches, over --ref-procs "
+                         "processes (-1: 64 000 for config 2, 16 000 for config 3; 0: skip the reference legs)")
+    ap.add_argument("--ref-procs", type=int, default=0, help="reference processes (0: the CPU threads of the share)")
+    ap.add_argument("--e2e-reads", type=int, default=1_000_000,
+                    help="reads of the drop-in end-to-end leg (oracle/_ref/ref_probe_gpu, 100 000 per call)")
+    ap.add_argument("--rank-parity", type=int, default=100_000,
+                    help="with N > 1 ranks: reads of each rank's timed batch checked against the restatement")
     a = ap.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
 
+    import hsa_amd  # noqa: F401  (libhsa_gpu.so before torch)
     import torch
     import torch.distributed as dist
     from hsa_amd import _lib, synth
@@ -284,8 +536,14 @@ def main():
     T = a.genome or (GENOME5_T if a.config == 5 else GENOME_T)
     RL = {4: 150, 5: 250}.get(a.config, READ_LEN)
     HW = _lib.ALN64_WORDS if wide else 9      # u32 words per hit record
+    if a.ref_sample < 0:
+        a.ref_sample = {2: 64_000, 3: 16_000}.get(a.config, 0)
+    ref_legs = rank == 0 and world == 1 and a.config in (2, 3) and not wide and a.ref_sample > 0 and T < (1 << 32)
     t0 = time.time()
-    gi, res = (build_index64 if wide else build_index)(T, GENOME_SEED, device)
+    if wide:
+        gi, res, extra = build_index64(T, GENOME_SEED, device)
+    else:
+        gi, res, extra = build_index(T, GENOME_SEED, device, with_files=ref_legs)
     log(f"[bench] rank {rank}: index ready ({gi.nbytes() / 2**30:.2f} GiB of rank blocks) in {time.time() - t0:.1f} s")
 
     # reads: rank r searches batches r, r+world, ... of one global stream (seed 5)
@@ -432,22 +690,36 @@ def main():
     fallback = int(((flags & 1) != 0).sum())
     reads_local = a.steps * a.batch
 
-    # final hit-list gather to rank 0 (RCCL over xGMI): each rank's last searched
-    # read set, as whole batches (hsa_amd/shard.py), then the counters
+    # final hit-list gather to rank 0 (RCCL over xGMI): every read set the timed steps
+    # searched (each is one global batch; a read set searched twice gives the same
+    # hits), then the counters.  Every rank also sends a digest of each of its batches,
+    # and rank 0 checks the gathered lists against them.
     total_hits_local = int(ctr[:, 1].sum())
+    gather = None
     if world > 1:
         from hsa_amd import shard
-        last_j = (a.warmup + a.steps - 1) % nd
-        last = outs[last_j]
-        nh_last = int(last["c"][1].item())
-        gidx = (a.warmup + a.steps - 1) * world + rank          # global batch index of that launch
-        res = {gidx: (last["n"].cpu().numpy(), last["f"].cpu().numpy().view(np.uint32), last["o"].cpu().numpy(),
-                      last["h"][:nh_last * HW].cpu().numpy().view(np.uint32).reshape(-1, HW))}
+        mine, digests = {}, {}
+        for j in used:
+            o = outs[j]
+            nh = int(o["c"][1].item())
+            n_j, f_j, ho_j = o["n"].cpu().numpy(), o["f"].cpu().numpy().view(np.uint32), o["o"].cpu().numpy()
+            h_j = o["h"][:nh * HW].cpu().numpy().view(np.uint32).reshape(-1, HW)
+            gidx = j * world + rank                                 # global batch index of read set j
+            mine[gidx] = (n_j, f_j, ho_j, h_j)
+            digests[gidx] = batch_digest(n_j, f_j, hits_in_read_order(n_j, ho_j, h_j))
         t0 = time.perf_counter()
-        g = shard.gather_to_root(res, dist, torch.device("cuda", local))
+        g = shard.gather_to_root(mine, dist, torch.device("cuda", local), per_batch=True)
+        t_gather = time.perf_counter() - t0
+        all_dig = [None] * world
+        dist.all_gather_object(all_dig, digests)
         if rank == 0:
-            log(f"[bench] gathered {len(g[0])} reads / {len(g[2])} hits from {world} ranks in "
-                f"{(time.perf_counter() - t0) * 1e3:.1f} ms")
+            want = {b: h for d in all_dig for b, h in d.items()}
+            bad = sorted(b for b in want if b not in g or batch_digest(g[b][0], g[b][1], g[b][2]) != want[b])
+            gather = {"batches": len(g), "reads": int(sum(len(v[0]) for v in g.values())),
+                      "hits": int(sum(len(v[2]) for v in g.values())), "ms": round(t_gather * 1e3, 1),
+                      "batches_differing_from_rank_digest": bad, "backend": dist.get_backend()}
+            log(f"[bench] gathered {gather['batches']} batches / {gather['reads']} reads / {gather['hits']} hits from "
+                f"{world} ranks in {gather['ms']} ms; {len(bad)} differ from their rank's digest")
         cnt = torch.tensor([total_hits_local, mapped, fallback], dtype=torch.int64, device="cuda")
         dist.all_reduce(cnt)
         mapped_all, fallback_all = int(cnt[1].item()), int(cnt[2].item())
@@ -513,6 +785,8 @@ def main():
         if a.config == 4:
             result["seed_rank_queries_per_read"] = round(seed_queries / reads_local, 1)
             result["roofline"]["splice_seeds_ms"] = round(float(np.mean(seeds_ms)), 3)
+        if gather is not None:
+            result["gather"] = gather
 
     # the drop-in path (rank 0, N=1, configs 2 and 3): the C-ABI bwa_cal_sa_reg_gap
     # (flat form) on HOST arrays, the way a host HSA aln calls it -- reads copied in,
@@ -537,6 +811,32 @@ def main():
         result["dropin"] = {"unit": "reads/s", "reads_per_call": dres,
                             "what": "hsa_cal_sa_reg_gap_flat on host arrays: H2D reads, widths + search + "
                                     "re-runs, D2H hits, per-read unpacking (PCIe and host work included)"}
+
+    # N > 1: every rank checks a sample of its own timed batch against the restatement
+    # (host threads of its share), rank 0 reports them all
+    if world > 1 and a.rank_parity and a.config != 4:
+        ox = (host_oracle_index64 if wide else host_oracle_index)(res, T)
+        from oracle_ctypes import default_opt
+        od = default_opt()
+        od.update(max_diff=4, fnr=-1.0, max_gapo=max_gapo, mode=od["mode"] & ~0x01)
+        j0 = a.warmup % nd
+        n = min(a.rank_parity, a.batch)
+        o = outs[j0]
+        t0 = time.perf_counter()
+        o_n, o_f, o_h, o_q = oracle_threaded(ox, batches[j0][:n], RL, od, cpu_info()["threads"])
+        bad, first = compare_batch(o["n"].cpu().numpy()[:n], o["f"].cpu().numpy().astype(np.uint32)[:n],
+                                   o["o"].cpu().numpy(), o["h"].cpu().numpy().view(np.uint32).reshape(-1, HW),
+                                   o_n, o_f, o_h)
+        log(f"[bench] rank {rank}: parity sample {n} reads, {bad} differ ({time.perf_counter() - t0:.1f} s)")
+        pr = [None] * world
+        dist.all_gather_object(pr, (rank, n, bad, first))
+        if rank == 0:
+            result["parity_ranks"] = {str(r): {"reads": nn, "mismatching_reads": b, "first_mismatch": f}
+                                      for r, nn, b, f in pr}
+            result["parity_ranks_against"] = ("oracle (C restatement" + (", 64-bit)" if wide else ")") +
+                                              ": the first reads of each rank's first timed read set; every field of "
+                                              "every hit, hit order, fallback flags")
+        del ox
 
     # parity and the CPU baseline (rank 0 at N=1 only): configs 2 and 3 compare the
     # WHOLE timed batch with the C restatement run on the host's cores (that run is
@@ -578,13 +878,15 @@ def main():
                 t1 = time.perf_counter()
                 ox.cal_sa_reg_gap(np.full(n1, RL, np.uint32), rs.reshape(-1), Opt.from_dict(od))
                 dt1 = time.perf_counter() - t1
+                share = (f"{threads} threads: the box's CPU share for one GPU (worker pools are capped at 16 per GPU; "
+                         f"{cpu['physical_cores']} physical cores are visible)")
                 result["cpu_baseline"] = {
                     "value": round(n / dt, 1), "unit": "reads/s", "cores": threads, "kind": "port",
                     "value_1core": round(n1 / dt1, 1), "cpu_model": cpu["model"],
                     "physical_cores_visible": cpu["physical_cores"], "affinity_cpus": cpu["affinity"],
-                    "sample": f"the whole timed batch ({n} reads) on the bwa_cal_sa_reg_gap restatement, "
-                              f"{threads} threads on disjoint chunks, {dt:.1f} s (the parity run above); "
-                              f"1 thread: {n1} reads in {dt1:.1f} s"}
+                    "sample": f"the whole timed batch ({n} reads) on the bwa_cal_sa_reg_gap restatement (gcc -O3), "
+                              f"{share}, disjoint chunks, {dt:.1f} s (the parity run above); 1 thread: {n1} reads in "
+                              f"{dt1:.1f} s"}
         if a.config == 4 and a.parity_sample:
             n = 4000 if a.parity_sample < 0 else min(a.parity_sample, a.batch)
             r0 = batches[a.warmup % nd][:n]
@@ -630,6 +932,27 @@ def main():
                                       "sample": f"{n} reads of the same workload: bwa_cal_sa_reg_gap restatement + "
                                                 f"the 6 seed searches of its {int((fl & 1).sum())} fallback reads, "
                                                 f"1 thread, in {dt1:.1f} s"}
+    # the reference's own CPU path, and the drop-in end to end (rank 0, N=1, configs 2, 3)
+    if ref_legs:
+        procs = a.ref_procs or cpu_info()["threads"]
+        j0 = a.warmup % nd
+        opt_args = ["-n", "4", "-o", str(max_gapo)]
+        try:
+            legs = reference_legs(T, res, extra, batches[j0], opt_args, min(a.ref_sample, a.batch), procs,
+                                  min(a.e2e_reads, a.batch))
+        except Exception as ex:                       # reported, never fatal: a baseline
+            legs = {"error": f"{type(ex).__name__}: {ex}"[:400]}
+            log(f"[bench] reference legs failed: {legs['error']}")
+        if "reference" in legs:
+            port = result.get("cpu_baseline")
+            result["cpu_baseline"] = dict(legs["reference"])
+            if port:
+                result["cpu_baseline"].update(cpu_model=port["cpu_model"],
+                                              physical_cores_visible=port["physical_cores_visible"],
+                                              port={k: port[k] for k in ("value", "cores", "value_1core", "sample")})
+            result["dropin_e2e"] = legs["dropin_e2e"]
+        else:
+            result["reference_legs"] = legs
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -224,10 +224,17 @@ static int search_range(hsa_index_t *const *ixs, int n_ix, const hsa_regime_t *r
             jobs[q].off = offs[r] - offs[r0]; jobs[q].len = lens[r]; jobs[q].max_diff = jmd[r]; jobs[q].seed_len = jsl[r];
             jobs[q].regime = 0;
         }
-        const uint64_t c1 = offs[r1 - 1] + lens[r1 - 1];
+        /* the range's codes: from its lowest offset to its highest read end (the caller's
+         * offsets need not ascend; hsa_cal_sa_reg_gap_multi checked every read's bounds) */
+        uint64_t c0 = offs[r0], c1 = 0;
+        for (int r = r0; r < r1; ++r) {
+            if (offs[r] < c0) c0 = offs[r];
+            if (offs[r] + lens[r] > c1) c1 = offs[r] + lens[r];
+        }
+        for (int q = 0; q < n; ++q) jobs[q].off = offs[r0 + q] - c0;
         hsa_stats_t st;
         uint32_t *h = NULL;
-        const long tot = hsa_search_batch(ixs[0], rg + regime, 1, jobs, n, codes + offs[r0], (size_t)(c1 - offs[r0]),
+        const long tot = hsa_search_batch(ixs[0], rg + regime, 1, jobs, n, codes + c0, (size_t)(c1 - c0),
                                           n_aln + r0, flags + r0, hit_off + r0, &h, &st);
         free(jobs);
         if (tot < 0) return (int)tot;
@@ -262,8 +269,12 @@ static int search_range(hsa_index_t *const *ixs, int n_ix, const hsa_regime_t *r
         memset(p, 0, sizeof *p);
         p->ix = ixs[k]; p->rg = rg + regime; p->jobs = jobs + j0; p->n = j1 - j0;
         p->na = na + j0; p->fl = fl + j0; p->ho = ho + j0;
-        /* the part's codes only: offsets rebased to its first read */
-        const uint64_t c0 = jobs[j0].off, c1 = jobs[j1 - 1].off + jobs[j1 - 1].len;
+        /* the part's codes only: offsets rebased to its lowest one */
+        uint64_t c0 = jobs[j0].off, c1 = 0;
+        for (int j = j0; j < j1; ++j) {
+            if (jobs[j].off < c0) c0 = jobs[j].off;
+            if (jobs[j].off + jobs[j].len > c1) c1 = jobs[j].off + jobs[j].len;
+        }
         for (int j = j0; j < j1; ++j) jobs[j].off -= c0;
         p->codes = codes + c0; p->codes_len = (size_t)(c1 - c0);
         started[k] = k > 0 && pthread_create(&th[k], NULL, slot_run, p) == 0;
@@ -313,6 +324,14 @@ long hsa_cal_sa_reg_gap_multi(hsa_index_t *const *ixs, int n_ix, gap_opt_t *opt,
     if (n_ix < 1 || n_ix > HSA_MAX_SLOTS) { hsa_gpu_set_error_text("1 to 16 device slots"); return HSA_E_ARG; }
     *hits = NULL;
     if (stats) memset(stats, 0, sizeof *stats);
+    for (int r = 0; r < n; ++r)
+        if (offs[r] > codes_len || lens[r] > codes_len - offs[r]) {
+            char m[96];
+            snprintf(m, sizeof m, "read %d: codes [%llu, +%u) past codes_len %zu", r, (unsigned long long)offs[r],
+                     lens[r], codes_len);
+            hsa_gpu_set_error_text(m);
+            return HSA_E_ARG;
+        }
     gap_opt_t local = *opt;                                 /* :254 */
     opt->mode &= ~BWA_MODE_GAPE;                            /* :261 through aux->opt */
     int max_len = 0, same_len = 1;
@@ -739,8 +758,10 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
         }
         hsa_splice_wmemo_clear();
     }
-    if (saprefetched) {
-        if (getenv("HSA_VERBOSE")) {
+    /* the runner's rounds add their lookups to the SA table too: clear it after every
+     * batch that prefetched or ran the coroutine runner, so it never outgrows a batch */
+    if (saprefetched || (n_sr > 0 && hsa_splice_sa_clear)) {
+        if (getenv("HSA_VERBOSE") && hsa_splice_sa_stats) {
             uint64_t sh = 0, sm = 0;
             hsa_splice_sa_stats(&sh, &sm);
             fprintf(stderr, "[hsa] splice SA -> position: %llu lookups answered from the batch, %llu in the runner's "

@@ -39,6 +39,7 @@
 #include "bwtaln_gpu.h"
 
 #define CO_STACK (512u << 10)     /* C stack per coroutine (the host's splice code + ours) */
+#define CO_GUARD 4096u            /* PROT_NONE page under each coroutine stack */
 #define CO_MAX 16384              /* coroutines alive at once (= extension slots) */
 #define SLICE_POPS 256u           /* pops per call per launch (hsa_extend_sliced) */
 
@@ -677,8 +678,15 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     tl_sched = &sched;
     for (int k = 0; k < W; ++k) {
         co_t *c = co + k;
-        c->stack = mmap(NULL, CO_STACK, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-        if (c->stack == MAP_FAILED) { fprintf(stderr, "[hsa_splice_run] cannot map a coroutine stack\n"); exit(1); }
+        /* one guard page below each stack: an overflow faults instead of silently
+         * corrupting the neighbouring coroutine's stack */
+        void *m = mmap(NULL, CO_STACK + CO_GUARD, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
+                       -1, 0);
+        if (m == MAP_FAILED || mprotect(m, CO_GUARD, PROT_NONE)) {
+            fprintf(stderr, "[hsa_splice_run] cannot map a coroutine stack\n");
+            exit(1);
+        }
+        c->stack = (char *)m + CO_GUARD;
         c->aux.bi_bwt = (Idx2BWT *)bi;
         c->aux.arr = arr;
         c->aux.max_len = max_len;
@@ -697,6 +705,7 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     int *sa_co = (int *)malloc(sizeof(int) * (size_t)W);
     long sa_launches = 0;
     int32_t *pslot = (int32_t *)malloc(sizeof(int32_t) * (size_t)W);
+    int *wide = (int *)malloc(sizeof(int) * (size_t)W);
     uint8_t *pdone = (uint8_t *)malloc((size_t)W);
     int next = 0, live = 0;
     long launches = 0, calls = 0;
@@ -724,13 +733,30 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
             }
         }
         /* one sliced launch over every parked call (slot = its coroutine): the finished
-         * ones resume, the others stay parked with their state on the device */
-        int np = 0, nsa = 0;
+         * ones resume, the others stay parked with their state on the device.  A call
+         * whose regime has more buckets than a slot holds (n_stacks > 256, e.g. -o 2
+         * -e 60) runs to completion in one hsa_extend_batch launch with the round's other
+         * such calls. */
+        int np = 0, nsa = 0, nwide = 0;
         for (int k = 0; k < W; ++k)
             if (co[k].read >= 0 && co[k].state == 1) {
                 if (co[k].req.kind == 1) { sa_idx[nsa] = co[k].req.sa; sa_co[nsa++] = k; }
+                else if (co[k].req.rg.n_stacks > HSA_EXT_SLICE_STACKS) wide[nwide++] = k;
                 else { pend[np] = &co[k].req; pslot[np++] = k; }
             }
+        if (nwide > 0) {
+            const double tw = hsa_now();
+            for (int j = 0; j < nwide; ++j) pend[j] = &co[wide[j]].req;
+            run_reqs(ix, pend, nwide);
+            for (int j = 0; j < nwide; ++j) co[wide[j]].state = 0;
+            t_gpu += hsa_now() - tw;
+            calls += nwide;
+            ++launches;
+            np = 0;                       /* pend is rebuilt below */
+            for (int k = 0; k < W; ++k)
+                if (co[k].read >= 0 && co[k].state == 1 && co[k].req.kind == 0 &&
+                    co[k].req.rg.n_stacks <= HSA_EXT_SLICE_STACKS) { pend[np] = &co[k].req; pslot[np++] = k; }
+        }
         if (nsa > 0) {                    /* the round's SA -> position lookups: one launch */
             const double ts = hsa_now();
             const int rc = hsa_sa_position_batch(ix, (size_t)nsa, sa_idx, sa_o4);
@@ -760,12 +786,12 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     }
     for (int k = 0; k < W; ++k) {
         co_t *c = co + k;
-        munmap(c->stack, CO_STACK);
+        munmap((char *)c->stack - CO_GUARD, CO_STACK + CO_GUARD);
         free(c->aux.width_back); free(c->aux.width_fore); free(c->aux.width_seed); free(c->aux.rc_seq);
         stack_free(c->aux.stack);
         free(c->req.buf);
     }
-    free(co); free(pend); free(pslot); free(pdone); free(sa_idx); free(sa_o4); free(sa_co);
+    free(co); free(pend); free(pslot); free(wide); free(pdone); free(sa_idx); free(sa_o4); free(sa_co);
     tl_sched = NULL;
     if (getenv("HSA_VERBOSE"))
         fprintf(stderr, "[hsa] splice runner: %d reads, %ld extension calls in %ld launches, %ld SA lookup launches: "

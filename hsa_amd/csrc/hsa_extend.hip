@@ -484,7 +484,7 @@ extern "C" int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, in
 // that needs more reports EXT_E_CAP / EXT_E_SCORE here and is re-run by the caller
 // through hsa_extend_batch.
 #define EXT_SLICE_CAP 2048u
-#define EXT_SLICE_NB 256u
+#define EXT_SLICE_NB ((uint32_t)HSA_EXT_SLICE_STACKS)
 
 extern "C" int hsa_extend_sliced(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_ext_job_t *jobs,
                                  const int32_t *slots, const uint8_t *resume, int n, const uint8_t *codes,

@@ -167,6 +167,12 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     if ((rc = jobs_limits(jobs, n_jobs, max_len, max_seed))) return rc;
     if (mh && (rc = mg_limits(jobs, mh->mg, n_jobs, *mh, max_seed))) return rc;
     if (codes_len >= 0xFFFFFFFFull) { hsa_set_error("read codes of one call must be < 4 GiB"); return HSA_E_ARG; }
+    for (int j = 0; j < n_jobs; ++j)        // the kernels read codes[off, off + len) of every job
+        if (jobs[j].off > codes_len || jobs[j].len > codes_len - jobs[j].off) {
+            hsa_set_error("job %d: codes [%llu, +%u) past codes_len %zu", j, (unsigned long long)jobs[j].off,
+                          jobs[j].len, codes_len);
+            return HSA_E_ARG;
+        }
     HSA_HIP(hipSetDevice(ix->device));
     hipStream_t st = ix->stream;
     if (stats) memset(stats, 0, sizeof *stats);

@@ -94,12 +94,20 @@ def pack(res: dict) -> np.ndarray:
     for b in sorted(res):
         n_aln, flags, hoff, hits = res[b]
         n = len(n_aln)
-        hw = int(np.asarray(hits).shape[1]) if np.asarray(hits).ndim == 2 else 9
+        hits = np.asarray(hits, np.uint32)
+        hw = int(hits.shape[1]) if hits.ndim == 2 else 9
+        hits = hits.reshape(-1, hw)
         # hits in read order (hit_off may point anywhere in the batch's hit array)
-        order = [np.asarray(hits[int(hoff[j]):int(hoff[j]) + max(int(n_aln[j]), 0)], np.uint32) for j in range(n)]
-        h = np.concatenate(order) if order else np.zeros((0, hw), np.uint32)
-        parts += [np.array([b, n, len(h), hw], np.int32), np.asarray(n_aln, np.int32),
-                  np.asarray(flags, np.uint32).view(np.int32), h.reshape(-1).view(np.int32)]
+        cnt = np.maximum(np.asarray(n_aln, np.int64), 0)
+        tot = int(cnt.sum())
+        if tot:
+            idx = np.repeat(np.asarray(hoff, np.int64) - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt) + \
+                np.arange(tot)
+            h = hits[idx]
+        else:
+            h = np.zeros((0, hw), np.uint32)
+        parts += [np.array([b, n, tot, hw], np.int32), np.asarray(n_aln, np.int32),
+                  np.asarray(flags, np.uint32).view(np.int32), np.ascontiguousarray(h).reshape(-1).view(np.int32)]
     return np.concatenate(parts) if parts else np.zeros(0, np.int32)
 
 
@@ -118,10 +126,10 @@ def unpack(buf: np.ndarray) -> dict:
     return out
 
 
-def gather_to_root(res: dict, dist, device, root: int = 0):
+def gather_to_root(res: dict, dist, device, root: int = 0, per_batch: bool = False):
     """Gather every rank's packed results to `root` (sizes first, then one padded
-    gather).  Returns (n_aln, flags, hits) over all reads in global order on root,
-    None elsewhere."""
+    gather).  Returns (n_aln, flags, hits) over all reads in global order on root (or,
+    with per_batch, {batch: (n_aln, flags, hits)}), None elsewhere."""
     import torch
     mine = torch.from_numpy(pack(res)).to(device)
     world = dist.get_world_size()
@@ -139,6 +147,8 @@ def gather_to_root(res: dict, dist, device, root: int = 0):
     allres = {}
     for r in range(world):
         allres.update(unpack(bufs[r][:int(sizes[r].item())].cpu().numpy()))
+    if per_batch:
+        return allres
     bs = sorted(allres)
     n_aln = np.concatenate([allres[b][0] for b in bs]) if bs else np.zeros(0, np.int32)
     flags = np.concatenate([allres[b][1] for b in bs]) if bs else np.zeros(0, np.uint32)

@@ -138,9 +138,12 @@ int hsa_extend_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes
  * ret[j]: 1, 2, -1 (finished: max_pos / aln_out valid), HSA_EXT_CONT (not finished:
  * submit it again with resume set), HSA_EXT_E_CAP (needs more stack than a slot holds:
  * run it through hsa_extend_batch), or another negative code (undefined in the
- * reference).  The job's aln is always the call's original hit.  n_stacks <= 256. */
+ * reference).  The job's aln is always the call's original hit.  Every regime's
+ * n_stacks must be <= HSA_EXT_SLICE_STACKS (a slot's bucket heads); a caller with a
+ * larger regime runs those calls through hsa_extend_batch. */
 #define HSA_EXT_CONT  (-999)
 #define HSA_EXT_E_CAP (-1001)
+#define HSA_EXT_SLICE_STACKS 256
 int hsa_extend_sliced(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_ext_job_t *jobs,
                       const int32_t *slots, const uint8_t *resume, int n, const uint8_t *codes, const int32_t *bids,
                       size_t win_len, int n_slots, uint32_t budget, int32_t *ret, int32_t *max_pos, uint32_t *aln_out);

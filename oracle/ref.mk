@@ -15,7 +15,8 @@ REFOBJS   = bwtaln bwtgap BWT BWTConstruct utils dictionary DNACount HSP inipars
             bamlite 2BWT-Interface bwaseqio r250 cs2nt bwtse kstring stdaln bwt_array
 OBJS      = $(addprefix $(OUT)/obj/,$(addsuffix .o,$(REFOBJS)))
 
-all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/ref_mgcap $(OUT)/ref_extcap $(OUT)/HSA_gpu $(OUT)/HSA_gpu_mg $(OUT)/HSA_gpu_all
+all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/ref_mgcap $(OUT)/ref_extcap $(OUT)/HSA_gpu $(OUT)/HSA_gpu_mg $(OUT)/HSA_gpu_all \
+     $(OUT)/ref_probe_gpu
 
 $(OUT)/obj/%.o: $(REF)/%.c
 	@mkdir -p $(OUT)/obj
@@ -124,6 +125,13 @@ GPUOBJ_EX = $(CURDIR)/../hsa_amd/csrc/bwtext_gpu.o
 $(OUT)/HSA_gpu_all: $(OUT)/obj/main.o $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) $(GPUOBJ_EX) $(GPULIB)
 	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) $(GPUOBJ_EX) \
 	    -L$(dir $(GPULIB)) -lhsa_gpu -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
+
+# ref_probe_gpu: ref_probe.c linked as HSA_gpu_all (every drop-in entry point ours, the
+# reference's bwt_splice_match in between): bench.py times the drop-in end to end on
+# bwa_seq_t batches with it and compares its hits with ref_probe's, read for read.
+$(OUT)/ref_probe_gpu: ref_probe.c $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) $(GPUOBJ_EX) $(GPULIB)
+	$(CC) $(REFFLAGS) -DHSA_GPU_PROBE -I$(REF) ref_probe.c $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) \
+	    $(GPUOBJ_EX) -L$(dir $(GPULIB)) -lhsa_gpu -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
 
 clean:
 	rm -rf $(OUT)

@@ -26,8 +26,21 @@
  *       the block search finds nothing).
  *   ref_probe meta  <prefix>
  *       prints textLength, inverseSa0, C[0..4] of both BWTs and saInterval.
+ *   ref_probe mkfmv <in.bwt> <out.fmv>
+ *       the .fmv (occValue + occValueMajor) of a .bwt file, by the reference's own
+ *       BWTGenerateOccValueFromBwt (BWTConstruct.c:997) and the occ half of
+ *       BWTSaveBwtCodeAndOcc's format (BWTConstruct.c:1209-1240): how bench.py turns a
+ *       device-built BWT into index files the reference's BWTLoad reads.
  *
  * reads.bin: u32 n, u32 len[n], then the concatenated 0..4 codes.
+ *
+ * Built a second time as ref_probe_gpu (-DHSA_GPU_PROBE, oracle/ref.mk): the same driver
+ * linked like HSA_gpu_all, i.e. the reference's objects with every drop-in entry point
+ * replaced by ours (bwa_cal_sa_reg_gap, bwt_match_gap, the splice path's extensions,
+ * widths and SA lookups) and the reference's own bwt_splice_match in between.  Its `aln`
+ * times the drop-in end to end on bwa_seq_t batches, splice fallback included, and
+ * writes the same out.bin, so the two outputs can be compared read for read (bit 0 of
+ * flags is not recorded there).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -36,6 +49,8 @@
 #include <sys/time.h>
 #include "bwtaln.h"
 #include "bwtgap.h"
+#include "BWTConstruct.h"
+#include "DNACount.h"
 
 static double now_s(void) { struct timeval tv; gettimeofday(&tv, 0); return tv.tv_sec + tv.tv_usec * 1e-6; }
 
@@ -73,8 +88,11 @@ static Idx2BWT *load_index(const char *prefix)
     return b;
 }
 
-/* --wrap=bwt_splice_match: record the read the batch driver is on. */
 static bwa_seq_t *g_seqs; static int g_nseqs; static int g_cursor; static uint32_t *g_flags;
+#ifdef HSA_GPU_PROBE
+int hsa_gpu_attach(const Idx2BWT *bi);      /* the drop-in's upload hook (include/hsa_bwtaln.h) */
+#else
+/* --wrap=bwt_splice_match: record the read the batch driver is on. */
 bwt_aln1_t *__real_bwt_splice_match(bwt_aux_t *aux, int *n);
 bwt_aln1_t *__wrap_bwt_splice_match(bwt_aux_t *aux, int *n)
 {
@@ -82,6 +100,7 @@ bwt_aln1_t *__wrap_bwt_splice_match(bwt_aux_t *aux, int *n)
         if (g_seqs[g_cursor].seq == aux->seq) { g_flags[g_cursor] |= 1; break; }
     return __real_bwt_splice_match(aux, n);
 }
+#endif
 
 static int cmd_aln(int argc, char **argv)
 {
@@ -113,6 +132,14 @@ static int cmd_aln(int argc, char **argv)
     Idx2BWT *bi = load_index(argv[1]);
     bwt_array_t *arr = bwt_array_init();
     reads_t r = load_reads(argv[2]);
+#ifdef HSA_GPU_PROBE
+    {   /* the index upload (hook after BWTLoad2BWT, bwtaln.c:467) stays outside the timing */
+        const double ta = now_s();
+        const int rc = hsa_gpu_attach(bi);
+        if (rc) { fprintf(stderr, "hsa_gpu_attach failed (%d)\n", rc); return 1; }
+        fprintf(stderr, "[ref_probe_gpu] index attached in %.3f s\n", now_s() - ta);
+    }
+#endif
     FILE *out = fopen(argv[3], "wb");
     uint32_t magic = 0x48415348u; fwrite(&magic, 4, 1, out); fwrite(&r.n, 4, 1, out);
     double t_search = 0;
@@ -142,7 +169,12 @@ static int cmd_aln(int argc, char **argv)
         free(seqs); free(flags);
     }
     fclose(out);
-    fprintf(stderr, "[ref_probe] bwa_cal_sa_reg_gap: %u reads in %.3f s (%.1f reads/s)\n",
+    fprintf(stderr, "[ref_probe%s] bwa_cal_sa_reg_gap: %u reads in %.3f s (%.1f reads/s)\n",
+#ifdef HSA_GPU_PROBE
+            "_gpu",
+#else
+            "",
+#endif
             r.n, t_search, t_search > 0 ? r.n / t_search : 0.0);
     printf("%.6f\n", t_search);
     return 0;
@@ -234,6 +266,42 @@ static int cmd_meta(int argc, char **argv)
     return 0;
 }
 
+static int cmd_mkfmv(int argc, char **argv)
+{
+    if (argc < 3) { fprintf(stderr, "usage: mkfmv in.bwt out.fmv\n"); return 1; }
+    FILE *f = fopen(argv[1], "rb");
+    if (!f) { fprintf(stderr, "cannot open %s\n", argv[1]); return 1; }
+    unsigned int cf[ALPHABET_SIZE + 1] = {0}, isa0 = 0;
+    if (fread(&isa0, 4, 1, f) != 1 || fread(cf + 1, 4, ALPHABET_SIZE, f) != ALPHABET_SIZE) { fprintf(stderr, "short .bwt\n"); return 1; }
+    BWT b;
+    memset(&b, 0, sizeof b);
+    b.textLength = cf[ALPHABET_SIZE];
+    b.inverseSa0 = isa0;
+    b.cumulativeFreq = cf;
+    b.bwtSizeInWord = BWTResidentSizeInWord(b.textLength) + WORD_BETWEEN_OCC / 2;      /* as BWTLoad, BWT.c:176 */
+    b.bwtCode = (unsigned int *)calloc(b.bwtSizeInWord, 4);
+    const unsigned int nw = BWTFileSizeInWord(b.textLength);
+    if (fread(b.bwtCode, 4, nw, f) != nw) { fprintf(stderr, "short .bwt codes\n"); return 1; }
+    fclose(f);
+    BWTClearTrailingBwtCode(&b);
+    b.occSizeInWord = BWTOccValueMinorSizeInWord(b.textLength);
+    b.occMajorSizeInWord = BWTOccValueMajorSizeInWord(b.textLength);
+    b.occValue = (unsigned int *)calloc(b.occSizeInWord, 4);
+    b.occValueMajor = (unsigned int *)calloc(b.occMajorSizeInWord, 4);
+    unsigned int *dt = (unsigned int *)malloc(DNA_OCC_CNT_TABLE_SIZE_IN_WORD * sizeof(unsigned int));
+    GenerateDNAOccCountTable(dt);
+    BWTGenerateOccValueFromBwt(b.bwtCode, b.occValue, b.occValueMajor, b.textLength, dt);
+    FILE *o = fopen(argv[2], "wb");
+    if (!o) { fprintf(stderr, "cannot write %s\n", argv[2]); return 1; }
+    fwrite(&b.inverseSa0, 4, 1, o);
+    fwrite(cf + 1, 4, ALPHABET_SIZE, o);
+    fwrite(b.occValue, 4, b.occSizeInWord, o);
+    fwrite(b.occValueMajor, 4, b.occMajorSizeInWord, o);
+    fclose(o);
+    free(b.bwtCode); free(b.occValue); free(b.occValueMajor); free(dt);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 3) { fprintf(stderr, "usage: ref_probe aln|occ|step|width|meta ...\n"); return 1; }
@@ -243,6 +311,7 @@ int main(int argc, char **argv)
     if (!strcmp(argv[1], "width")) return cmd_width(argc - 1, argv + 1);
     if (!strcmp(argv[1], "meta")) return cmd_meta(argc - 1, argv + 1);
     if (!strcmp(argv[1], "sa")) return cmd_sa(argc - 1, argv + 1);
+    if (!strcmp(argv[1], "mkfmv")) return cmd_mkfmv(argc - 1, argv + 1);
     fprintf(stderr, "unknown command %s\n", argv[1]);
     return 1;
 }

@@ -47,3 +47,50 @@ def test_compare_batch_identical_and_single_field_change():
 def test_cpu_info_fields():
     c = bench.cpu_info()
     assert 1 <= c["threads"] <= 16 and c["affinity"] >= 1 and isinstance(c["model"], str)
+
+
+def test_hits_in_read_order_and_digest():
+    rng = np.random.default_rng(5)
+    o_n, o_f, o_h, g_n, g_f, g_o, g_h = _scrambled(rng, 300)
+    assert np.array_equal(bench.hits_in_read_order(g_n, g_o, g_h), o_h)
+    d = bench.batch_digest(o_n, o_f, o_h)
+    assert d == bench.batch_digest(g_n, g_f, bench.hits_in_read_order(g_n, g_o, g_h))
+    h2 = o_h.copy()
+    h2[3, 4] ^= 1
+    assert bench.batch_digest(o_n, o_f, h2) != d
+
+
+def test_shard_pack_roundtrip_scrambled():
+    """shard.pack puts each read's hits in read order whatever the kernel's layout."""
+    from hsa_amd import shard
+    rng = np.random.default_rng(8)
+    o_n, o_f, o_h, g_n, g_f, g_o, g_h = _scrambled(rng, 400)
+    out = shard.unpack(shard.pack({7: (g_n, g_f, g_o, g_h)}))
+    n_aln, flags, hits = out[7]
+    assert np.array_equal(n_aln, o_n) and np.array_equal(flags, o_f) and np.array_equal(hits, o_h)
+
+
+def test_spawn_ranks_sets_rank_env(tmp_path):
+    """`bench.py --gpus N` without a launcher starts N ranks with the rendezvous
+    environment and relays rank 0's stdout (a stand-in script here: no GPU)."""
+    script = tmp_path / "rank.py"
+    script.write_text("import json, os, sys\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "assert os.environ['LOCAL_RANK'] == str(r) and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "if r == 0: print(json.dumps({'world': int(os.environ['WORLD_SIZE']), 'argv': sys.argv[1:]}))\n")
+    import contextlib
+    import io
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = bench.spawn_ranks(3, ["--gpus", "3"], script=str(script))
+    assert rc == 0
+    import json
+    assert json.loads(buf.getvalue()) == {"world": 3, "argv": ["--gpus", "3"]}
+
+
+def test_spawn_ranks_reports_a_failing_rank(tmp_path):
+    script = tmp_path / "fail.py"
+    script.write_text("import os, sys, time\n"
+                      "if os.environ['RANK'] == '1': sys.exit(3)\n"
+                      "time.sleep(30)\n")
+    assert bench.spawn_ranks(2, [], script=str(script)) == 3

@@ -6,9 +6,10 @@ which the reference's 32-bit bwtint_t cannot index, 2BWT-Interface.h:26).
   golden hits, the 32-bit kernels on the same index, and the 64-bit oracle;
 * ranks past 2^32: hsa_occ4_batch64 on a 4.3 G-character code string equals the
   64-bit oracle at random positions and at every boundary the layout has (2^32, the
-  2^24 superblocks, the '$' row);
+  count-wrap blocks of the wrap table, the '$' row);
 * search past 2^32: a device-built BWT of a 4.3 Gbp synthetic text, reads from the
-  whole text, -n 4 -o 1: every hit equals the 64-bit oracle's (liboracle64.so, the
+  whole text, -n 4 -o 1 (100 bp) and config 5's own instantiation (250 bp, -n 4 -o 0,
+  64-bit intervals with 4-bit pruning rows): every hit equals the 64-bit oracle's (liboracle64.so, the
   same restatement pinned against the 32-bit one in tests/test_oracle.py), and hits
   with SA bounds >= 2^32 occur.  No reference output exists at this size (the
   reference cannot index it): parity is against the restatement only."""
@@ -125,6 +126,43 @@ def test_wide_kernels_match_32bit_and_oracle(case):
         assert int(c64[2]) == int(st[0])
 
 
+# golden cases whose two option regimes coincide (no gap opens, or -e given: GAPE is
+# off from the start, bwtaln.c:261, :548), so a steady-state device batch reproduces
+# the reference's own run read for read
+STEADY_CASES = ["tiny_mm100_n4o0", "tiny_opts_seed", "tiny_exact36_n0", "tiny_edge_n3o1e3L", "tiny_opts_bigstack"]
+
+
+@pytest.mark.parametrize("case", STEADY_CASES)
+def test_wide_4bit_rows_match_reference(case, monkeypatch, capfd):
+    """hsa_search_device64 with the 4-bit pruning rows forced (HSA_WFMT=nib, exact for
+    these bounds) against the compiled reference's golden hits: every read that passes
+    the filters and does not fall to the splice path has the reference's bwt_aln1_t
+    list (the 64-bit records narrowed), and the fallback flags agree."""
+    from oracle_ctypes import aln64_to_aln32, default_opt
+    monkeypatch.setenv("HSA_WFMT", "nib")
+    monkeypatch.setenv("HSA_VERBOSE", "1")
+    g = load_case(case)
+    od = parse_opts(g["args"], default_opt())
+    od["mode"] &= ~0x01
+    offs = np.concatenate([[0], np.cumsum(g["lens"].astype(np.int64))])
+    keep = []
+    for r in range(len(g["lens"])):
+        sq = g["codes"][offs[r]:offs[r + 1]]
+        polyat = len(sq) >= 15 and ((sq[:15] == 0).all() or (sq[:15] == 3).all())
+        if int((sq > 3).sum()) <= od["max_diff"] and not polyat:
+            keep.append(r)
+    lens, codes = _device_jobs(g, od)
+    assert len(lens) == len(keep)
+    n64, f64, o64, h64, _ = search(index64(g["index"]), lens, codes, od, True)
+    assert "4-bit rows" in capfd.readouterr().err
+    exp = split_hits(g["n_aln"], g["hits"])
+    exp_splice = (g["flags"][keep] & 1).astype(bool)
+    assert np.array_equal((f64 & 1).astype(bool), exp_splice)
+    got = per_read(n64, o64, h64)
+    bad = [j for j, r in enumerate(keep) if not exp_splice[j] and not np.array_equal(aln64_to_aln32(got[j]), exp[r])]
+    assert not bad, f"{len(bad)} reads differ from the reference; first read {keep[bad[0]]}"
+
+
 def test_wide_index_serves_32bit_entry_points():
     """A sub-2^32 index made by hsa_index_create_device64 answers the 32-bit rank
     primitive exactly as hsa_index_create's, and the 64-bit one agrees."""
@@ -156,8 +194,9 @@ def _counts_lsb(w, T):
 
 def test_rank_past_2_32_matches_oracle():
     """Occ at 64-bit positions over a 4.3 G-character code string (random codes; the
-    rank structure does not need a BWT): random positions plus 2^32 +- 1, superblock
-    edges, the '$' row and T + 1."""
+    rank structure does not need a BWT): random positions plus 2^32 +- 1, multiples of
+    2^24 (the old superblock edges, kept as arbitrary far-apart probes), the '$' row and
+    T + 1."""
     import torch
     from hsa_amd._lib import GpuIndex, check, lib
     from oracle_ctypes import OracleIndex64
@@ -251,14 +290,15 @@ def test_rank_count_wraps_match_oracle():
     gi.close()
 
 
-def test_search_past_2_32_matches_oracle():
+@pytest.fixture(scope="module")
+def big_index():
     """A 4.3 Gbp synthetic text, its forward and reverse BWTs built on the device
-    (hsa_build_bwt_device64: u64 suffix positions), 2 000 reads of 100 bp from the
-    whole text with an indel or substitutions, -n 4 -o 1."""
+    (hsa_build_bwt_device64: u64 suffix positions), the 64-bit index over them and the
+    64-bit restatement's index over the same code words."""
     import torch
     from hsa_amd import synth
     from hsa_amd._lib import GpuIndex, check, lib
-    from oracle_ctypes import OracleIndex64, Opt, default_opt
+    from oracle_ctypes import OracleIndex64
     T = BIG_T
     nw = (T + 15) // 16
     text = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
@@ -278,15 +318,14 @@ def test_search_past_2_32_matches_oracle():
     host = [r[0][:nw].cpu().numpy().view(np.uint32) for r in res]
     ox = OracleIndex64(T, res[0][1], res[0][2], host[0], T, res[1][1], res[1][2], host[1])
     genome = synth.PackedGenome(T, 77)
-    recs = [(0, T)]
-    r1, _ = synth.make_reads(genome, recs, 1000, 100, 31, max_mm=3)
-    r2, _ = synth.make_reads(genome, recs, 1000, 100, 32, indel=True, max_mm_indel=1)
-    reads = np.concatenate([r1, r2])
-    lens = np.full(len(reads), 100, np.uint32)
+    yield gi, ox, genome
+    gi.close()
+
+
+def _check_past_2_32(gi, ox, reads, od, wide_hits=True):
+    from oracle_ctypes import Opt
+    lens = np.full(len(reads), reads.shape[1], np.uint32)
     codes = reads.reshape(-1)
-    od = default_opt()
-    od.update(max_diff=4, fnr=-1.0, max_gapo=1)
-    od["mode"] &= ~0x01
     g_n, g_f, g_o, g_h, ctr = search(gi, lens, codes, od, True)
     e_n, e_f, e_h, st = ox.cal_sa_reg_gap(lens, codes, Opt.from_dict(od))
     assert np.array_equal(g_n, e_n)
@@ -296,7 +335,50 @@ def test_search_past_2_32_matches_oracle():
     bad = [i for i in range(len(got)) if not np.array_equal(got[i], exp[i])]
     assert not bad, f"{len(bad)} reads differ from the 64-bit oracle; first {bad[0]}"
     assert int(ctr[2]) == int(st[0]), "rank queries"
+    assert int(ctr[4]) == int(st[1]), "gap_pop count"
     hits = np.concatenate([x for x in got if len(x)])
-    assert (hits[:, 3] > 0).any(), "no hit with k >= 2^32"
+    if wide_hits:
+        assert (hits[:, 3] > 0).any(), "no hit with k >= 2^32"
+    return e_n
+
+
+def test_search_past_2_32_matches_oracle(big_index):
+    """2 000 reads of 100 bp from the whole 4.3 Gbp text with an indel or
+    substitutions, -n 4 -o 1 (8-bit pruning rows, 64-bit intervals)."""
+    from hsa_amd import synth
+    from oracle_ctypes import default_opt
+    gi, ox, genome = big_index
+    recs = [(0, BIG_T)]
+    r1, _ = synth.make_reads(genome, recs, 1000, 100, 31, max_mm=3)
+    r2, _ = synth.make_reads(genome, recs, 1000, 100, 32, indel=True, max_mm_indel=1)
+    od = default_opt()
+    od.update(max_diff=4, fnr=-1.0, max_gapo=1)
+    od["mode"] &= ~0x01
+    e_n = _check_past_2_32(gi, ox, np.concatenate([r1, r2]), od)
     assert (e_n > 0).mean() > 0.9
-    gi.close()
+
+
+def test_config5_kernel_past_2_32_matches_oracle(big_index, monkeypatch, capfd):
+    """Config 5's own kernel instantiation: 250 bp reads, -n 4 -o 0, 64-bit intervals
+    AND 4-bit pruning rows (the planner picks them by itself for long ungapped reads,
+    as in the config-5 bench).  2 000 reads from the whole 4.3 Gbp text with 0-4
+    substitutions, half reverse-complemented (make_reads), 1 in 50 with an N; every
+    hsa_aln64_t field of every hit, the splice-fallback flags and the rank-query and pop
+    counts equal the 64-bit restatement's, and hits with SA bounds past 2^32 occur."""
+    from hsa_amd import synth
+    from oracle_ctypes import default_opt
+    monkeypatch.setenv("HSA_VERBOSE", "1")
+    monkeypatch.delenv("HSA_WFMT", raising=False)
+    gi, ox, genome = big_index
+    reads, _ = synth.make_reads(genome, [(0, BIG_T)], 2000, 250, 8 * 1_000_000 + 77, max_mm=4)
+    reads = reads.copy()
+    rng = np.random.default_rng(5)
+    for r in range(0, len(reads), 50):
+        reads[r, int(rng.integers(0, 250))] = 4
+    od = default_opt()
+    od.update(max_diff=4, fnr=-1.0, max_gapo=0)
+    od["mode"] &= ~0x01
+    e_n = _check_past_2_32(gi, ox, reads, od)
+    err = capfd.readouterr().err
+    assert "4-bit rows" in err, "config 5's 4-bit-row instantiation was not the one that ran"
+    assert (e_n > 0).mean() > 0.9

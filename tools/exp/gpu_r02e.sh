@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-PFX=c3_ BENCH_ARGS="--config 3 --steps 1" bash tools/exp_pcs.sh
+PFX=c3_ BENCH_ARGS="--config 3 --steps 1" bash tools/exp/exp_pcs.sh
 for iv in 32 64; do
   timeout -k 10 300 python -u bench.py --config 5 --genome 3000000005 --intervals $iv --steps 3 --warmup 1 --cpu-sample 0 --parity-sample 4000 --dropin 0 > gpurun_out/iv_$iv.json 2> gpurun_out/iv_$iv.err || { tail gpurun_out/iv_$iv.err; exit 2; }
   echo "iv=$iv: $(grep -h 'kernels\|parity:' gpurun_out/iv_$iv.err | tr '\n' ' ')"
