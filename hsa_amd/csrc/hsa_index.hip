@@ -341,6 +341,8 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     (void)hipFree(ix->blk_base[0]); (void)hipFree(ix->blk_base[1]);
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big); hsa_scratch_free(ix->huge);
     if (ix->d_ovf2) (void)hipFree(ix->d_ovf2);
+    if (ix->d_any) (void)hipFree(ix->d_any);
+    if (ix->d_any_aux) (void)hipFree(ix->d_any_aux);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
     (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);

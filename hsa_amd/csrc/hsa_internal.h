@@ -57,6 +57,9 @@ struct hsa_index {
     void *d_seed = nullptr; size_t d_seed_cap = 0; // splice seed calls (hsa_splice_seeds_device)
     void *d_ext = nullptr; size_t d_ext_cap = 0;   // seed-extension stacks (hsa_extend_batch)
     void *d_slices = nullptr; size_t d_slices_cap = 0; // persistent extension slots (hsa_extend_sliced)
+    // k_search_any (hsa_search_any.h): per-lane scratch, job lists and counters, regimes
+    void *d_any = nullptr; size_t d_any_cap = 0;
+    void *d_any_aux = nullptr; size_t d_any_aux_cap = 0;
     // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;

@@ -3,6 +3,8 @@
 // are in hsa_search_kernels.h.
 #include "hsa_search_kernels.h"
 
+#include <vector>
+
 // ---------------------------------------------------------------- splice seeds
 // The seed calls of bwt_splice_match (bwtgap.c:797-812) for every read the main pass
 // flagged HSA_F_FALLBACK: one thread per (read, strand).  The strand's three seeds
@@ -154,6 +156,142 @@ static int mg_limits(const hsa_job_t *jobs, const hsa_mg_job_t *mg, int n, const
     return 0;
 }
 
+// k_search_any over host arrays (hsa_search_any.h): reads longer than k_search holds,
+// or every read of a regime outside its layouts.  Same outputs as search_batch_impl.
+static long search_any_host(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs, int n,
+                            const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags, uint64_t *hit_off,
+                            uint32_t **hits_out, hsa_stats_t *stats, const MgHost *mh)
+{
+    hipStream_t st = ix->stream;
+    uint32_t max_len = 1, max_seed = 0;
+    for (int j = 0; j < n; ++j) {
+        if (jobs[j].len > max_len) max_len = jobs[j].len;
+        const bool own = mh ? mh->mg[j].seed == HSA_SEED_OWN : (int)jobs[j].len > jobs[j].seed_len;
+        if (own && (uint32_t)jobs[j].seed_len > max_seed) max_seed = (uint32_t)jobs[j].seed_len;
+    }
+    AnyBufs AB;
+    int rc = any_prepare(ix, regimes, n_regimes, (size_t)n, st, AB);
+    if (rc) return rc;
+    // inputs after the fast path's regime staging ([0, 1536) of d_in stays as it is)
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t o_jobs = 1536, o_codes = o_jobs + al((size_t)n * sizeof(hsa_job_t));
+    const size_t o_mg = o_codes + al(codes_len + 64), o_cw = o_mg + (mh ? al((size_t)n * sizeof(hsa_mg_job_t)) : 0);
+    const size_t cw_bytes = mh ? mh->width_pairs * 8 : 0;
+    void *before = ix->d_in;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, o_cw + cw_bytes + 256))) return rc;
+    if (before != ix->d_in) ix->staged_valid = 0;       // the regime staging went with the old buffer
+    char *din = (char *)ix->d_in;
+    HSA_HIP(hipMemcpyAsync(din + o_jobs, jobs, sizeof(hsa_job_t) * n, hipMemcpyHostToDevice, st));
+    HSA_HIP(hipMemcpyAsync(din + o_codes, codes, codes_len, hipMemcpyHostToDevice, st));
+    MgPass mgp{nullptr, nullptr};
+    if (mh) {
+        HSA_HIP(hipMemcpyAsync(din + o_mg, mh->mg, sizeof(hsa_mg_job_t) * n, hipMemcpyHostToDevice, st));
+        HSA_HIP(hipMemcpyAsync(din + o_cw, mh->widths, cw_bytes, hipMemcpyHostToDevice, st));
+        mgp = MgPass{(const hsa_mg_job_t *)(din + o_mg), (int32_t *)(din + o_cw)};
+    }
+    const uint64_t hit_cap = (uint64_t)n * 64 + 65536;
+    const size_t o_fl = al((size_t)n * 4), o_ho = o_fl + al((size_t)n * 4), o_hits = o_ho + al((size_t)n * 8);
+    if ((rc = hsa_grow(&ix->d_out, &ix->d_out_cap, o_hits + hit_cap * 36 + 256))) return rc;
+    char *dout = (char *)ix->d_out;
+    unsigned long long *d_ctr = (unsigned long long *)ix->d_ctr;
+    HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));
+    HSA_HIP(hipEventRecord(ix->ev0, st));
+    const hsa_job_t *dj = (const hsa_job_t *)(din + o_jobs);
+    const uint8_t *dc = (const uint8_t *)(din + o_codes);
+    int32_t *d_n = (int32_t *)dout;
+    uint32_t *d_fl = (uint32_t *)(dout + o_fl);
+    uint64_t *d_ho = (uint64_t *)(dout + o_ho);
+    uint32_t *d_hits = (uint32_t *)(dout + o_hits);
+    if ((rc = any_pass<uint32_t>(ix, AB, regimes, n_regimes, dj, nullptr, nullptr, n, (size_t)n, max_len, max_seed, dc,
+                                 mh ? &mgp : nullptr, d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, AB.cnt + 2, AB.l_ovf,
+                                 AB.cnt + 3, false, st)) ||
+        (rc = any_pass<uint32_t>(ix, AB, regimes, n_regimes, dj, AB.l_ovf, AB.cnt + 3, 0, (size_t)n, max_len, max_seed,
+                                 dc, mh ? &mgp : nullptr, d_n, d_fl, d_ho, d_hits, hit_cap, d_ctr, AB.cnt + 4, nullptr,
+                                 nullptr, true, st)))
+        return rc;
+    HSA_HIP(hipEventRecord(ix->ev1, st));
+    unsigned long long ctr[16];
+    HSA_HIP(hipMemcpyAsync(ctr, d_ctr, sizeof ctr, hipMemcpyDeviceToHost, st));
+    HSA_HIP(hipMemcpyAsync(n_aln, d_n, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HSA_HIP(hipMemcpyAsync(flags, d_fl, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HSA_HIP(hipMemcpyAsync(hit_off, d_ho, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    HSA_HIP(hipStreamSynchronize(st));
+    if (ctr[5]) { hsa_set_error("%llu reads pushed a score past the regime's n_stacks", ctr[5]); return HSA_E_ARG; }
+    if (ctr[11]) { hsa_set_error("%llu reads exceed the large-pass capacity", ctr[11]); return HSA_E_ARG; }
+    float ms = 0;
+    HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+    const uint64_t total = ctr[1];
+    uint32_t *h = (uint32_t *)malloc((total + 1) * 36);
+    if (total) HSA_HIP(hipMemcpy(h, d_hits, total * 36, hipMemcpyDeviceToHost));
+    if (mh) {
+        int32_t *cw = (int32_t *)malloc(cw_bytes + 8);
+        HSA_HIP(hipMemcpy(cw, din + o_cw, cw_bytes, hipMemcpyDeviceToHost));
+        for (int j = 0; j < n; ++j)
+            memcpy(mh->widths_out + 2 * mh->mg[j].wb_off, cw + 2 * mh->mg[j].wb_off, 8 * ((size_t)jobs[j].len + 1));
+        free(cw);
+    }
+    if (stats) {
+        stats->rank_queries += ctr[2]; stats->blocks_loaded += ctr[3]; stats->pops += ctr[4];
+        stats->kernel_ms += ms; stats->main_kernel_ms += ms; stats->main_launches += 1;
+    }
+    *hits_out = h;
+    return (long)total;
+}
+
+// A batch with reads (or a regime) k_search cannot hold: the reads it can hold through
+// search_batch_impl, the others through k_search_any; outputs merged in job order.
+static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs,
+                              int n_jobs, const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
+                              uint64_t *hit_off, uint32_t **hits_out, hsa_stats_t *stats, const MgHost *mh);
+
+static long search_split(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs, int n,
+                         const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags, uint64_t *hit_off,
+                         uint32_t **hits_out, hsa_stats_t *stats, const MgHost *mh, bool fast_rg)
+{
+    std::vector<int> part[2];                        // 0: k_search, 1: k_search_any
+    for (int j = 0; j < n; ++j) part[fast_rg && jobs[j].len <= FAST_MAX_LEN ? 0 : 1].push_back(j);
+    uint32_t *hs[2] = {nullptr, nullptr};
+    long tot[2] = {0, 0};
+    if (stats) memset(stats, 0, sizeof *stats);
+    for (int k = 0; k < 2; ++k) {
+        const int m = (int)part[k].size();
+        if (m == 0) continue;
+        std::vector<hsa_job_t> pj(m);
+        std::vector<hsa_mg_job_t> pm(mh ? m : 0);
+        for (int q = 0; q < m; ++q) {
+            pj[q] = jobs[part[k][q]];
+            if (mh) pm[q] = mh->mg[part[k][q]];
+        }
+        const MgHost pmh = mh ? MgHost{pm.data(), mh->widths, mh->width_pairs, mh->widths_out} : MgHost{};
+        std::vector<int32_t> na(m);
+        std::vector<uint32_t> fl(m);
+        std::vector<uint64_t> ho(m);
+        hsa_stats_t ps;
+        memset(&ps, 0, sizeof ps);
+        const long t = k == 0 ? search_batch_impl(ix, regimes, n_regimes, pj.data(), m, codes, codes_len, na.data(), fl.data(),
+                                                  ho.data(), &hs[k], &ps, mh ? &pmh : nullptr)
+                              : search_any_host(ix, regimes, n_regimes, pj.data(), m, codes, codes_len, na.data(),
+                                                fl.data(), ho.data(), &hs[k], &ps, mh ? &pmh : nullptr);
+        if (t < 0) { free(hs[0]); free(hs[1]); return t; }
+        tot[k] = t;
+        for (int q = 0; q < m; ++q) {
+            const int j = part[k][q];
+            n_aln[j] = na[q]; flags[j] = fl[q]; hit_off[j] = ho[q] + (k ? (uint64_t)tot[0] : 0);
+        }
+        if (stats) {
+            stats->rank_queries += ps.rank_queries; stats->blocks_loaded += ps.blocks_loaded; stats->pops += ps.pops;
+            stats->overflow_reruns += ps.overflow_reruns; stats->kernel_ms += ps.kernel_ms;
+            stats->main_kernel_ms += ps.main_kernel_ms; stats->main_launches += ps.main_launches;
+        }
+    }
+    uint32_t *h = (uint32_t *)malloc(((size_t)tot[0] + (size_t)tot[1] + 1) * 36);
+    if (tot[0]) memcpy(h, hs[0], (size_t)tot[0] * 36);
+    if (tot[1]) memcpy(h + (size_t)tot[0] * 9, hs[1], (size_t)tot[1] * 36);
+    free(hs[0]); free(hs[1]);
+    *hits_out = h;
+    return tot[0] + tot[1];
+}
+
 static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *jobs,
                               int n_jobs, const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags,
                               uint64_t *hit_off, uint32_t **hits_out, hsa_stats_t *stats, const MgHost *mh)
@@ -173,6 +311,14 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
                           jobs[j].len, codes_len);
             return HSA_E_ARG;
         }
+    {
+        const bool fast_rg = fast_regimes(regimes, n_regimes);
+        bool all_fit = fast_rg;
+        for (int j = 0; j < n_jobs && all_fit; ++j) all_fit = jobs[j].len <= FAST_MAX_LEN;
+        if (!all_fit)
+            return search_split(ix, regimes, n_regimes, jobs, n_jobs, codes, codes_len, n_aln, flags, hit_off, hits_out,
+                                stats, mh, fast_rg);
+    }
     HSA_HIP(hipSetDevice(ix->device));
     hipStream_t st = ix->stream;
     if (stats) memset(stats, 0, sizeof *stats);

@@ -1190,15 +1190,21 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 
 
 
+#include "hsa_search_any.h"
+
 // ---------------------------------------------------------------- host helpers (both TUs)
+// What any search accepts (k_search_any's bounds); fast_regimes: what k_search's layouts hold.
 static int check_regimes(const hsa_regime_t *rg, int n)
 {
     for (int r = 0; r < n; ++r) {
         const hsa_regime_t &R = rg[r];
         if (R.s_mm < 0 || R.s_gapo < 0 || R.s_gape < 0) { hsa_set_error("negative penalty"); return HSA_E_ARG; }
-        if (R.n_stacks <= 0 || R.n_stacks > MAXS) { hsa_set_error("n_stacks %d outside 1..%d", R.n_stacks, MAXS); return HSA_E_ARG; }
-        if (R.max_gapo > 14 || R.max_gape > 254) { hsa_set_error("max_gapo/max_gape out of range"); return HSA_E_ARG; }
-        if (R.max_diff < -1 || R.max_diff > 125) { hsa_set_error("max_diff out of range"); return HSA_E_ARG; }
+        if (R.n_stacks <= 0 || R.n_stacks > ANY_MAX_STACKS) {
+            hsa_set_error("n_stacks %d outside 1..%d", R.n_stacks, ANY_MAX_STACKS);
+            return HSA_E_ARG;
+        }
+        if (R.max_gapo < 0 || R.max_gape < 0) { hsa_set_error("max_gapo/max_gape negative"); return HSA_E_ARG; }
+        if (R.max_diff < -1) { hsa_set_error("max_diff out of range"); return HSA_E_ARG; }
     }
     return 0;
 }
@@ -1221,6 +1227,25 @@ static int bucket_map(const hsa_regime_t &R, uint8_t map[MAXS])
     for (int s = 0; s < MAXS; ++s) map[s] = used[s] && k < 0xFF ? (uint8_t)k++ : (uint8_t)0xFF;
     return k;
 }
+
+// Regimes whose every bound fits k_search's layouts: the entry meta word (n_gapo 4
+// bits, n_gape 8, n_mm 7), the score table (MAXS), the bucket mask (MAXB reachable
+// scores) and the 16-bit pruning elements (bids compared with bounds <= 254).  Other
+// regimes run k_search_any.
+static bool fast_regimes(const hsa_regime_t *rg, int n)
+{
+    if (getenv("HSA_FORCE_ANY")) return false;       // tests: every search through k_search_any
+    for (int r = 0; r < n; ++r) {
+        const hsa_regime_t &R = rg[r];
+        if (R.max_gapo > 14 || R.max_gape > 254 || R.max_diff > 125 || R.max_seed_diff > 254 || R.n_stacks > MAXS)
+            return false;
+        uint8_t map[MAXS];
+        if (bucket_map(R, map) > MAXB) return false;
+    }
+    return true;
+}
+
+#define FAST_MAX_LEN 1023u       // k_search: 10-bit read positions (meta word, control word)
 
 // The dense bucket of a score is simply its n_mm when no gap opens exist and every
 // reachable mismatch count has its own score (k_search skips the table then).
@@ -1506,7 +1531,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     if (P.wide) hipLaunchKernelGGL((k_widths<uint16_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
     else hipLaunchKernelGGL((k_widths<uint8_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
     HSA_HIP(hipGetLastError());
-    if (ix->ev_split && !n_dev) HSA_HIP(hipEventRecord(ix->ev_split, st));
+    if (ix->ev_split && qctr == 0) HSA_HIP(hipEventRecord(ix->ev_split, st));   // the main pass only
     if (P.wide) launch_search<uint16_t, IT>(P, A, st);
     else launch_search<uint8_t, IT>(P, A, st);
     HSA_HIP(hipGetLastError());
@@ -1541,8 +1566,8 @@ static int jobs_limits(const hsa_job_t *jobs, int n, int &max_len, int &max_seed
 {
     max_len = 0; max_seed = 0;
     for (int j = 0; j < n; ++j) {
-        if (jobs[j].len > 1023) { hsa_set_error("read %d longer than 1023", j); return HSA_E_ARG; }
-        if (jobs[j].max_diff > 125 || jobs[j].max_diff < -1) { hsa_set_error("max_diff out of range"); return HSA_E_ARG; }
+        if (jobs[j].len > ANY_MAX_LEN) { hsa_set_error("read %d longer than %d (gap_entry_t.info, bwtgap.c:157)", j, ANY_MAX_LEN); return HSA_E_ARG; }
+        if (jobs[j].max_diff < -1) { hsa_set_error("max_diff out of range"); return HSA_E_ARG; }
         if ((int)jobs[j].len > max_len) max_len = (int)jobs[j].len;
         if ((int)jobs[j].len > jobs[j].seed_len && jobs[j].seed_len > max_seed) max_seed = jobs[j].seed_len;
     }
@@ -1577,6 +1602,93 @@ static int stage_regimes(hsa_index *ix, const hsa_regime_t *regimes, int n_regim
     return 0;
 }
 
+// ---------------------------------------------------------------- the k_search_any passes
+// Device buffers of one search's k_search_any passes (in ix->d_any_aux): the regimes, the
+// counters (0 jobs for k_search, 1 jobs for k_search_any, 2 its queue head, 3 jobs it
+// hands to its large-capacity pass, 4 that pass's queue head) and the job lists.
+struct AnyBufs {
+    hsa_regime_t *reg;
+    unsigned long long *cnt;
+    int32_t *l_fast, *l_any, *l_ovf;
+};
+
+static int any_prepare(hsa_index *ix, const hsa_regime_t *regimes, int n_regimes, size_t n, hipStream_t st, AnyBufs &B)
+{
+    const size_t lb = (n * 4 + 255) / 256 * 256;
+    int rc = hsa_grow(&ix->d_any_aux, &ix->d_any_aux_cap, 512 + 3 * lb);
+    if (rc) return rc;
+    char *d = (char *)ix->d_any_aux;
+    B.reg = (hsa_regime_t *)d;
+    B.cnt = (unsigned long long *)(d + 256);
+    B.l_fast = (int32_t *)(d + 512);
+    B.l_any = (int32_t *)(d + 512 + lb);
+    B.l_ovf = (int32_t *)(d + 512 + 2 * lb);
+    HSA_HIP(hipMemcpyAsync(B.reg, regimes, sizeof(hsa_regime_t) * n_regimes, hipMemcpyHostToDevice, st));
+    HSA_HIP(hipMemsetAsync(B.cnt, 0, 64, st));
+    HSA_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+// jobs up to fast_max bases go to k_search's list, longer ones to k_search_any's
+static __global__ void __launch_bounds__(BLOCK) k_partition(const hsa_job_t *jobs, int n, uint32_t fast_max,
+                                                            int32_t *l_fast, int32_t *l_any, unsigned long long *cnt)
+{
+    const int j = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    if (j >= n) return;
+    if (jobs[j].len <= fast_max) l_fast[atomicAdd(&cnt[0], 1ull)] = j;
+    else l_any[atomicAdd(&cnt[1], 1ull)] = j;
+}
+
+// One k_search_any pass.  big: the large-capacity pass (pools up to the reference's
+// max_entries bound, 262 144 hits, few lanes) for the jobs the first pass overflowed.
+template <typename IT>
+static int any_pass(hsa_index *ix, const AnyBufs &B, const hsa_regime_t *regimes, int n_regimes, const hsa_job_t *d_jobs,
+                    const int32_t *d_list, const unsigned long long *n_dev, int n_host, size_t n_bound, uint32_t max_len,
+                    uint32_t max_seed, const uint8_t *d_codes, const MgPass *mg, int32_t *d_n, uint32_t *d_fl,
+                    uint64_t *d_ho, uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr,
+                    unsigned long long *qhead, int32_t *ovf_list, unsigned long long *ovf_n, bool big, hipStream_t st)
+{
+    if (n_bound == 0) return 0;
+    AnyArgs A;
+    memset(&A, 0, sizeof A);
+    A.fwd = RankDir{ix->blk[0], ix->isa0};
+    A.rev = RankDir{ix->blk[1], ix->risa0};
+    A.fwd64 = hsa_rank_dir64(ix, 0);
+    A.rev64 = hsa_rank_dir64(ix, 1);
+    A.T = ix->T; A.T64 = ix->T64;
+    memcpy(A.C, ix->C, sizeof A.C);
+    memcpy(A.C64, ix->C64, sizeof A.C64);
+    A.regimes = B.reg; A.jobs = d_jobs; A.list = d_list; A.n_dev = n_dev; A.n_host = n_host; A.codes = d_codes;
+    A.mg = mg ? mg->d_mg : nullptr; A.cw = mg ? mg->d_cw : nullptr;
+    A.n_aln = d_n; A.flags = d_fl; A.hit_off = d_ho; A.hits = d_hits; A.hit_cap = hit_cap; A.ctr = d_ctr;
+    A.qhead = qhead; A.ovf_list = ovf_list; A.ovf_n = ovf_n;
+    uint32_t nst = 1, max_entries = 0;
+    for (int r = 0; r < n_regimes; ++r) {
+        nst = (uint32_t)regimes[r].n_stacks > nst ? (uint32_t)regimes[r].n_stacks : nst;
+        max_entries = (uint32_t)regimes[r].max_entries > max_entries ? (uint32_t)regimes[r].max_entries : max_entries;
+    }
+    // capacities: live entries never exceed max_entries + 9 (bwtgap.c:150-151)
+    const uint64_t want = (uint64_t)max_entries + 16u;
+    const uint32_t pcap = big ? (uint32_t)(want < (4ull << 20) ? want : (4ull << 20)) : 8192u;
+    const uint32_t hcap = big ? 262144u : 512u;
+    const size_t lb = any_layout<IT>(A, max_len, max_seed, nst, pcap, hcap, 10);
+    const size_t budget = big ? ((size_t)16 << 30) : ((size_t)4 << 30), lanes_max = big ? 64 : 16384;
+    size_t lanes = n_bound < lanes_max ? n_bound : lanes_max;
+    if (lanes * lb > budget) lanes = budget / lb;
+    if (lanes < 1) lanes = 1;
+    A.nlanes = (uint32_t)lanes;
+    if (lanes * lb + 256 > ix->d_any_cap) HSA_HIP(hipStreamSynchronize(st));   // a pass may still use the old one
+    int rc = hsa_grow(&ix->d_any, &ix->d_any_cap, lanes * lb + 256);
+    if (rc) return rc;
+    A.scratch = (uint8_t *)ix->d_any;
+    if (getenv("HSA_VERBOSE"))
+        fprintf(stderr, "[hsa] k_search_any%s: %zu lanes x %zu B (pool %u, hits %u, %u stacks, reads <= %u bp)\n",
+                big ? " (large pass)" : "", lanes, lb, pcap, hcap, nst, max_len);
+    hipLaunchKernelGGL(k_search_any<IT>, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, st, A);
+    HSA_HIP(hipGetLastError());
+    return 0;
+}
+
 // hsa_search_device / hsa_search_device64: the main pass over a device-resident batch,
 // then the BIG and HUGE capacity re-runs, all queued on one stream without a host sync.
 template <typename IT>
@@ -1588,12 +1700,39 @@ static int search_device_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     if (sizeof(IT) == 8 && !ix->wide) { hsa_set_error("not a 64-bit index (hsa_index_create_device64)"); return HSA_E_ARG; }
     int rc = check_regimes(regimes, n_regimes);
     if (rc) return rc;
-    if (b->max_len < 1 || b->max_len > 1023 || b->max_seed < 0 || b->max_seed > 1023) {
+    if (b->max_len < 1 || b->max_len > ANY_MAX_LEN || b->max_seed < 0 || b->max_seed > ANY_MAX_LEN) {
         hsa_set_error("max_len/max_seed out of range");
         return HSA_E_ARG;
     }
     HSA_HIP(hipSetDevice(ix->device));
     hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+    unsigned long long *ctr = (unsigned long long *)b->d_counters;
+    hipEvent_t *pe = ix->pev[ix->pev_n % hsa_index::PASS_RING];
+    for (int j = 0; j < 3; ++j)
+        if (!pe[j]) HSA_HIP(hipEventCreate(&pe[j]));
+    // reads longer than k_search holds, or a regime outside its layouts: k_search_any
+    // (all jobs for such a regime; the long ones, partitioned on the device, otherwise)
+    const bool fast_rg = fast_regimes(regimes, n_regimes);
+    const bool any_path = !fast_rg || (uint32_t)b->max_len > FAST_MAX_LEN;
+    AnyBufs AB{};
+    if (any_path && (rc = any_prepare(ix, regimes, n_regimes, (size_t)b->n_jobs, st, AB))) return rc;
+    if (!fast_rg) {
+        ++ix->pev_n;
+        HSA_HIP(hipEventRecord(pe[0], st));
+        HSA_HIP(hipEventRecord(pe[1], st));
+        HSA_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(unsigned long long), st));
+        if ((rc = any_pass<IT>(ix, AB, regimes, n_regimes, b->d_jobs, nullptr, nullptr, b->n_jobs, (size_t)b->n_jobs,
+                               (uint32_t)b->max_len, (uint32_t)b->max_seed, b->d_codes, nullptr, b->d_n_aln, b->d_flags,
+                               b->d_hit_off, b->d_hits, b->hit_cap, ctr, AB.cnt + 2, AB.l_ovf, AB.cnt + 3, false, st)) ||
+            (rc = any_pass<IT>(ix, AB, regimes, n_regimes, b->d_jobs, AB.l_ovf, AB.cnt + 3, 0, (size_t)b->n_jobs,
+                               (uint32_t)b->max_len, (uint32_t)b->max_seed, b->d_codes, nullptr, b->d_n_aln, b->d_flags,
+                               b->d_hit_off, b->d_hits, b->hit_cap, ctr, AB.cnt + 4, nullptr, nullptr, true, st)))
+            return rc;
+        HSA_HIP(hipEventRecord(pe[2], st));
+        return 0;
+    }
+    const int fast_len = (uint32_t)b->max_len > FAST_MAX_LEN ? (int)FAST_MAX_LEN : b->max_len;
+    const int fast_seed = b->max_seed > fast_len ? fast_len : b->max_seed;
     void *before = ix->d_in;
     if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1536))) return rc;
     int nb = 0;
@@ -1604,35 +1743,49 @@ static int search_device_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     int max_entries = 0;
     for (int r = 0; r < n_regimes; ++r) max_entries = regimes[r].max_entries > max_entries ? regimes[r].max_entries : max_entries;
     const bool nib_ok = nib_exact(regimes, n_regimes);
-    if ((rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_MAIN, P, 0, EB, nib_ok)) ||
-        (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_BIG, B, 0, EB, nib_ok)) ||
-        (rc = plan_launch(ix, b->n_jobs, b->max_len, b->max_seed, nb, gaps, wide, PASS_HUGE, H, max_entries, EB)))
+    if ((rc = plan_launch(ix, b->n_jobs, fast_len, fast_seed, nb, gaps, wide, PASS_MAIN, P, 0, EB, nib_ok)) ||
+        (rc = plan_launch(ix, b->n_jobs, fast_len, fast_seed, nb, gaps, wide, PASS_BIG, B, 0, EB, nib_ok)) ||
+        (rc = plan_launch(ix, b->n_jobs, fast_len, fast_seed, nb, gaps, wide, PASS_HUGE, H, max_entries, EB)))
         return rc;
     if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, (size_t)b->n_jobs * 4 + 64)) ||
         (rc = hsa_grow(&ix->d_ovf2, &ix->d_ovf2_cap, (size_t)b->n_jobs * 4 + 64)))
         return rc;
-    unsigned long long *ctr = (unsigned long long *)b->d_counters;
     const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
     const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
-    hipEvent_t *pe = ix->pev[ix->pev_n % hsa_index::PASS_RING];
-    for (int j = 0; j < 3; ++j)
-        if (!pe[j]) HSA_HIP(hipEventCreate(&pe[j]));
     ++ix->pev_n;
     ix->ev_split = pe[1];
     HSA_HIP(hipEventRecord(pe[0], st));
-    if ((rc = launch_pass<IT>(ix, P, ix->main, d_reg, d_bmap, b->d_jobs, nullptr, b->n_jobs, b->max_len, b->max_seed,
-                          b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st,
-                          (int32_t *)ix->d_ovf)))
+    const int32_t *fast_list = nullptr;
+    const unsigned long long *fast_n = nullptr;
+    if (any_path) {                                  // long reads in the batch: split it on the device
+        const unsigned g = (unsigned)(((size_t)b->n_jobs + BLOCK - 1) / BLOCK);
+        hipLaunchKernelGGL(k_partition, dim3(g ? g : 1), dim3(BLOCK), 0, st, b->d_jobs, b->n_jobs, FAST_MAX_LEN, AB.l_fast,
+                           AB.l_any, AB.cnt);
+        HSA_HIP(hipGetLastError());
+        fast_list = AB.l_fast;
+        fast_n = AB.cnt;
+    }
+    if ((rc = launch_pass<IT>(ix, P, ix->main, d_reg, d_bmap, b->d_jobs, fast_list, b->n_jobs, fast_len, fast_seed,
+                              b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits, b->hit_cap, ctr, st,
+                              (int32_t *)ix->d_ovf, fast_n)))
         return rc;
     // exact re-runs of the reads that overflowed their lane's capacity: BIG for the
     // main pass's (count ctr[8]), HUGE for BIG's (count ctr[12]); the read counts stay
     // on the device, so an empty re-run is a launch whose lanes exit at once
     if ((rc = launch_pass<IT>(ix, B, ix->big, d_reg, d_bmap, b->d_jobs, (const int32_t *)ix->d_ovf, b->n_jobs,
-                          b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
-                          b->hit_cap, ctr, st, (int32_t *)ix->d_ovf2, ctr + 8, 9, nullptr, 12)) ||
+                              fast_len, fast_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
+                              b->hit_cap, ctr, st, (int32_t *)ix->d_ovf2, ctr + 8, 9, nullptr, 12)) ||
         (rc = launch_pass<IT>(ix, H, ix->huge, d_reg, d_bmap, b->d_jobs, (const int32_t *)ix->d_ovf2, b->n_jobs,
-                          b->max_len, b->max_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
-                          b->hit_cap, ctr, st, nullptr, ctr + 12, 15)))
+                              fast_len, fast_seed, b->d_codes, b->d_n_aln, b->d_flags, b->d_hit_off, b->d_hits,
+                              b->hit_cap, ctr, st, nullptr, ctr + 12, 15)))
+        return rc;
+    if (any_path &&
+        ((rc = any_pass<IT>(ix, AB, regimes, n_regimes, b->d_jobs, AB.l_any, AB.cnt + 1, 0, (size_t)b->n_jobs,
+                            (uint32_t)b->max_len, (uint32_t)b->max_seed, b->d_codes, nullptr, b->d_n_aln, b->d_flags,
+                            b->d_hit_off, b->d_hits, b->hit_cap, ctr, AB.cnt + 2, AB.l_ovf, AB.cnt + 3, false, st)) ||
+         (rc = any_pass<IT>(ix, AB, regimes, n_regimes, b->d_jobs, AB.l_ovf, AB.cnt + 3, 0, (size_t)b->n_jobs,
+                            (uint32_t)b->max_len, (uint32_t)b->max_seed, b->d_codes, nullptr, b->d_n_aln, b->d_flags,
+                            b->d_hit_off, b->d_hits, b->hit_cap, ctr, AB.cnt + 4, nullptr, nullptr, true, st))))
         return rc;
     HSA_HIP(hipEventRecord(pe[2], st));
     ix->ev_split = ix->evm;

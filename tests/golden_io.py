@@ -14,6 +14,12 @@ def cases():
         return json.load(f)
 
 
+def limits_cases():
+    """Cases past the fast search kernel's layouts (tools/make_golden.py --limits)."""
+    with open(os.path.join(GOLD, "manifest_limits.json")) as f:
+        return json.load(f)
+
+
 def load_case(name):
     z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
     d = {k: z[k] for k in z.files}

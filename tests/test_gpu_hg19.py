@@ -23,7 +23,7 @@ def _index():
     import bench
     if not _IX:
         import torch
-        gi, res = bench.build_index(bench.GENOME_T, bench.GENOME_SEED, torch.cuda.current_device())
+        gi, res, _ = bench.build_index(bench.GENOME_T, bench.GENOME_SEED, torch.cuda.current_device())
         _IX["gi"], _IX["ox"] = gi, bench.host_oracle_index(res, bench.GENOME_T)
         del res
     return _IX["gi"], _IX["ox"]

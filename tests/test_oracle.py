@@ -2,7 +2,7 @@
 import numpy as np
 import pytest
 
-from golden_io import EXTCAP_CASES, GOLD, INDEX, cases, load_case, load_extcap, parse_opts, split_hits
+from golden_io import EXTCAP_CASES, GOLD, INDEX, cases, limits_cases, load_case, load_extcap, parse_opts, split_hits
 from hsa_amd import index_io
 from oracle_ctypes import Opt, OracleIndex, default_opt
 
@@ -72,7 +72,7 @@ def test_step_consistency():
             k, l, rk, rl = int(ok[c]), int(ol[c]), int(ork[c]), int(orl[c])
 
 
-@pytest.mark.parametrize("name", sorted(cases().keys()))
+@pytest.mark.parametrize("name", sorted(cases().keys()) + sorted(limits_cases().keys()))
 def test_batch_matches_reference(name):
     """bwa_cal_sa_reg_gap restatement vs the reference on every golden case.
 
@@ -165,7 +165,7 @@ def test_oracle64_occ_step_width_equal_32():
         assert np.array_equal(o64.cal_width(seq), o32.cal_width(seq).astype(np.uint64))
 
 
-@pytest.mark.parametrize("name", sorted(cases().keys()))
+@pytest.mark.parametrize("name", sorted(cases().keys()) + sorted(limits_cases().keys()))
 def test_oracle64_batch_matches_reference(name):
     """bwa_cal_sa_reg_gap with 64-bit intervals on every golden case: the reference's
     hits, widened to hsa_aln64_t (bwt_aln1_t fields, 64-bit k/l/rev_k/rev_l)."""

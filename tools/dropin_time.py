@@ -27,7 +27,7 @@ def main():
     import bench
     from hsa_amd import synth
     from hsa_amd._lib import GapOpt
-    gi, res = bench.build_index(bench.GENOME_T, bench.GENOME_SEED, torch.cuda.current_device())
+    gi, res, _ = bench.build_index(bench.GENOME_T, bench.GENOME_SEED, torch.cuda.current_device())
     del res
     genome = synth.PackedGenome(bench.GENOME_T, bench.GENOME_SEED)
     recs = synth.record_layout(bench.GENOME_T, bench.RECORDS)

@@ -9,6 +9,7 @@ Every fixture is data: synthetic inputs plus the reference's outputs on them.
     python tools/make_golden.py --ecoli    # E.coli-sized digests (committed)
     python tools/make_golden.py --dropin   # FASTQ + reference SAM for the drop-in test
     python tools/make_golden.py --sa       # SA -> position golden values (R11)
+    python tools/make_golden.py --limits   # reads / options past the fast kernel's layouts
 """
 from __future__ import annotations
 
@@ -243,6 +244,47 @@ def tiny_cases(work):
     print(f"tiny_width: {len(seqs)} reads")
 
     with open(os.path.join(GOLD, "manifest_tiny.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+
+
+def limits_cases(work):
+    """Cases past k_search's fixed layouts, which the drop-in serves with k_search_any
+    (hsa_amd/csrc/hsa_search_any.h): reads of 1 100-1 500 bp mixed with 100 bp ones,
+    n_stacks 298 with 250 reachable scores (-o 2 -e 60), and 15 gap opens (-o 15).  On
+    the committed tiny index; manifest_limits.json."""
+    T, seed = 200003, 7
+    g = synth.genome_codes(T, seed)
+    rec = synth.record_layout(T, 3)
+    prefix = os.path.join(GOLD, "index", "tiny.fa")
+    cases = []
+    seqs = []
+    r, _ = synth.make_reads(g, rec, 120, 1500, 41, max_mm=6)
+    seqs += list(r)
+    r, _ = synth.make_reads(g, rec, 80, 1500, 42, indel=True, max_mm_indel=3)
+    seqs += list(r)
+    r, _ = synth.make_reads(g, rec, 60, 1100, 43, max_mm=8)
+    seqs += list(r)
+    r, _ = synth.make_reads(g, rec, 100, 100, 44, max_mm=4)
+    seqs += list(r)
+    for j in range(0, len(seqs), 37):          # an N here and there
+        q = seqs[j].copy()
+        q[len(q) // 3] = 4
+        seqs[j] = q
+    seqs += [synth.genome_codes(1300, 5000 + j) for j in range(10)]   # unmappable: splice fallback
+    order = np.argsort(synth._u(45, len(seqs), 0))                     # lengths interleaved
+    seqs = [seqs[i] for i in order]
+    cases.append(("long1500_n8o1", seqs, ["-n", "8", "-o", "1"]))
+    r, _ = synth.make_reads(g, rec, 300, 100, 46, indel=True, max_mm_indel=2)
+    cases.append(("gap100_o2e60", list(r), ["-n", "4", "-o", "2", "-e", "60"]))
+    r, _ = synth.make_reads(g, rec, 200, 100, 47, indel=True, max_mm_indel=1)
+    cases.append(("gap100_o15", list(r), ["-n", "16", "-o", "15", "-m", "20000"]))
+    manifest = {}
+    for name, seqs, args in cases:
+        n_aln, flags, hits, secs = run_aln(prefix, seqs, args, work)
+        save_case(name, "tiny", seqs, args, 100000, n_aln, flags, hits)
+        manifest[name] = {"index": "tiny", "args": args, "batch": 100000, "n": len(seqs),
+                          "sha256": hits_digest(n_aln, flags, hits), "ref_seconds": secs}
+    with open(os.path.join(GOLD, "manifest_limits.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 
 
@@ -559,6 +601,7 @@ def main():
     ap.add_argument("--mgcap", action="store_true")
     ap.add_argument("--extcap", action="store_true")
     ap.add_argument("--width0", action="store_true")
+    ap.add_argument("--limits", action="store_true")
     a = ap.parse_args()
     if not os.path.exists(os.path.join(REF, "ref_probe")):
         sys.exit("build oracle/_ref first: make -C oracle -f ref.mk")
@@ -576,6 +619,8 @@ def main():
             extcap_cases(work)
         elif a.width0:
             width0_cases(work)
+        elif a.limits:
+            limits_cases(work)
         else:
             tiny_cases(work)
 

@@ -45,7 +45,7 @@ def main():
 
     t_start = time.perf_counter()
     T, RL, N = bench.GENOME_T, bench.READ_LEN, a.batch
-    gi, res = bench.build_index(T, bench.GENOME_SEED, torch.cuda.current_device())
+    gi, res, _ = bench.build_index(T, bench.GENOME_SEED, torch.cuda.current_device())
     ox = bench.host_oracle_index(res, T)
     del res
     genome = synth.PackedGenome(T, bench.GENOME_SEED)
