@@ -118,7 +118,10 @@ __global__ void __launch_bounds__(64) k_search_any(AnyArgs a)
     AnyEnt<IT> *const pool = reinterpret_cast<AnyEnt<IT> *>(base + a.o_pool);
     const IT TT = Ix::T(a);
     const uint64_t n_jobs = a.n_dev ? *a.n_dev : (uint64_t)a.n_host;
+    // statistics: a read's work counts once, when it completes (a read this pass hands
+    // to the large-capacity pass is counted there)
     uint64_t st_q = 0, st_wq = 0, st_fq = 0, st_b = 0, st_p = 0;
+    uint64_t tq = 0, twq = 0, tfq = 0, tb = 0, tp = 0;
 
     for (;;) {
         const unsigned long long q = atomicAdd(a.qhead, 1ull);
@@ -415,7 +418,10 @@ __global__ void __launch_bounds__(64) k_search_any(AnyArgs a)
         a.n_aln[job] = n_out;
         a.flags[job] = fl;
         a.hit_off[job] = out_off;
+        if (!(fl & HSA_F_OVERFLOW)) { tq += st_q; twq += st_wq; tfq += st_fq; tb += st_b; tp += st_p; }
+        st_q = st_wq = st_fq = st_b = st_p = 0;
     }
+    st_q = tq; st_wq = twq; st_fq = tfq; st_b = tb; st_p = tp;
     atomicAdd(&a.ctr[2], (unsigned long long)st_q);
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);

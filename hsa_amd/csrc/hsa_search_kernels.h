@@ -1669,7 +1669,8 @@ static int any_pass(hsa_index *ix, const AnyBufs &B, const hsa_regime_t *regimes
     }
     // capacities: live entries never exceed max_entries + 9 (bwtgap.c:150-151)
     const uint64_t want = (uint64_t)max_entries + 16u;
-    const uint32_t pcap = big ? (uint32_t)(want < (4ull << 20) ? want : (4ull << 20)) : 8192u;
+    static const uint32_t pcap1 = getenv("HSA_ANY_PCAP") ? (uint32_t)atoi(getenv("HSA_ANY_PCAP")) : 8192u;   // A/B only
+    const uint32_t pcap = big ? (uint32_t)(want < (4ull << 20) ? want : (4ull << 20)) : pcap1;
     const uint32_t hcap = big ? 262144u : 512u;
     const size_t lb = any_layout<IT>(A, max_len, max_seed, nst, pcap, hcap, 10);
     const size_t budget = big ? ((size_t)16 << 30) : ((size_t)4 << 30), lanes_max = big ? 64 : 16384;

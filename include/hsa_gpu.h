@@ -192,6 +192,11 @@ long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regime
  *        Non-zero means: search those reads again with a larger hit_cap.
  *   [13] width queries of every forward-strand row (computed speculatively)
  *   [14] the part of [13] the reference issues (forward strands searched)
+ * Reads past k_search's layouts (longer than 1 023 bases: split off on the device) and
+ * regimes past them (n_stacks > 512, > 128 reachable scores, max_gapo > 14, max_diff >
+ * 125: every read) run k_search_any (hsa_search_any.h) after k_search, into the same
+ * outputs and counters; its large-capacity re-runs count a read's work once.  max_len
+ * may be up to 65 535 (gap_entry_t.info's 16-bit position, bwtgap.c:157).
  * d_codes: the read codes; the kernels read whole aligned 16-byte words, so the
  *   buffer must stay readable 16 bytes past the last read's end. */
 typedef struct {
