@@ -507,7 +507,7 @@ def main():
     ap.add_argument("--pool", type=int, default=0)
     ap.add_argument("--ref-sample", type=int, default=-1,
                     help="reads the REFERENCE's own CPU path (oracle/_ref/ref_probe) searches, over --ref-procs "
-                         "processes (-1: 64 000 for config 2, 16 000 for config 3; 0: skip the reference legs)")
+                         "processes (-1: 128 000 for config 2, 32 000 for config 3; 0: skip the reference legs)")
     ap.add_argument("--ref-procs", type=int, default=0, help="reference processes (0: the CPU threads of the share)")
     ap.add_argument("--e2e-reads", type=int, default=1_000_000,
                     help="reads of the drop-in end-to-end leg (oracle/_ref/ref_probe_gpu, 100 000 per call)")
@@ -537,7 +537,7 @@ def main():
     RL = {4: 150, 5: 250}.get(a.config, READ_LEN)
     HW = _lib.ALN64_WORDS if wide else 9      # u32 words per hit record
     if a.ref_sample < 0:
-        a.ref_sample = {2: 64_000, 3: 16_000}.get(a.config, 0)
+        a.ref_sample = {2: 128_000, 3: 32_000}.get(a.config, 0)
     ref_legs = rank == 0 and world == 1 and a.config in (2, 3) and not wide and a.ref_sample > 0 and T < (1 << 32)
     t0 = time.time()
     if wide:

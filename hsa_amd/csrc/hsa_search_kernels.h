@@ -1615,6 +1615,12 @@ struct AnyBufs {
 static int any_prepare(hsa_index *ix, const hsa_regime_t *regimes, int n_regimes, size_t n, hipStream_t st, AnyBufs &B)
 {
     const size_t lb = (n * 4 + 255) / 256 * 256;
+    if (ix->d_any_cap > ((size_t)8 << 30)) {       // a past large pass's stacks: give them back
+        HSA_HIP(hipStreamSynchronize(st));
+        (void)hipFree(ix->d_any);
+        ix->d_any = nullptr;
+        ix->d_any_cap = 0;
+    }
     int rc = hsa_grow(&ix->d_any_aux, &ix->d_any_aux_cap, 512 + 3 * lb);
     if (rc) return rc;
     char *d = (char *)ix->d_any_aux;
@@ -1649,6 +1655,15 @@ static int any_pass(hsa_index *ix, const AnyBufs &B, const hsa_regime_t *regimes
                     unsigned long long *qhead, int32_t *ovf_list, unsigned long long *ovf_n, bool big, hipStream_t st)
 {
     if (n_bound == 0) return 0;
+    if (big && n_dev) {
+        // the large pass's lanes hold whole stacks: size it by the reads that overflowed
+        // (one stream sync; this path only runs for reads/regimes k_search cannot hold)
+        unsigned long long cnt = 0;
+        HSA_HIP(hipMemcpyAsync(&cnt, n_dev, sizeof cnt, hipMemcpyDeviceToHost, st));
+        HSA_HIP(hipStreamSynchronize(st));
+        if (cnt == 0) return 0;
+        n_bound = (size_t)cnt;
+    }
     AnyArgs A;
     memset(&A, 0, sizeof A);
     A.fwd = RankDir{ix->blk[0], ix->isa0};
@@ -1673,7 +1688,15 @@ static int any_pass(hsa_index *ix, const AnyBufs &B, const hsa_regime_t *regimes
     const uint32_t pcap = big ? (uint32_t)(want < (4ull << 20) ? want : (4ull << 20)) : pcap1;
     const uint32_t hcap = big ? 262144u : 512u;
     const size_t lb = any_layout<IT>(A, max_len, max_seed, nst, pcap, hcap, 10);
-    const size_t budget = big ? ((size_t)16 << 30) : ((size_t)4 << 30), lanes_max = big ? 64 : 16384;
+    // the large pass holds whole stacks (~75 MB a lane at max_entries 2 000 000) and its
+    // reads are the slow ones: as many lanes as half the free HBM allows, up to 64 GB
+    size_t budget = (size_t)4 << 30, lanes_max = 16384;
+    if (big) {
+        size_t fr = 0, tot = 0;
+        HSA_HIP(hipMemGetInfo(&fr, &tot));
+        budget = fr / 2 < ((size_t)64 << 30) ? fr / 2 : ((size_t)64 << 30);
+        lanes_max = 4096;
+    }
     size_t lanes = n_bound < lanes_max ? n_bound : lanes_max;
     if (lanes * lb > budget) lanes = budget / lb;
     if (lanes < 1) lanes = 1;

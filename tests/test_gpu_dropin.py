@@ -74,14 +74,14 @@ HSA_GPU_ALL = os.path.join(ROOT, "oracle", "_ref", "HSA_gpu_all")
 @pytest.mark.skipif(not os.path.exists(HSA_GPU_ALL), reason="oracle/_ref/HSA_gpu_all not built (make -C oracle)")
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,reads", [("default", "reads"), ("n4o0", "reads"), ("splice_default", "splice_reads"),
-                                        ("splice_n4o1", "splice_reads"), ("splice_o2e60", "splice_reads")])
+                                        ("splice_n4o1", "splice_reads"), ("splice_n4o1O120", "splice_reads")])
 def test_dropin_all_entry_points_sam_identical(name, reads):
     """Every drop-in entry point replaced at once (oracle/ref.mk HSA_gpu_all):
     bwa_cal_sa_reg_gap, bwt_match_gap, and the SAM stage's bwa_cal_pac_pos, whose SA ->
     position lookups (seq_id, position and the duplicate filter of the extra hits in
     every SAM line) run as one GPU batch per read batch (hsa_amd/csrc/bwtse_gpu.c).
-    splice_o2e60 (-o 2 -e 60): n_stacks 298, past k_search's bucket mask and an extension
-    slice slot, so the main path runs k_search_any and the extensions hsa_extend_batch."""
+    splice_n4o1O120 (-O 120): n_stacks 283, more score LIFOs than an extension slice slot
+    holds, so the splice path's extensions run through hsa_extend_batch."""
     idx = os.path.join(GOLD, "index", "tiny.fa")
     fq = os.path.join(GOLD, MAN[reads])
     r = subprocess.run([HSA_GPU_ALL, "aln", *MAN[name]["args"], idx, fq], capture_output=True, timeout=120)

@@ -315,11 +315,10 @@ def ecoli_cases(work):
 
 
 DROPIN_ARGS = {"default": [], "n4o0": ["-n", "4", "-o", "0"]}
-# splice_o2e60: n_stacks 298 (more stack buckets than an extension slice slot holds and
-# more reachable scores than the fast search kernel's bucket mask): the reference takes
-# ~9 min of CPU on this read set
+# splice_n4o1O120: a gap open costs 120, so n_stacks is 283 -- more score LIFOs than an
+# extension slice slot holds (the splice path's extensions take hsa_extend_batch)
 DROPIN_SPLICE_ARGS = {"splice_default": [], "splice_n4o1": ["-n", "4", "-o", "1"],
-                      "splice_o2e60": ["-o", "2", "-e", "60"]}
+                      "splice_n4o1O120": ["-n", "4", "-o", "1", "-O", "120"]}
 
 
 def write_fastq_mixed(path, seqs):
