@@ -28,6 +28,7 @@
 /* coroutine switches _longjmp between stacks, which the fortified longjmp refuses */
 #undef _FORTIFY_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -288,7 +289,7 @@ typedef struct {
 static wm_ent_t *g_wm;
 static size_t g_wm_cap, g_wm_n;
 static uint64_t g_wm_hits, g_wm_misses;
-static pthread_mutex_t g_wm_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_rwlock_t g_wm_mu = PTHREAD_RWLOCK_INITIALIZER;
 static hsa_arena_t g_wm_arena;          /* keys and widths of the entries */
 
 static size_t wkey(int type, int len, const ubyte_t *str, uint8_t *buf)
@@ -347,20 +348,20 @@ static void wm_put(int type, int len, const ubyte_t *str, const uint32_t *w, int
 
 void hsa_splice_wmemo_clear(void)
 {
-    pthread_mutex_lock(&g_wm_mu);
+    pthread_rwlock_wrlock(&g_wm_mu);
     hsa_arena_free(&g_wm_arena);
     free(g_wm);
     g_wm = NULL;
     g_wm_cap = g_wm_n = 0;
-    pthread_mutex_unlock(&g_wm_mu);
+    pthread_rwlock_unlock(&g_wm_mu);
 }
 
 void hsa_splice_wmemo_stats(uint64_t *hits, uint64_t *misses)
 {
-    pthread_mutex_lock(&g_wm_mu);
+    pthread_rwlock_wrlock(&g_wm_mu);
     *hits = g_wm_hits; *misses = g_wm_misses;
     g_wm_hits = g_wm_misses = 0;
-    pthread_mutex_unlock(&g_wm_mu);
+    pthread_rwlock_unlock(&g_wm_mu);
 }
 
 /* bwt_cal_width on the GPU for n sequences of one type; w: 2 * (len + 1) words each */
@@ -381,7 +382,7 @@ int bwt_cal_width(const Idx2BWT *bi_bwt, int len, const ubyte_t *str, bwt_width_
     const size_t kl = wkey(type == 1, len, str, key);
     const uint64_t h = key_hash(key, kl);
     int found = 0, ret = 0;
-    pthread_mutex_lock(&g_wm_mu);
+    pthread_rwlock_rdlock(&g_wm_mu);
     if (g_wm_n)
         for (size_t j = h & (g_wm_cap - 1); g_wm[j].h; j = (j + 1) & (g_wm_cap - 1))
             if (g_wm[j].h == h && g_wm[j].key_len == kl && !memcmp(g_wm[j].key, key, kl)) {
@@ -392,9 +393,9 @@ int bwt_cal_width(const Idx2BWT *bi_bwt, int len, const ubyte_t *str, bwt_width_
                 found = 1;
                 break;
             }
-    if (found) ++g_wm_hits;
-    else if (g_wm_n) ++g_wm_misses;
-    pthread_mutex_unlock(&g_wm_mu);
+    if (found) __atomic_fetch_add(&g_wm_hits, 1, __ATOMIC_RELAXED);
+    else if (g_wm_n) __atomic_fetch_add(&g_wm_misses, 1, __ATOMIC_RELAXED);
+    pthread_rwlock_unlock(&g_wm_mu);
     if (key != stackbuf) free(key);
     if (found) return ret;
     uint64_t off = 0;
@@ -466,13 +467,13 @@ int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
         const double tg = hsa_now();
         widths_gpu(ix, type, (int)q, offs, lens, codes, co, w);
         t_gpu += hsa_now() - tg;
-        pthread_mutex_lock(&g_wm_mu);
+        pthread_rwlock_wrlock(&g_wm_mu);
         size_t o = 0;
         for (size_t j = 0; j < q; ++j) {
             wm_put(type, (int)lens[j], src[j], w + o, (int)w[o + 2 * lens[j] + 1]);
             o += 2 * ((size_t)lens[j] + 1);
         }
-        pthread_mutex_unlock(&g_wm_mu);
+        pthread_rwlock_unlock(&g_wm_mu);
         free(offs); free(lens); free(src); free(codes); free(w);
     }
     if (getenv("HSA_VERBOSE"))
@@ -492,7 +493,7 @@ typedef struct { uint32_t key, sid, ori, occ; } sa_ent_t;   /* key = sa index + 
 static sa_ent_t *g_sa;
 static size_t g_sa_cap2, g_sa_n2;
 static uint64_t g_sa_hits, g_sa_misses;
-static pthread_mutex_t g_sa_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_rwlock_t g_sa_mu = PTHREAD_RWLOCK_INITIALIZER;
 
 static size_t sa_slot(uint32_t key, size_t cap)
 {
@@ -547,16 +548,16 @@ int hsa_splice_sa_prefetch(const Idx2BWT *bi, size_t n, const uint32_t *idx)
     const double t_start = hsa_now();
     uint32_t *todo = (uint32_t *)malloc(sizeof(uint32_t) * n);
     size_t m = 0;
-    pthread_mutex_lock(&g_sa_mu);
+    pthread_rwlock_rdlock(&g_sa_mu);
     for (size_t i = 0; i < n; ++i) if (!sa_get(idx[i])) todo[m++] = idx[i];
-    pthread_mutex_unlock(&g_sa_mu);
+    pthread_rwlock_unlock(&g_sa_mu);
     if (m) {
         uint32_t *o4 = (uint32_t *)malloc(sizeof(uint32_t) * 4 * m);
         const int rc = hsa_sa_position_batch(hsa_gpu_index_of(bi), m, todo, o4);
         if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
-        pthread_mutex_lock(&g_sa_mu);
+        pthread_rwlock_wrlock(&g_sa_mu);
         for (size_t i = 0; i < m; ++i) sa_put(todo[i], o4 + 4 * i);
-        pthread_mutex_unlock(&g_sa_mu);
+        pthread_rwlock_unlock(&g_sa_mu);
         free(o4);
     }
     free(todo);
@@ -567,30 +568,31 @@ int hsa_splice_sa_prefetch(const Idx2BWT *bi, size_t n, const uint32_t *idx)
 
 void hsa_splice_sa_clear(void)
 {
-    pthread_mutex_lock(&g_sa_mu);
+    pthread_rwlock_wrlock(&g_sa_mu);
     free(g_sa);
     g_sa = NULL;
     g_sa_cap2 = g_sa_n2 = 0;
-    pthread_mutex_unlock(&g_sa_mu);
+    pthread_rwlock_unlock(&g_sa_mu);
 }
 
 void hsa_splice_sa_stats(uint64_t *hits, uint64_t *misses)
 {
-    pthread_mutex_lock(&g_sa_mu);
+    pthread_rwlock_wrlock(&g_sa_mu);
     *hits = g_sa_hits; *misses = g_sa_misses;
     g_sa_hits = g_sa_misses = 0;
-    pthread_mutex_unlock(&g_sa_mu);
+    pthread_rwlock_unlock(&g_sa_mu);
 }
 
 /* BWTRetrievePositionFromSAIndex (2BWT-Interface.c:329) for the splice path. */
 void hsa_splice_sa_position(Idx2BWT *bi, unsigned int sa_index, unsigned int *seq_id, unsigned int *ori_pos,
                             unsigned int *occ_pos)
 {
-    pthread_mutex_lock(&g_sa_mu);
+    pthread_rwlock_rdlock(&g_sa_mu);
     const sa_ent_t *e = sa_get(sa_index);
     sa_ent_t v = e ? *e : (sa_ent_t){0, 0, 0, 0};
-    if (e) ++g_sa_hits; else ++g_sa_misses;
-    pthread_mutex_unlock(&g_sa_mu);
+    if (e) __atomic_fetch_add(&g_sa_hits, 1, __ATOMIC_RELAXED);
+    else __atomic_fetch_add(&g_sa_misses, 1, __ATOMIC_RELAXED);
+    pthread_rwlock_unlock(&g_sa_mu);
     if (e) { sa_write(v.occ, v.sid, v.ori, seq_id, ori_pos, occ_pos); return; }
     co_t *me = tl_co;
     if (me) {                             /* park; the round's lookups are one launch */
@@ -663,20 +665,183 @@ static void co_start(co_t *c, int r, const hsa_splice_read_t *rd)
     c->entered = 0;
 }
 
+/* One host thread of the runner: its coroutines, the reads they take from the shared
+ * queue, and its own scheduling point (tl_sched). */
+typedef struct runner_s runner_t;
+typedef struct {
+    runner_t *R;
+    int id;
+    co_t *co;                 /* this worker's coroutines: global slots [c0, c0 + W) */
+    int W, c0, live;
+    jmp_buf sched;
+    pthread_t th;
+} worker_t;
+
+struct runner_s {
+    const Idx2BWT *bi;
+    hsa_index_t *ix;
+    const hsa_splice_read_t *reads;
+    bwt_aln1_t **out;
+    int *n_out;
+    int n, T;
+    int next;                 /* the next read of the queue (atomic) */
+    pthread_barrier_t bar;
+    int done;                 /* set by the leader: no read is left anywhere */
+    worker_t *w;
+    /* the leader's round: parked calls of every worker */
+    ext_req_t **pend;
+    int32_t *pslot;
+    uint8_t *pdone;
+    co_t **pco;
+    int *wide;
+    uint32_t *sa_idx, *sa_o4;
+    co_t **sa_co;
+    long launches, calls, sa_launches;
+    double t_gpu;
+};
+
+/* Run every runnable coroutine of worker w until it parks or finishes; a finished one
+ * takes the next read of the queue at once. */
+static void worker_round(worker_t *w)
+{
+    runner_t *R = w->R;
+    tl_sched = &w->sched;
+    for (volatile int k = 0; k < w->W; ++k) {       /* volatile: live across _setjmp */
+        co_t *c = w->co + k;
+        while (c->read >= 0 && c->state == 0) {
+            tl_co = c;
+            if (!_setjmp(w->sched)) {
+                if (!c->entered) { c->entered = 1; setcontext(&c->uc); }
+                _longjmp(c->jb, 1);
+            }
+            tl_co = NULL;
+            if (c->state == 2) {
+                R->out[c->read] = c->result;
+                R->n_out[c->read] = c->n_aln;
+                const int r = __atomic_fetch_add(&R->next, 1, __ATOMIC_RELAXED);
+                if (r < R->n) co_start(c, r, R->reads + r);
+                else { c->read = -1; --w->live; }
+            }
+        }
+    }
+}
+
+/* The leader's part of a round: one SA -> position launch and one sliced extension
+ * launch (wide regimes: one hsa_extend_batch) over the parked calls of all workers. */
+static void leader_round(runner_t *R)
+{
+    int np = 0, nsa = 0, nwide = 0, live = 0;
+    for (int t = 0; t < R->T; ++t) {
+        worker_t *w = R->w + t;
+        live += w->live;
+        for (int k = 0; k < w->W; ++k) {
+            co_t *c = w->co + k;
+            if (c->read < 0 || c->state != 1) continue;
+            if (c->req.kind == 1) { R->sa_idx[nsa] = c->req.sa; R->sa_co[nsa++] = c; }
+            else if (c->req.rg.n_stacks > HSA_EXT_SLICE_STACKS) { R->pco[nwide] = c; R->pend[nwide] = &c->req; ++nwide; }
+        }
+    }
+    if (live == 0) { R->done = 1; return; }
+    if (nsa > 0) {                    /* the round's SA -> position lookups: one launch */
+        const double ts = hsa_now();
+        const int rc = hsa_sa_position_batch(R->ix, (size_t)nsa, R->sa_idx, R->sa_o4);
+        if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
+        pthread_rwlock_wrlock(&g_sa_mu);
+        for (int j = 0; j < nsa; ++j) {
+            ext_req_t *q = &R->sa_co[j]->req;
+            sa_write(R->sa_o4[4 * j], R->sa_o4[4 * j + 1], R->sa_o4[4 * j + 2], q->sid_p, q->ori_p, q->occ_p);
+            sa_put(R->sa_idx[j], R->sa_o4 + 4 * j);
+            R->sa_co[j]->state = 0;
+        }
+        pthread_rwlock_unlock(&g_sa_mu);
+        R->t_gpu += hsa_now() - ts;
+        ++R->sa_launches;
+    }
+    /* a call whose regime has more score LIFOs than a slice slot holds (n_stacks > 256,
+     * e.g. -O 120) runs to completion in one hsa_extend_batch launch */
+    if (nwide > 0) {
+        const double tw = hsa_now();
+        run_reqs(R->ix, R->pend, nwide);
+        for (int j = 0; j < nwide; ++j) R->pco[j]->state = 0;
+        R->t_gpu += hsa_now() - tw;
+        R->calls += nwide;
+        ++R->launches;
+    }
+    /* one sliced launch over every other parked extension (slot = its coroutine): the
+     * finished ones resume, the others stay parked with their state on the device */
+    int W = 0;
+    for (int t = 0; t < R->T; ++t) {
+        worker_t *w = R->w + t;
+        for (int k = 0; k < w->W; ++k) {
+            co_t *c = w->co + k;
+            if (c->read >= 0 && c->state == 1 && c->req.kind == 0 && c->req.rg.n_stacks <= HSA_EXT_SLICE_STACKS) {
+                R->pend[np] = &c->req; R->pslot[np] = w->c0 + k; R->pco[np] = c; ++np;
+            }
+        }
+        W += w->W;
+    }
+    if (np == 0) return;
+    const double tg = hsa_now();
+    const int nd = run_slices(R->ix, R->pend, R->pslot, np, W, R->pdone);
+    R->t_gpu += hsa_now() - tg;
+    if (getenv("HSA_EXT_TRACE"))
+        fprintf(stderr, "[hsa_splice_run] round %ld: %d parked, %d finished, %.3f ms\n", R->launches, np, nd,
+                1e3 * (hsa_now() - tg));
+    R->calls += nd;
+    ++R->launches;
+    for (int j = 0; j < np; ++j)
+        if (R->pdone[j]) R->pco[j]->state = 0;
+}
+
+static void *worker_main(void *arg)
+{
+    worker_t *w = (worker_t *)arg;
+    runner_t *R = w->R;
+    for (;;) {
+        worker_round(w);
+        pthread_barrier_wait(&R->bar);
+        if (w->id == 0) leader_round(R);
+        pthread_barrier_wait(&R->bar);
+        if (R->done) break;
+    }
+    tl_sched = NULL;
+    return NULL;
+}
+
+static int runner_threads(int n)
+{
+    const char *e = getenv("HSA_SPLICE_THREADS");
+    int t = e ? atoi(e) : 0;
+    if (t <= 0) {
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        t = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) : 1;
+        if (t > 16) t = 16;                 /* one GPU's share of a shared host */
+    }
+    const int by_reads = (n + 63) / 64;     /* at least 64 reads a thread */
+    if (t > by_reads) t = by_reads;
+    return t < 1 ? 1 : t;
+}
+
 /* bwt_splice_match for reads[0..n) (see the file comment): out[r] / n_out[r] are what
- * bwt_splice_match(aux of read r) returns.  Returns the number of GPU extension
+ * bwt_splice_match(aux of read r) returns.  T host threads run the reads as coroutines
+ * (each thread its own; reads pulled from one queue), and every round's parked calls
+ * of all threads go to the device in one launch.  Returns the number of GPU extension
  * launches. */
 long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int n_stacks, int n,
                     const hsa_splice_read_t *reads, bwt_aln1_t **out, int *n_out)
 {
     if (n <= 0) return 0;
     if (!bwt_splice_match) { for (int r = 0; r < n; ++r) { out[r] = NULL; n_out[r] = 0; } return 0; }
-    hsa_index_t *ix = hsa_gpu_index_of(bi);
-    const int W = n < CO_MAX ? n : CO_MAX;
-    co_t *co = (co_t *)calloc((size_t)W, sizeof(co_t));
-    jmp_buf sched;
-    tl_sched = &sched;
-    for (int k = 0; k < W; ++k) {
+    runner_t R;
+    memset(&R, 0, sizeof R);
+    R.bi = bi; R.ix = hsa_gpu_index_of(bi); R.reads = reads; R.out = out; R.n_out = n_out; R.n = n;
+    const int Wtot = n < CO_MAX ? n : CO_MAX;
+    R.T = runner_threads(n);
+    if (R.T > Wtot) R.T = Wtot;
+    R.w = (worker_t *)calloc((size_t)R.T, sizeof(worker_t));
+    co_t *co = (co_t *)calloc((size_t)Wtot, sizeof(co_t));
+    for (int k = 0; k < Wtot; ++k) {
         co_t *c = co + k;
         /* one guard page below each stack: an overflow faults instead of silently
          * corrupting the neighbouring coroutine's stack */
@@ -699,103 +864,48 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
         c->req.buf = (uint8_t *)malloc(c->req.buf_cap);
         c->read = -1;
     }
-    ext_req_t **pend = (ext_req_t **)malloc(sizeof(ext_req_t *) * (size_t)W);
-    uint32_t *sa_idx = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)W);
-    uint32_t *sa_o4 = (uint32_t *)malloc(sizeof(uint32_t) * 4 * (size_t)W);
-    int *sa_co = (int *)malloc(sizeof(int) * (size_t)W);
-    long sa_launches = 0;
-    int32_t *pslot = (int32_t *)malloc(sizeof(int32_t) * (size_t)W);
-    int *wide = (int *)malloc(sizeof(int) * (size_t)W);
-    uint8_t *pdone = (uint8_t *)malloc((size_t)W);
-    int next = 0, live = 0;
-    long launches = 0, calls = 0;
-    double t_gpu = 0.0;
-    const double t_run = hsa_now();
-    for (int k = 0; k < W; ++k) { co_start(co + k, next, reads + next); ++next; ++live; }
-    while (live > 0) {
-        /* run every runnable coroutine until it parks or finishes; a finished one takes
-         * the next read at once */
-        for (int k = 0; k < W; ++k) {
-            co_t *c = co + k;
-            while (c->read >= 0 && c->state == 0) {
-                tl_co = c;
-                if (!_setjmp(sched)) {
-                    if (!c->entered) { c->entered = 1; setcontext(&c->uc); }
-                    _longjmp(c->jb, 1);
-                }
-                tl_co = NULL;
-                if (c->state == 2) {
-                    out[c->read] = c->result;
-                    n_out[c->read] = c->n_aln;
-                    if (next < n) { co_start(c, next, reads + next); ++next; }
-                    else { c->read = -1; --live; }
-                }
-            }
-        }
-        /* one sliced launch over every parked call (slot = its coroutine): the finished
-         * ones resume, the others stay parked with their state on the device.  A call
-         * whose regime has more buckets than a slot holds (n_stacks > 256, e.g. -o 2
-         * -e 60) runs to completion in one hsa_extend_batch launch with the round's other
-         * such calls. */
-        int np = 0, nsa = 0, nwide = 0;
-        for (int k = 0; k < W; ++k)
-            if (co[k].read >= 0 && co[k].state == 1) {
-                if (co[k].req.kind == 1) { sa_idx[nsa] = co[k].req.sa; sa_co[nsa++] = k; }
-                else if (co[k].req.rg.n_stacks > HSA_EXT_SLICE_STACKS) wide[nwide++] = k;
-                else { pend[np] = &co[k].req; pslot[np++] = k; }
-            }
-        if (nwide > 0) {
-            const double tw = hsa_now();
-            for (int j = 0; j < nwide; ++j) pend[j] = &co[wide[j]].req;
-            run_reqs(ix, pend, nwide);
-            for (int j = 0; j < nwide; ++j) co[wide[j]].state = 0;
-            t_gpu += hsa_now() - tw;
-            calls += nwide;
-            ++launches;
-            np = 0;                       /* pend is rebuilt below */
-            for (int k = 0; k < W; ++k)
-                if (co[k].read >= 0 && co[k].state == 1 && co[k].req.kind == 0 &&
-                    co[k].req.rg.n_stacks <= HSA_EXT_SLICE_STACKS) { pend[np] = &co[k].req; pslot[np++] = k; }
-        }
-        if (nsa > 0) {                    /* the round's SA -> position lookups: one launch */
-            const double ts = hsa_now();
-            const int rc = hsa_sa_position_batch(ix, (size_t)nsa, sa_idx, sa_o4);
-            if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
-            pthread_mutex_lock(&g_sa_mu);
-            for (int j = 0; j < nsa; ++j) {
-                ext_req_t *q = &co[sa_co[j]].req;
-                sa_write(sa_o4[4 * j], sa_o4[4 * j + 1], sa_o4[4 * j + 2], q->sid_p, q->ori_p, q->occ_p);
-                sa_put(sa_idx[j], sa_o4 + 4 * j);
-                co[sa_co[j]].state = 0;
-            }
-            pthread_mutex_unlock(&g_sa_mu);
-            t_gpu += hsa_now() - ts;
-            ++sa_launches;
-        }
-        if (np == 0) continue;
-        const double tg = hsa_now();
-        const int nd = run_slices(ix, pend, pslot, np, W, pdone);
-        t_gpu += hsa_now() - tg;
-        if (getenv("HSA_EXT_TRACE"))
-            fprintf(stderr, "[hsa_splice_run] round %ld: %d parked, %d finished, %.3f ms\n", launches, np, nd,
-                    1e3 * (hsa_now() - tg));
-        calls += nd;
-        ++launches;
-        for (int j = 0; j < np; ++j)
-            if (pdone[j]) co[pslot[j]].state = 0;
+    /* coroutines split evenly over the threads; the first reads handed out in order */
+    for (int t = 0, c0 = 0; t < R.T; ++t) {
+        worker_t *w = R.w + t;
+        const int W = Wtot / R.T + (t < Wtot % R.T);
+        w->R = &R; w->id = t; w->co = co + c0; w->W = W; w->c0 = c0;
+        c0 += W;
     }
-    for (int k = 0; k < W; ++k) {
+    for (int k = 0; k < Wtot; ++k) {
+        for (int t = 0; t < R.T; ++t)
+            if (k >= R.w[t].c0 && k < R.w[t].c0 + R.w[t].W) { ++R.w[t].live; break; }
+        co_start(co + k, k, reads + k);
+    }
+    R.next = Wtot;
+    R.pend = (ext_req_t **)malloc(sizeof(ext_req_t *) * (size_t)Wtot);
+    R.pslot = (int32_t *)malloc(sizeof(int32_t) * (size_t)Wtot);
+    R.pdone = (uint8_t *)malloc((size_t)Wtot);
+    R.pco = (co_t **)malloc(sizeof(co_t *) * (size_t)Wtot);
+    R.sa_idx = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)Wtot);
+    R.sa_o4 = (uint32_t *)malloc(sizeof(uint32_t) * 4 * (size_t)Wtot);
+    R.sa_co = (co_t **)malloc(sizeof(co_t *) * (size_t)Wtot);
+    const double t_run = hsa_now();
+    pthread_barrier_init(&R.bar, NULL, (unsigned)R.T);
+    for (int t = 1; t < R.T; ++t)
+        if (pthread_create(&R.w[t].th, NULL, worker_main, R.w + t)) {
+            fprintf(stderr, "[hsa_splice_run] cannot start a runner thread\n");
+            exit(1);
+        }
+    worker_main(R.w);
+    for (int t = 1; t < R.T; ++t) pthread_join(R.w[t].th, NULL);
+    pthread_barrier_destroy(&R.bar);
+    for (int k = 0; k < Wtot; ++k) {
         co_t *c = co + k;
         munmap((char *)c->stack - CO_GUARD, CO_STACK + CO_GUARD);
         free(c->aux.width_back); free(c->aux.width_fore); free(c->aux.width_seed); free(c->aux.rc_seq);
         stack_free(c->aux.stack);
         free(c->req.buf);
     }
-    free(co); free(pend); free(pslot); free(wide); free(pdone); free(sa_idx); free(sa_o4); free(sa_co);
-    tl_sched = NULL;
+    free(co); free(R.w); free(R.pend); free(R.pslot); free(R.pdone); free(R.pco); free(R.sa_idx); free(R.sa_o4);
+    free(R.sa_co);
     if (getenv("HSA_VERBOSE"))
-        fprintf(stderr, "[hsa] splice runner: %d reads, %ld extension calls in %ld launches, %ld SA lookup launches: "
-                        "%.3f s in the launches (copies included), %.3f s of host splice code\n", n, calls, launches,
-                sa_launches, t_gpu, hsa_now() - t_run - t_gpu);
-    return launches;
+        fprintf(stderr, "[hsa] splice runner: %d reads on %d host threads, %ld extension calls in %ld launches, %ld SA "
+                        "lookup launches: %.3f s in the launches (copies included), %.3f s of host splice code\n", n,
+                R.T, R.calls, R.launches, R.sa_launches, R.t_gpu, hsa_now() - t_run - R.t_gpu);
+    return R.launches;
 }

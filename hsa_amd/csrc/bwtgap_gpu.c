@@ -155,7 +155,7 @@ typedef struct {
 static memo_ent_t *g_memo;
 static size_t g_memo_cap, g_memo_n;
 static uint64_t g_memo_hits, g_memo_misses;
-static pthread_mutex_t g_memo_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_rwlock_t g_memo_mu = PTHREAD_RWLOCK_INITIALIZER;   /* lookups share it */
 static hsa_arena_t g_memo_arena;        /* keys, hits and widths of the entries */
 
 static size_t key_of(const bwt_aux_t *a, uint8_t *buf)
@@ -193,12 +193,12 @@ static uint64_t key_hash(const uint8_t *p, size_t n)
 
 void hsa_splice_memo_clear(void)
 {
-    pthread_mutex_lock(&g_memo_mu);
+    pthread_rwlock_wrlock(&g_memo_mu);
     hsa_arena_free(&g_memo_arena);
     free(g_memo);
     g_memo = NULL;
     g_memo_cap = g_memo_n = 0;
-    pthread_mutex_unlock(&g_memo_mu);
+    pthread_rwlock_unlock(&g_memo_mu);
 }
 
 static void memo_put(const bwt_aux_t *in, const bwt_width_t *wout, const bwt_aln1_t *hits, int n_aln)
@@ -270,12 +270,12 @@ static void sa_list_add(const bwt_aln1_t *h, int n)     /* caller holds g_memo_m
 /* The collected SA indices (ownership passes to the caller, who frees them). */
 size_t hsa_splice_take_sa_list(uint32_t **idx)
 {
-    pthread_mutex_lock(&g_memo_mu);
+    pthread_rwlock_wrlock(&g_memo_mu);
     *idx = g_sa_list;
     const size_t n = g_sa_n;
     g_sa_list = NULL;
     g_sa_n = g_sa_cap = 0;
-    pthread_mutex_unlock(&g_memo_mu);
+    pthread_rwlock_unlock(&g_memo_mu);
     return n;
 }
 
@@ -295,7 +295,7 @@ static void batch_into_memo(bwt_aux_t *calls, int c, bwt_width_t **win, int *n_o
     bwt_match_gap_batch(cp, c, out, n_out);
     const double t1 = hsa_now();
     g_t_search += t1 - t0;
-    pthread_mutex_lock(&g_memo_mu);
+    pthread_rwlock_wrlock(&g_memo_mu);
     for (int i = 0; i < c; ++i) {
         bwt_width_t *after = calls[i].width_back;
         const int alias = calls[i].width_seed == after;
@@ -305,7 +305,7 @@ static void batch_into_memo(bwt_aux_t *calls, int c, bwt_width_t **win, int *n_o
         sa_list_add(out[i], n_out[i]);
         free(after); free(out[i]);
     }
-    pthread_mutex_unlock(&g_memo_mu);
+    pthread_rwlock_unlock(&g_memo_mu);
     g_t_put += hsa_now() - t1;
     free(cp); free(out);
 }
@@ -493,10 +493,10 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
 /* Table statistics since the last call (hits, misses), for logs. */
 void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses)
 {
-    pthread_mutex_lock(&g_memo_mu);
+    pthread_rwlock_wrlock(&g_memo_mu);
     *hits = g_memo_hits; *misses = g_memo_misses;
     g_memo_hits = g_memo_misses = 0;
-    pthread_mutex_unlock(&g_memo_mu);
+    pthread_rwlock_unlock(&g_memo_mu);
 }
 
 /* bwt_match_gap (bwtgap.c:118, declared bwtgap.h:26): the reference's entry point,
@@ -504,19 +504,19 @@ void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses)
  * Same return contract: a calloc'd array, never NULL, freed by the caller. */
 bwt_aln1_t *bwt_match_gap(bwt_aux_t *aux, int *_n_aln)
 {
-    pthread_mutex_lock(&g_memo_mu);
+    pthread_rwlock_rdlock(&g_memo_mu);
     const memo_ent_t *e = memo_get(aux);
     if (e) {
-        ++g_memo_hits;
+        __atomic_fetch_add(&g_memo_hits, 1, __ATOMIC_RELAXED);
         bwt_aln1_t *out = (bwt_aln1_t *)calloc((size_t)aln_capacity(e->n_aln), sizeof(bwt_aln1_t));
         if (e->n_aln > 0) memcpy(out, e->hits, sizeof(bwt_aln1_t) * (size_t)e->n_aln);
         memcpy(aux->width_back, e->wout, sizeof(bwt_width_t) * ((size_t)e->len + 1));
         *_n_aln = e->n_aln;
-        pthread_mutex_unlock(&g_memo_mu);
+        pthread_rwlock_unlock(&g_memo_mu);
         return out;
     }
-    if (g_memo_n) ++g_memo_misses;
-    pthread_mutex_unlock(&g_memo_mu);
+    if (g_memo_n) __atomic_fetch_add(&g_memo_misses, 1, __ATOMIC_RELAXED);
+    pthread_rwlock_unlock(&g_memo_mu);
     bwt_aln1_t *out = NULL;
     bwt_match_gap_batch(&aux, 1, &out, _n_aln);
     return out;
