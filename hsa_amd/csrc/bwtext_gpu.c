@@ -665,6 +665,65 @@ static void co_start(co_t *c, int r, const hsa_splice_read_t *rd)
     c->entered = 0;
 }
 
+/* The coroutines (stacks, per-read buffers, the stack object the host's code sees) are
+ * kept between calls: a batch's splice path is short, and mapping, guarding and
+ * unmapping thousands of stacks per call cost as much as running them (and the
+ * unmaps' TLB shootdowns grow with the runner's threads). */
+static co_t *g_co;
+static int g_co_n, g_co_len, g_co_stacks;
+static pthread_mutex_t g_co_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static co_t *co_pool(int W, int max_len, int n_stacks)
+{
+    if (W > g_co_n) {
+        co_t *p = (co_t *)realloc(g_co, sizeof(co_t) * (size_t)W);
+        if (!p) { fprintf(stderr, "[hsa_splice_run] out of memory\n"); exit(1); }
+        memset(p + g_co_n, 0, sizeof(co_t) * (size_t)(W - g_co_n));
+        g_co = p;
+        for (int k = g_co_n; k < W; ++k) {
+            co_t *c = g_co + k;
+            /* one guard page below each stack: an overflow faults instead of silently
+             * corrupting the neighbouring coroutine's stack */
+            void *m = mmap(NULL, CO_STACK + CO_GUARD, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
+                           -1, 0);
+            if (m == MAP_FAILED || mprotect(m, CO_GUARD, PROT_NONE)) {
+                fprintf(stderr, "[hsa_splice_run] cannot map a coroutine stack\n");
+                exit(1);
+            }
+            c->stack = (char *)m + CO_GUARD;
+        }
+        g_co_n = W;
+    }
+    if (max_len > g_co_len || n_stacks != g_co_stacks) {
+        const int len = max_len > g_co_len ? max_len : g_co_len;
+        for (int k = 0; k < g_co_n; ++k) {
+            co_t *c = g_co + k;
+            if (c->aux.stack) stack_free(c->aux.stack);
+            free(c->aux.width_back); free(c->aux.width_fore); free(c->aux.width_seed); free(c->aux.rc_seq);
+            free(c->req.buf);
+            c->aux.stack = NULL;
+        }
+        g_co_len = len;
+        g_co_stacks = n_stacks;
+    }
+    for (int k = 0; k < W; ++k) {
+        co_t *c = g_co + k;
+        if (!c->aux.stack) {
+            c->aux.width_back = (bwt_width_t *)calloc((size_t)g_co_len + 1, sizeof(bwt_width_t));
+            c->aux.width_fore = (bwt_width_t *)calloc((size_t)g_co_len + 1, sizeof(bwt_width_t));
+            c->aux.width_seed = (bwt_width_t *)calloc((size_t)g_co_len + 1, sizeof(bwt_width_t));
+            c->aux.rc_seq = (ubyte_t *)calloc((size_t)g_co_len + 1, 1);
+            c->aux.stack = stack_new(n_stacks);
+            c->req.buf_cap = 5 * ((size_t)g_co_len + 4);    /* the largest window: the read and both bounds */
+            c->req.buf = (uint8_t *)malloc(c->req.buf_cap);
+        }
+        c->read = -1;
+        c->state = 0;
+        c->entered = 0;
+    }
+    return g_co;
+}
+
 /* One host thread of the runner: its coroutines, the reads they take from the shared
  * queue, and its own scheduling point (tl_sched). */
 typedef struct runner_s runner_t;
@@ -697,7 +756,8 @@ struct runner_s {
     uint32_t *sa_idx, *sa_o4;
     co_t **sa_co;
     long launches, calls, sa_launches;
-    double t_gpu;
+    double t_gpu, t_setup, t_work;   /* t_work: the rounds' slowest worker, summed */
+    double *busy;                    /* per worker, the round's coroutine time */
 };
 
 /* Run every runnable coroutine of worker w until it parks or finishes; a finished one
@@ -798,9 +858,16 @@ static void *worker_main(void *arg)
     worker_t *w = (worker_t *)arg;
     runner_t *R = w->R;
     for (;;) {
+        const double t0 = hsa_now();
         worker_round(w);
+        R->busy[w->id] = hsa_now() - t0;
         pthread_barrier_wait(&R->bar);
-        if (w->id == 0) leader_round(R);
+        if (w->id == 0) {
+            double mx = 0.0;
+            for (int t = 0; t < R->T; ++t) mx = R->busy[t] > mx ? R->busy[t] : mx;
+            R->t_work += mx;
+            leader_round(R);
+        }
         pthread_barrier_wait(&R->bar);
         if (R->done) break;
     }
@@ -840,29 +907,13 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     R.T = runner_threads(n);
     if (R.T > Wtot) R.T = Wtot;
     R.w = (worker_t *)calloc((size_t)R.T, sizeof(worker_t));
-    co_t *co = (co_t *)calloc((size_t)Wtot, sizeof(co_t));
+    const double t_setup = hsa_now();
+    pthread_mutex_lock(&g_co_mu);
+    co_t *co = co_pool(Wtot, max_len, n_stacks);
     for (int k = 0; k < Wtot; ++k) {
-        co_t *c = co + k;
-        /* one guard page below each stack: an overflow faults instead of silently
-         * corrupting the neighbouring coroutine's stack */
-        void *m = mmap(NULL, CO_STACK + CO_GUARD, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE,
-                       -1, 0);
-        if (m == MAP_FAILED || mprotect(m, CO_GUARD, PROT_NONE)) {
-            fprintf(stderr, "[hsa_splice_run] cannot map a coroutine stack\n");
-            exit(1);
-        }
-        c->stack = (char *)m + CO_GUARD;
-        c->aux.bi_bwt = (Idx2BWT *)bi;
-        c->aux.arr = arr;
-        c->aux.max_len = max_len;
-        c->aux.width_back = (bwt_width_t *)calloc((size_t)max_len + 1, sizeof(bwt_width_t));
-        c->aux.width_fore = (bwt_width_t *)calloc((size_t)max_len + 1, sizeof(bwt_width_t));
-        c->aux.width_seed = (bwt_width_t *)calloc((size_t)max_len + 1, sizeof(bwt_width_t));
-        c->aux.rc_seq = (ubyte_t *)calloc((size_t)max_len + 1, 1);
-        c->aux.stack = stack_new(n_stacks);
-        c->req.buf_cap = 5 * ((size_t)max_len + 4);    /* the largest window: the read and both bounds */
-        c->req.buf = (uint8_t *)malloc(c->req.buf_cap);
-        c->read = -1;
+        co[k].aux.bi_bwt = (Idx2BWT *)bi;
+        co[k].aux.arr = arr;
+        co[k].aux.max_len = max_len;
     }
     /* coroutines split evenly over the threads; the first reads handed out in order */
     for (int t = 0, c0 = 0; t < R.T; ++t) {
@@ -884,7 +935,9 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     R.sa_idx = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)Wtot);
     R.sa_o4 = (uint32_t *)malloc(sizeof(uint32_t) * 4 * (size_t)Wtot);
     R.sa_co = (co_t **)malloc(sizeof(co_t *) * (size_t)Wtot);
+    R.busy = (double *)calloc((size_t)R.T, sizeof(double));
     const double t_run = hsa_now();
+    R.t_setup = t_run - t_setup;
     pthread_barrier_init(&R.bar, NULL, (unsigned)R.T);
     for (int t = 1; t < R.T; ++t)
         if (pthread_create(&R.w[t].th, NULL, worker_main, R.w + t)) {
@@ -894,18 +947,13 @@ long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int
     worker_main(R.w);
     for (int t = 1; t < R.T; ++t) pthread_join(R.w[t].th, NULL);
     pthread_barrier_destroy(&R.bar);
-    for (int k = 0; k < Wtot; ++k) {
-        co_t *c = co + k;
-        munmap((char *)c->stack - CO_GUARD, CO_STACK + CO_GUARD);
-        free(c->aux.width_back); free(c->aux.width_fore); free(c->aux.width_seed); free(c->aux.rc_seq);
-        stack_free(c->aux.stack);
-        free(c->req.buf);
-    }
-    free(co); free(R.w); free(R.pend); free(R.pslot); free(R.pdone); free(R.pco); free(R.sa_idx); free(R.sa_o4);
-    free(R.sa_co);
+    pthread_mutex_unlock(&g_co_mu);
+    free(R.w); free(R.pend); free(R.pslot); free(R.pdone); free(R.pco); free(R.sa_idx); free(R.sa_o4);
+    free(R.sa_co); free(R.busy);
     if (getenv("HSA_VERBOSE"))
         fprintf(stderr, "[hsa] splice runner: %d reads on %d host threads, %ld extension calls in %ld launches, %ld SA "
-                        "lookup launches: %.3f s in the launches (copies included), %.3f s of host splice code\n", n,
-                R.T, R.calls, R.launches, R.sa_launches, R.t_gpu, hsa_now() - t_run - R.t_gpu);
+                        "lookup launches: %.3f s in the launches (copies included), %.3f s of host splice code "
+                        "(rounds' slowest worker %.3f s, set-up %.3f s)\n", n, R.T, R.calls, R.launches, R.sa_launches,
+                R.t_gpu, hsa_now() - t_run - R.t_gpu, R.t_work, R.t_setup);
     return R.launches;
 }
