@@ -343,6 +343,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (ix->d_ovf2) (void)hipFree(ix->d_ovf2);
     if (ix->d_any) (void)hipFree(ix->d_any);
     if (ix->d_any_aux) (void)hipFree(ix->d_any_aux);
+    if (ix->d_split) (void)hipFree(ix->d_split);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
     (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);

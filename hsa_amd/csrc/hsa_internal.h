@@ -60,6 +60,7 @@ struct hsa_index {
     // k_search_any (hsa_search_any.h): per-lane scratch, job lists and counters, regimes
     void *d_any = nullptr; size_t d_any_cap = 0;
     void *d_any_aux = nullptr; size_t d_any_aux_cap = 0;
+    void *d_split = nullptr; size_t d_split_cap = 0;   // strand-split items' results (k_split_finalize)
     // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;

@@ -109,6 +109,14 @@ struct SearchArgs {
     uint32_t *wq;                  // k_widths: rank queries of each forward-strand width row
     uint32_t batch_k;              // rare-event batching: at most this many lanes wait (see (A) in k_search)
     uint32_t batch_idle;           //   ... or run once the waiting lanes have idled this many lane-iterations
+    // strand-split mode (small batches): work item p searches ONE strand of list position
+    // p >> 1 (p even: rc, odd: fwd) on its own lane, so a read's two searches run side by
+    // side instead of one after the other; k_split_finalize keeps the fwd strand only
+    // when rc has no hit (bwtaln.c:343-359) and counts its work only then
+    uint32_t split;
+    int32_t *sp_n;                 // per item: hits, or -1 for a capacity overflow
+    uint64_t *sp_off;
+    uint32_t *sp_q, *sp_p;         //   its rank queries and pops (counted by the finalize)
 };
 
 // The kernel's arguments re-read from the kernarg segment where a rare path uses them
@@ -489,6 +497,52 @@ static __global__ void __launch_bounds__(BLOCK) k_widths_export(SearchArgs a)
 }
 
 
+// Strand-split mode, after k_search: per read, the rc strand's result if it has a hit,
+// else the fwd strand's (bwtaln.c:343-359), else the splice fallback; the fwd search and
+// its widths count as the reference's work only then.  A read whose deciding strand
+// overflowed its lane goes to the next capacity pass whole (both strands, in order).
+static __global__ void __launch_bounds__(BLOCK) k_split_finalize(SearchArgs a)
+{
+    const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    unsigned long long q_add = 0, p_add = 0, w_add = 0;
+    if (q < n_jobs) {
+        const int job = a.job_list ? a.job_list[q] : (int)q;
+        const int32_t nr = a.sp_n[2 * q], nf = a.sp_n[2 * q + 1];
+        int32_t na = 0;
+        uint32_t fl = 0;
+        uint64_t off = 0;
+        if (nr < 0 || (nr == 0 && nf < 0)) {
+            fl = HSA_F_OVERFLOW;
+            if (a.ovf_list) a.ovf_list[atomicAdd(&a.ctr[a.ovf_ctr], 1ull)] = job;
+            else atomicAdd(&a.ctr[11], 1ull);
+        } else if (nr > 0) {
+            na = nr; off = a.sp_off[2 * q];
+            q_add = a.sp_q[2 * q]; p_add = a.sp_p[2 * q];
+        } else {
+            w_add = a.wq[q];
+            q_add = (unsigned long long)a.sp_q[2 * q] + a.sp_q[2 * q + 1] + w_add;
+            p_add = (unsigned long long)a.sp_p[2 * q] + a.sp_p[2 * q + 1];
+            if (nf > 0) { na = nf; off = a.sp_off[2 * q + 1]; }
+            else fl = HSA_F_FALLBACK;
+        }
+        a.n_aln[job] = na;
+        a.flags[job] = fl;
+        a.hit_off[job] = off;
+    }
+    // one atomic per wave and counter
+    for (int d = 32; d >= 1; d >>= 1) {
+        q_add += __shfl_xor(q_add, d);
+        p_add += __shfl_xor(p_add, d);
+        w_add += __shfl_xor(w_add, d);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (q_add) atomicAdd(&a.ctr[2], q_add);
+        if (p_add) atomicAdd(&a.ctr[4], p_add);
+        if (w_add) { atomicAdd(&a.ctr[7], w_add); atomicAdd(&a.ctr[14], w_add); }
+    }
+}
+
 // NT = lanes per workgroup: 256, or 64 when per-lane LDS (many buckets, long reads)
 // would leave fewer than 16 waves per CU in 256-lane workgroups (plan_launch)
 // HUGE: the last capacity pass (reads that overflowed the big pass): 32-bit pool
@@ -565,6 +619,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     // per-lane statistics (a lane's counts of one launch stay far below 2^32); kept in
     // VGPRs: wave-uniform accumulators pushed the kernel's SGPRs into spills
     uint32_t st_p = 0, st_wq = 0, st_q = 0, st_b = 0;
+    uint32_t sq0 = 0, sp0 = 0;            // split mode: the counters when the item started
     const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
 #ifdef HSA_DIAG
     uint32_t dc[18] = {0};
@@ -709,6 +764,16 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     };
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
         const ColdArgs r = cold_args();
+        if (r->split) {                       // one strand of a read: k_split_finalize decides
+            const uint32_t pi = qpos * 2u + (1u - C_STRAND(ctl));
+            r->sp_n[pi] = (fl & HSA_F_OVERFLOW) ? -1 : na;
+            r->sp_off[pi] = ho;
+            r->sp_q[pi] = st_q - sq0;
+            r->sp_p[pi] = st_p - sp0;
+            st_q = sq0; st_p = sp0;
+            SET_PH(ctl, PH_IDLE);
+            return;
+        }
         const int job = r->job_list ? r->job_list[qpos] : (int)qpos;
         if (fl & HSA_F_OVERFLOW) {
             if (r->ovf_list) r->ovf_list[atomicAdd(&r->ctr[r->ovf_ctr], 1ull)] = job;   // re-run by the next pass
@@ -758,8 +823,8 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 }
             }
             finish_job(0, n_aln, o);
-        } else if (cold_args()->mg) {
-            finish_job(0, 0, 0);        // one call, one strand
+        } else if (cold_args()->mg || cold_args()->split) {
+            finish_job(0, 0, 0);        // one call (or one split item), one strand
         } else if (C_STRAND(ctl)) {
             ctl &= ~(1u << 3);          // strand 0
             st_wq += cold_args()->wq[qpos];   // its widths are the reference's work now (bwtaln.c:344-348)
@@ -883,9 +948,10 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 base = __shfl(base, leader);
                 if (need) {
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
-                    if (j < (unsigned long long)n_jobs) {
-                        qpos = (uint32_t)j;
-                        const int job = r->job_list ? r->job_list[j] : (int)j;
+                    if (j < (unsigned long long)n_jobs << (r->split ? 1 : 0)) {
+                        const uint32_t item = (uint32_t)j;
+                        qpos = r->split ? item >> 1 : item;
+                        const int job = r->job_list ? r->job_list[qpos] : (int)qpos;
                         const hsa_job_t J = r->jobs[job];
                         opt_max_diff = J.max_diff;
                         const uint32_t len = J.len;
@@ -901,6 +967,8 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                             const uint32_t has_seed = (int)len > J.seed_len;
                             ctl = 8u | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 | len << 10 |
                                   (has_seed ? (uint32_t)J.seed_len : 0u) << 20;     // strand 1 (rc first, bwtaln.c:343)
+                            if (r->split && (item & 1u)) ctl &= ~8u;              // split: odd items search fwd
+                            sq0 = st_q; sp0 = st_p;
                         }
                         const hsa_regime_t *R = s_reg + (J.regime & 1);
                         pen = (uint32_t)R->s_mm | (uint32_t)R->s_gapo << 10 | (uint32_t)R->s_gape << 20;
@@ -1274,6 +1342,7 @@ struct LaunchPlan {
     size_t lds;
     bool huge;                       // PASS_HUGE: 32-bit links, reused slots
     uint32_t ntab;                   // score table entries per regime in LDS
+    size_t resident;                 // lanes resident on the chip (every CU full)
 };
 
 // The capacity passes of one search: MAIN (every read), BIG (the reads that overflowed
@@ -1352,6 +1421,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     if (per_cu < 1) { hsa_set_error("search kernel does not fit (LDS %zu)", P.lds); return HSA_E_ARG; }
     const uint32_t NTB = P.nt;
     size_t blocks = (size_t)ix->n_cu * per_cu;
+    P.resident = blocks * NTB;
     size_t need_blocks = ((size_t)n_jobs + NTB - 1) / NTB;
     if (P.huge) {
         blocks = 1;                                          // 64 lanes: a handful of reads
@@ -1475,6 +1545,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.batch_k = (uint32_t)g_batch_k;
     A.batch_idle = (uint32_t)g_batch_idle;
     A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0; A.ovf_ctr = 8;
+    A.split = 0; A.sp_n = nullptr; A.sp_off = nullptr; A.sp_q = nullptr; A.sp_p = nullptr;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg)) : nullptr;
@@ -1482,14 +1553,33 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     return A;
 }
 
+// Strand-split mode for the main pass of a small batch: each read's two strands on two
+// lanes when both fit on the chip at once (HSA_SPLIT=0/1 forces it off/on).  A read's
+// search chain halves (rc and fwd side by side); the fwd strand's work is speculative, so
+// large batches, which fill every lane anyway, keep one read per lane.
+static bool use_split(const LaunchPlan &P, int n, const unsigned long long *n_dev, const MgPass *mg, uint32_t qctr)
+{
+    if (mg || n_dev || qctr != 0 || P.huge || n <= 0) return false;
+    const char *e = getenv("HSA_SPLIT");
+    if (e) return atoi(e) != 0;
+    return 2 * (size_t)n <= P.resident;
+}
+
 template <typename IT = uint32_t>
-static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, const hsa_regime_t *d_regimes,
+static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, const hsa_regime_t *d_regimes,
                        const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
                        int max_seed, const uint8_t *d_codes, int32_t *d_n, uint32_t *d_fl, uint64_t *d_ho,
                        uint32_t *d_hits, uint64_t hit_cap, unsigned long long *d_ctr, hipStream_t st,
                        int32_t *ovf_list = nullptr, const unsigned long long *n_dev = nullptr, uint32_t qctr = 0,
                        const MgPass *mg = nullptr, uint32_t ovf_ctr = 8)
 {
+    const bool split = use_split(P0, n, n_dev, mg, qctr);
+    LaunchPlan P = P0;
+    if (split) {                                        // lanes for 2 n items
+        const size_t need = (2 * (size_t)n + P.nt - 1) / P.nt, cap = P.resident / P.nt;
+        P.blocks = need < cap ? need : cap;
+        P.lanes = P.blocks * P.nt;
+    }
     // 64-bit intervals: two uint4 per pool entry, 10 staged words per hit (HitW)
     constexpr size_t EW = sizeof(IT) / 4;
     int rc = hsa_scratch_reserve(S, P.lanes, P.pcap * EW, P.hcap * EW, P.huge ? 4 : 2);
@@ -1525,6 +1615,16 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     SearchArgs A = pass_args<IT>(ix, P, S, d_regimes, d_bmap, d_jobs, d_list, n, max_len, max_seed, d_codes, d_n, d_fl,
                                  d_ho, d_hits, hit_cap, d_ctr, nullptr);
     A.ovf_list = ovf_list; A.n_dev = n_dev; A.qctr = qctr; A.ovf_ctr = ovf_ctr;
+    if (split) {
+        const size_t m = 2 * (size_t)n, al = (m * 8 + 255) / 256 * 256;
+        if ((rc = hsa_grow(&ix->d_split, &ix->d_split_cap, 3 * al))) return rc;
+        char *d = (char *)ix->d_split;
+        A.split = 1;
+        A.sp_off = (uint64_t *)d;
+        A.sp_n = (int32_t *)(d + al);
+        A.sp_q = (uint32_t *)(d + al + al / 2);
+        A.sp_p = (uint32_t *)(d + 2 * al);
+    }
     if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
     size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
     if (wblocks < 1) wblocks = 1;
@@ -1535,6 +1635,12 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P, SearchScratch &S, con
     if (P.wide) launch_search<uint16_t, IT>(P, A, st);
     else launch_search<uint8_t, IT>(P, A, st);
     HSA_HIP(hipGetLastError());
+    if (split) {
+        const unsigned nb = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
+        hipLaunchKernelGGL(k_split_finalize, dim3(nb), dim3(BLOCK), 0, st, A);
+        HSA_HIP(hipGetLastError());
+        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] strand-split main pass: %d reads on %zu lanes\n", n, P.lanes);
+    }
     return 0;
 }
 

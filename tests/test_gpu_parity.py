@@ -102,6 +102,15 @@ def test_search_matches_reference(name):
     _compare(name)
 
 
+@pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "tiny_edge_default", "rep_gap60_default", "tiny_gap100_n4o1_b400"])
+def test_search_matches_reference_one_lane_per_read(name, monkeypatch):
+    """Batches smaller than the chip run strand-split (each read's rc and fwd searches on
+    two lanes, k_split_finalize choosing, bwtaln.c:343-359); this is the one-read-per-lane
+    main pass that large batches use, on the same golden cases."""
+    monkeypatch.setenv("HSA_SPLIT", "0")
+    _compare(name)
+
+
 @pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "rep_mm100_n4o1"])
 def test_overflow_rerun_is_exact(name):
     """A tiny per-lane pool forces most reads through the large-capacity re-run."""
@@ -180,12 +189,15 @@ def test_device_path_rerun_is_exact():
     assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("case", ["tiny_mm100_n4o0", "tiny_gap100_n4o1", "rep_mm100_n4o1"])
-def test_rank_queries_match_oracle(case):
+def test_rank_queries_match_oracle(case, split, monkeypatch):
     """The roofline numerator: the rank queries the kernels count (d_counters[2]) are
     the ones the reference algorithm issues -- widths only for the strands it
     searches (bwtaln.c:343-359), 2 per bidirectional step -- exactly the oracle's
-    count on the same reads (no read overflows at the default capacity)."""
+    count on the same reads (no read overflows at the default capacity) -- also in the
+    strand-split main pass, which counts a fwd search only when rc had no hit."""
+    monkeypatch.setenv("HSA_SPLIT", split)
     got, (_, _, _, st) = _device_run(case)
     assert got["c"][8] == 0
     assert int(got["c"][2]) == int(st[0]), (int(got["c"][2]), int(st[0]))
