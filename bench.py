@@ -59,6 +59,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_QUERY = 64    # one 64-byte HBM sector per Occ query
 SA_INTERVAL = 8         # the .sa sampling of `HSA index` (2BWT-Builder.c:97)
 REF_BATCH = 100_000     # bwa_aln_core's batch (bwtaln.c:477)
+PASS_RING = 1024        # per-pass kernel events the library keeps (hsa_index::PASS_RING)
 
 
 def log(*a):
@@ -544,7 +545,9 @@ def main():
         gi, res, extra = build_index64(T, GENOME_SEED, device)
     else:
         gi, res, extra = build_index(T, GENOME_SEED, device, with_files=ref_legs)
-    log(f"[bench] rank {rank}: index ready ({gi.nbytes() / 2**30:.2f} GiB of rank blocks) in {time.time() - t0:.1f} s")
+    trie_d, trie_sd, trie_b = gi.trie()
+    log(f"[bench] rank {rank}: index ready ({gi.nbytes() / 2**30:.2f} GiB of rank blocks, root tries {trie_d}/{trie_sd} "
+        f"levels in {trie_b / 2**20:.0f} MiB) in {time.time() - t0:.1f} s")
 
     # reads: rank r searches batches r, r+world, ... of one global stream (seed 5)
     t0 = time.time()
@@ -650,9 +653,10 @@ def main():
     kms = [e0.elapsed_time(e1) for e0, e1 in ev]
     # per-kernel device time of every timed step: HIP events the library records on
     # its stream around k_widths and k_search (+ its overflow re-run) of each pass
-    w_ms, s_ms = gi.pass_times(a.steps)
+    n_pt = min(a.steps, PASS_RING)             # the library keeps the newest PASS_RING passes
+    w_ms, s_ms = gi.pass_times(n_pt)
     w_ms, s_ms = w_ms.astype(float), s_ms.astype(float)
-    seeds_ms = np.array(kms) - w_ms - s_ms if a.config == 4 else None
+    seeds_ms = np.array(kms[-n_pt:]) - w_ms - s_ms if a.config == 4 else None
     log(f"[bench] rank {rank}: per-step kernels: k_widths {np.mean(w_ms):.2f} ms, k_search {np.mean(s_ms):.2f} ms"
         + (f", splice seeds {np.mean(seeds_ms):.2f} ms" if a.config == 4 else ""))
     if os.environ.get("HSA_DIAG_OUT"):
@@ -774,6 +778,10 @@ def main():
                          "rank_queries_per_read": round(queries / reads_local, 1),
                          "k_search_rank_queries_per_read": round(q_search / reads_local, 1),
                          "sectors_per_query": round(blocks / max(queries, 1), 4),
+                         "tries": {"width_depth": trie_d, "search_depth": trie_sd, "bytes": trie_b,
+                                   "loads_per_read": round(int(ctr[:, 10].sum()) / reads_local, 1),
+                                   "what": "steps answered by one root-trie load instead of a rank pair "
+                                           "(hsa_amd/csrc/hsa_trie.h); they still count as the reference's queries"},
                          "bytes_per_query": BYTES_PER_QUERY,
                          "peak_random_sector_measured": round(rand_gbs, 1),
                          "peak_random_sector_measured_coop4x16": round(coop_gbs, 1),

@@ -30,7 +30,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_cal_sa_reg_gap_multi", "hsa_index_create_device64", "hsa_index_is64", "hsa_occ4_batch64",
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
-    "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced",
+    "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced", "hsa_index_trie",
 ]
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
@@ -167,6 +167,7 @@ def lib():
     L.hsa_index_free.argtypes = [vp]
     L.hsa_index_bytes.restype = C.c_size_t
     L.hsa_index_bytes.argtypes = [vp]
+    L.hsa_index_trie.argtypes = [vp, C.c_void_p, C.c_void_p, C.c_void_p]
     L.hsa_index_stream.restype = vp
     L.hsa_index_stream.argtypes = [vp]
     L.hsa_occ4_batch.argtypes = [vp, C.c_int, C.c_size_t, u32, u32]
@@ -352,6 +353,12 @@ class GpuIndex:
 
     def nbytes(self) -> int:
         return int(lib().hsa_index_bytes(self.h))
+
+    def trie(self):
+        """(width-trie depth, search-trie depth, bytes) of the index's root tries."""
+        d, sd, b = C.c_uint32(), C.c_uint32(), C.c_size_t()
+        check(lib().hsa_index_trie(self.h, C.byref(d), C.byref(sd), C.byref(b)))
+        return int(d.value), int(sd.value), int(b.value)
 
     def occ4(self, d, pos):
         pos = np.ascontiguousarray(pos, np.uint32)

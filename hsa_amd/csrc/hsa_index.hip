@@ -15,6 +15,7 @@
 
 #include "hsa_device.h"
 #include "hsa_internal.h"
+#include "hsa_trie.h"
 
 static thread_local char g_err[1024] = "";
 int g_waves_per_cu = 16;
@@ -231,6 +232,74 @@ RankDir64 hsa_rank_dir64(const hsa_index *ix, int dir)
     return RankDir64{ix->blk[dir], dir ? ix->risa0_64 : ix->isa0_64, ix->any_wrap[dir] ? 1u : 0u};
 }
 
+// The root tries of hsa_trie.h, level by level on the index's stream.  The width trie
+// (k_widths) has HSA_TRIE_DEPTH levels (0 = none; by default 12, less for a text shorter
+// than 4^(D-1) characters, whose deeper levels would hold mostly empty strings).  The
+// search trie (k_search) is built only when HSA_TRIE_MODE >= 1 at index creation, with
+// min(D, HSA_TRIE_SDEPTH or 11) levels: k_search measured slower with it.
+template <typename IT, typename RD>
+static int build_tries_t(hsa_index *ix, RD fwd, RD rev, IT T, const IT *C)
+{
+    uint32_t D = HSA_TRIE_DEFAULT_DEPTH;
+    if (const char *e = getenv("HSA_TRIE_DEPTH")) {        // as asked (tests: tries deeper than the text)
+        D = (uint32_t)atoi(e);
+        if (D > HSA_TRIE_MAX_DEPTH) D = HSA_TRIE_MAX_DEPTH;
+    } else {
+        while (D > 0 && (1ull << (2 * D)) > 4ull * (uint64_t)T) --D;
+    }
+    uint32_t Ds = 0;
+    if (const char *m = getenv("HSA_TRIE_MODE"); m && atoi(m) >= 1) {
+        Ds = 11;
+        if (const char *sd = getenv("HSA_TRIE_SDEPTH")) Ds = (uint32_t)atoi(sd);
+        Ds = Ds < D ? Ds : D;
+    }
+    ix->trie_depth = ix->trie_sdepth = 0;
+    if (D == 0) return 0;
+    const size_t es = sizeof(IT) == 4 ? 16 : 32, ws = sizeof(IT) == 4 ? 8 : 16;
+    const size_t nw = trie_base(D + 1), ns = Ds ? trie_base(Ds + 1) : 0;
+    HSA_HIP(hipMalloc(&ix->d_trie_w, nw * ws));
+    if (Ds) {
+        HSA_HIP(hipMalloc(&ix->d_trie_s, ns * es));
+        HSA_HIP(hipMalloc(&ix->d_trie_m, trie_mbase(Ds) + 16));
+    }
+    TrieC<IT> Cv;
+    for (int c = 0; c < 4; ++c) Cv.v[c] = C[c];
+    unsigned *d_bad = nullptr, bad = 0;
+    HSA_HIP(hipMalloc(&d_bad, 4));
+    HSA_HIP(hipMemsetAsync(d_bad, 0, 4, ix->stream));
+    for (uint32_t d = 0; d < D; ++d) {
+        const unsigned nb = (unsigned)(((1ull << (2 * d)) + 255) / 256);
+        if (d < Ds)
+            hipLaunchKernelGGL((k_trie_search_level<IT, RD>), dim3(nb), dim3(256), 0, ix->stream, fwd, T, Cv, d,
+                               ix->d_trie_s, ix->d_trie_m, d_bad);
+        hipLaunchKernelGGL((k_trie_width_level<IT, RD>), dim3(nb), dim3(256), 0, ix->stream, rev, T, Cv, d, ix->d_trie_w,
+                           d_bad);
+        HSA_HIP(hipGetLastError());
+    }
+    HSA_HIP(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, ix->stream));
+    HSA_HIP(hipStreamSynchronize(ix->stream));
+    (void)hipFree(d_bad);
+    if (bad) {                      // the two BWTs disagree: no trie (rank steps only)
+        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] root tries: intervals past the text, not kept\n");
+        (void)hipFree(ix->d_trie_w); (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m);
+        ix->d_trie_w = nullptr; ix->d_trie_s = nullptr; ix->d_trie_m = nullptr;
+        return 0;
+    }
+    ix->trie_depth = D;
+    ix->trie_sdepth = Ds;
+    ix->trie_wide = sizeof(IT) == 8;
+    ix->trie_bytes = nw * ws + ns * es + (Ds ? trie_mbase(Ds) : 0);
+    return 0;
+}
+
+static int build_tries(hsa_index *ix)
+{
+    if (ix->wide)
+        return build_tries_t<uint64_t, RankDir64>(ix, hsa_rank_dir64(ix, 0), hsa_rank_dir64(ix, 1), ix->T64, ix->C64);
+    return build_tries_t<uint32_t, RankDir>(ix, RankDir{ix->blk[0], ix->isa0}, RankDir{ix->blk[1], ix->risa0}, ix->T,
+                                            ix->C);
+}
+
 int hsa_need32(const hsa_index *ix)
 {
     if (!ix->is64) return 0;
@@ -272,7 +341,7 @@ extern "C" int hsa_index_create_device(int device, uint32_t T, uint32_t isa0, co
     ix->T = T; ix->isa0 = isa0; memcpy(ix->C, C, sizeof ix->C);
     ix->rT = rT; ix->risa0 = risa0; memcpy(ix->rC, rC, sizeof ix->rC);
     if ((rc = build_blocks(ix, 0, T, d_code_lsb, ix->stream)) ||
-        (rc = build_blocks(ix, 1, rT, d_rcode_lsb, ix->stream))) {
+        (rc = build_blocks(ix, 1, rT, d_rcode_lsb, ix->stream)) || (rc = build_tries(ix))) {
         hsa_index_free(ix);
         return rc;
     }
@@ -302,7 +371,7 @@ extern "C" int hsa_index_create_device64(int device, uint64_t T, uint64_t isa0, 
         for (int c = 0; c < 5; ++c) { ix->C[c] = (uint32_t)C[c]; ix->rC[c] = (uint32_t)rC[c]; }
     }
     if ((rc = build_blocks(ix, 0, T, d_code_lsb, ix->stream)) || (rc = build_blocks(ix, 1, rT, d_rcode_lsb, ix->stream)) ||
-        (rc = build_wraps(ix, 0, ix->stream)) || (rc = build_wraps(ix, 1, ix->stream))) {
+        (rc = build_wraps(ix, 0, ix->stream)) || (rc = build_wraps(ix, 1, ix->stream)) || (rc = build_tries(ix))) {
         hsa_index_free(ix);
         return rc;
     }
@@ -346,6 +415,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (ix->d_split) (void)hipFree(ix->d_split);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
     (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
+    (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m); (void)hipFree(ix->d_trie_w);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
     if (ix->evm) (void)hipEventDestroy(ix->evm);
@@ -361,6 +431,13 @@ extern "C" size_t hsa_index_bytes(const hsa_index_t *ix)
     return (ix->nblk[0] + ix->nblk[1]) * 16;
 }
 extern "C" int hsa_index_is64(const hsa_index_t *ix) { return ix->is64 ? 1 : 0; }
+extern "C" int hsa_index_trie(const hsa_index_t *ix, uint32_t *depth, uint32_t *sdepth, size_t *bytes)
+{
+    if (depth) *depth = ix->trie_depth;
+    if (sdepth) *sdepth = ix->trie_sdepth;
+    if (bytes) *bytes = ix->trie_bytes;
+    return 0;
+}
 extern "C" int hsa_index_device(const hsa_index_t *ix) { return ix->device; }
 extern "C" void *hsa_index_stream(const hsa_index_t *ix) { return (void *)ix->stream; }
 

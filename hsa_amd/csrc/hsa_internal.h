@@ -65,6 +65,15 @@ struct hsa_index {
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;
     uint64_t *d_ctr = nullptr;
+    // root tries (hsa_trie.h): every string of up to trie_depth characters; built with
+    // the index's interval width (trie_wide: 64-bit entries), 0 = none
+    uint4 *d_trie_s = nullptr;          // search trie entries (levels 1..D)
+    uint8_t *d_trie_m = nullptr;        // search trie child masks (levels 0..D-1)
+    void *d_trie_w = nullptr;           // width trie entries (levels 1..D)
+    uint32_t trie_depth = 0;            // width trie levels
+    uint32_t trie_sdepth = 0;           // search trie levels (0: not built)
+    bool trie_wide = false;
+    size_t trie_bytes = 0;
     unsigned char staged[1280];         // last regime block copied to d_in (skip identical re-copies)
     int staged_valid = 0;
     bool staged_mmb = false;            // staged regimes: bucket == n_mm (see mm_buckets)
@@ -73,7 +82,7 @@ struct hsa_index {
     hipEvent_t evm = nullptr;           // between k_widths and k_search of the last pass (timing split)
     // hsa_search_device passes: start / between k_widths and k_search / end, per pass, in a
     // ring (hsa_pass_times), so a caller can time every launch of a back-to-back run
-    static constexpr int PASS_RING = 64;
+    static constexpr int PASS_RING = 1024;
     hipEvent_t pev[PASS_RING][3] = {};
     uint64_t pev_n = 0;
     hipEvent_t ev_split = nullptr;      // recorded by launch_pass between k_widths and k_search

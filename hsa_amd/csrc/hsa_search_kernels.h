@@ -43,6 +43,7 @@
 
 #include "hsa_device.h"
 #include "hsa_internal.h"
+#include "hsa_trie.h"
 
 #define MODE_GAPE 0x01
 #define MODE_LOGGAP 0x04
@@ -117,6 +118,15 @@ struct SearchArgs {
     int32_t *sp_n;                 // per item: hits, or -1 for a capacity overflow
     uint64_t *sp_off;
     uint32_t *sp_q, *sp_p;         //   its rank queries and pops (counted by the finalize)
+    // root tries (hsa_trie.h) of the index, ktd levels (0: none, or not of this
+    // instantiation's interval width): k_search (ungapped regimes) answers the steps of
+    // strings up to ktd characters from kts / ktm, k_widths from ktw
+    const uint4 *kts;
+    const uint8_t *ktm;
+    const void *ktw;
+    uint32_t ktd;                  // width trie levels
+    uint32_t ksd;                  // search trie levels k_search uses (0: none)
+    uint32_t kjm;                  // characters an exact tail jumps per trie load
 };
 
 // The kernel's arguments re-read from the kernarg segment where a rare path uses them
@@ -344,25 +354,35 @@ template <typename IT> struct WChain {
     uint32_t bid;
     IT prevw;
     uint32_t acc;
+    uint32_t tl, tix;              // width trie: characters since the last reset, and their node
 };
 
 template <typename WT, typename IT>
 __device__ __forceinline__ void width_step(const SearchArgs &a, WChain<IT> &ch, uint32_t t, uint32_t n, uint32_t c,
                                            uint32_t cbits, uint32_t *__restrict__ brow, IT *__restrict__ wrow,
-                                           uint32_t &st_q, uint32_t &st_b)
+                                           uint32_t &st_q, uint32_t &st_b, uint32_t &st_t)
 {
     using F = WFmt<WT>;
     IT w;
     if (t < n) {
         if (c < 4) {
-            IT ok, ol;
-            st_b += occ1_pair(Ix<IT>::rev(a), ch.k, ch.l + 1u, c, ok, ol);
+            if (ch.tl < a.ktd) {
+                // a string of <= ktd characters since the reset: its interval from the
+                // width trie (the same forward extension, hsa_trie.h)
+                ch.tix = ch.tix * 4u + c;
+                ++ch.tl;
+                trie_w_load<IT>(a.ktw, trie_base(ch.tl) + ch.tix, ch.k, ch.l);
+                ++st_t;
+            } else {
+                IT ok, ol;
+                st_b += occ1_pair(Ix<IT>::rev(a), ch.k, ch.l + 1u, c, ok, ol);
+                const IT cc = pick4(Ix<IT>::C(a), c);
+                ch.k = cc + ok + 1u;
+                ch.l = cc + ol;
+            }
             st_q += 2;
-            const IT cc = pick4(Ix<IT>::C(a), c);
-            ch.k = cc + ok + 1u;
-            ch.l = cc + ol;
         }
-        if (ch.k > ch.l || c > 3) { ch.k = 0; ch.l = Ix<IT>::T(a); ++ch.bid; }
+        if (ch.k > ch.l || c > 3) { ch.k = 0; ch.l = Ix<IT>::T(a); ++ch.bid; ch.tl = 0; ch.tix = 0; }
         w = ch.l - ch.k + 1u;
     } else {
         w = 0; ++ch.bid;                                         // width[len] = {0, ++bid}
@@ -395,8 +415,8 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
     uint32_t *const brow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.wb)) + rb * (a.rb / 4) * 64 + rl;
     uint32_t *const srow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.ws)) + rb * (a.rs / 4) * 64 + rl;
     IT *const wrow = reinterpret_cast<IT *>(a.wg) + rb * a.rg * 64 + rl;
-    WChain<IT> f{0, Ix<IT>::T(a), 0, 0, 0}, sd{0, Ix<IT>::T(a), 0, 0, 0};
-    uint32_t st_q = 0, st_b = 0;
+    WChain<IT> f{0, Ix<IT>::T(a), 0, 0, 0, 0, 0}, sd{0, Ix<IT>::T(a), 0, 0, 0, 0, 0};
+    uint32_t st_q = 0, st_b = 0, st_t = 0;
 #ifdef HSA_DIAG
     uint32_t du = 0, dw = 0;
 #endif
@@ -412,10 +432,10 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
 #endif
         const uint32_t cf = t < len ? base(t) : 4u;
         // the read's elements also carry the strand sequence's base (k_search's getc)
-        width_step<WT, IT>(a, f, t, len, cf, t < len ? F::code_bits(cf) : 0u, brow, wrow, st_q, st_b);
+        width_step<WT, IT>(a, f, t, len, cf, t < len ? F::code_bits(cf) : 0u, brow, wrow, st_q, st_b, st_t);
         if (has_seed && t <= slen) {
             const uint32_t cs = t < slen ? base(s0 + t) : 4u;
-            width_step<WT, IT>(a, sd, t, slen, cs, 0u, srow, nullptr, st_q, st_b);
+            width_step<WT, IT>(a, sd, t, slen, cs, 0u, srow, nullptr, st_q, st_b, st_t);
         }
     }
     // rank queries: the reverse-complement strand is always searched (bwtaln.c:343);
@@ -429,6 +449,7 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
         atomicAdd(&a.ctr[13], (unsigned long long)st_q);
     }
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
+    if (st_t) atomicAdd(&a.ctr[10], (unsigned long long)st_t);
 #ifdef HSA_DIAG
     atomicAdd(&g_dctr[18], (unsigned long long)du);
     atomicAdd(&g_dctr[19], (unsigned long long)dw);
@@ -618,7 +639,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     E e{0, 0, 0, 0};
     // per-lane statistics (a lane's counts of one launch stay far below 2^32); kept in
     // VGPRs: wave-uniform accumulators pushed the kernel's SGPRs into spills
-    uint32_t st_p = 0, st_wq = 0, st_q = 0, st_b = 0;
+    uint32_t st_p = 0, st_wq = 0, st_q = 0, st_b = 0, st_t = 0;
     uint32_t sq0 = 0, sp0 = 0;            // split mode: the counters when the item started
     const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
 #ifdef HSA_DIAG
@@ -987,8 +1008,13 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         TMARK(0);
 #endif
         // ---------------- (B) control until a rank step is needed
+        // req: 1 rank pair at rp1, rp2; from the root trie (ungapped regimes, nodes of
+        // fewer than ktd characters, which hold their trie node in e.x): 2 an exact tail's
+        // jump (entry rp1; tq = characters | N-stop << 8 | depth << 9), 3 an expansion's
+        // child mask (byte rp1), 4 an expansion's four children at the last level (rp1..+3)
         int req = 0;
         IT rp1 = 0, rp2 = 0;
+        uint32_t tq = 0;
 #ifdef HSA_DIAG
         if (lane == 0) DC(5);
 #endif
@@ -1055,12 +1081,41 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
                 continue;
             }
+            // a trie node: ungapped, the strand longer than the trie (so no trie node is
+            // ever a hit), fewer than ktd characters matched
+            const uint32_t dep = (uint32_t)(C_LEN(ctl) - ei);
+            const bool tn = !GAPS && (uint32_t)C_LEN(ctl) > a.ksd && dep < a.ksd;
             if (em == 0 && (M_ST(m) == ST_M || (R_MODE & MODE_GAPE) || M_GE(m) == R_MAXGE)) {
+                if (tn) {
+                    // bwt_match_exact from a trie node: the read's next bases down to the
+                    // trie's last level (or to an N) in one load
+                    const uint32_t jm = a.ksd - dep < a.kjm ? a.ksd - dep : a.kjm;
+                    uint32_t idx = e.x, j = 0;
+                    bool nstop = false;
+#pragma unroll
+                    for (uint32_t t = 0; t < HSA_TRIE_MAX_DEPTH; ++t) {
+                        if (t < jm && !nstop) {
+                            const uint32_t c = getc(ei - 1 - (int)t);
+                            if (c > 3) nstop = true;
+                            else { idx = idx * 4u + c; ++j; }
+                        }
+                    }
+                    if (j == 0) continue;                                 // an N first (2BWT-Interface.c:377)
+                    req = 2; rp1 = (IT)(trie_base(dep + j) + idx);
+                    tq = j | (nstop ? 256u : 0u) | dep << 9;
+                    SET_PH(ctl, PH_EXACT);
+                    break;
+                }
                 ik = e.x; il = e.y; aux = e.z + (e.y - e.x); pos = (uint32_t)(ei - 1);   // bwt_match_exact
                 SET_PH(ctl, PH_EXACT);
                 continue;
             }
-            req = 1; rp1 = e.x; rp2 = e.y + 1u;
+            if (tn) {
+                req = dep + 1u < a.ksd ? 3 : 4;
+                rp1 = (IT)(req == 3 ? trie_mbase(dep) + e.x : trie_base(a.ksd) + 4ull * e.x);
+            } else {
+                req = 1; rp1 = e.x; rp2 = e.y + 1u;
+            }
             if constexpr (F::NIB) cur_c = getc(ei - 1);                  // the expansion's base (D)
             SET_PH(ctl, PH_EXPAND);
         }
@@ -1083,8 +1138,22 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
         }
 #endif
         uint32_t two = 0;
-        if (req) two = occ_pair(Ix<IT>::fwd(a), rp1, rp2, oa, ob) - 1u;
-        if (req) { st_q += 2u; st_b += 1u + two; }
+        IT rkt[4];
+        uint32_t tL = 0, tm = 0;
+        if (req == 1) {
+            two = occ_pair(Ix<IT>::fwd(a), rp1, rp2, oa, ob) - 1u;
+            st_q += 2u; st_b += 1u + two;
+        } else if (req == 2) {
+            trie_s_load<IT>(a.kts, (uint64_t)rp1, oa[0], ob[0], rkt[0], tL);
+            ++st_t;
+        } else if (req == 3) {
+            tm = a.ktm[(uint64_t)rp1];
+            st_q += 2u; ++st_t;
+        } else if (req == 4) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) trie_s_load<IT>(a.kts, (uint64_t)rp1 + c, oa[c], ob[c], rkt[c], tL);
+            st_q += 2u; ++st_t;
+        }
 
 #ifdef HSA_DIAG
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1092,9 +1161,25 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 #endif
         // ---------------- (D) apply
         const uint32_t ph = C_PH(ctl);
-        if (F::NIB && req && ph == PH_EXACT && cur_c > 3) {
+        if (F::NIB && req == 1 && ph == PH_EXACT && cur_c > 3) {
             st_q -= 2u; st_b -= 1u + two;                                // not a step (2BWT-Interface.c:377)
             SET_PH(ctl, PH_POP);
+        } else if (req == 2) {
+            // the trie's exact jump: the steps bwt_match_exact takes until its interval
+            // empties (L) or it meets an N or the trie's last level; from there on, rank
+            // steps (PH_EXACT)
+            const uint32_t j = tq & 255u, dep = tq >> 9;
+            st_q += 2u * (tL ? tL - dep : j);
+            if (tL || (tq & 256u)) {
+                SET_PH(ctl, PH_POP);
+            } else {
+                ik = oa[0]; il = ob[0]; aux = rkt[0] + (ob[0] - oa[0]);
+                pos = (uint32_t)M_I(e.w) - 1u - j;
+                // the write-back guard (2BWT-Interface.c:383-386) reads the start entry's
+                // k, l, rev_k, rev_l: of a node, only the root's k and rev_k are zero
+                if (dep == 0) { e.x = 0; e.y = TT; e.z = 0; }
+                else { e.x = 1; e.y = 1; e.z = 1; }
+            }
         } else if (req && ph == PH_EXACT) {
             // BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170), one character
             const uint32_t c = F::NIB ? cur_c : getc((int)pos);
@@ -1124,7 +1209,8 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             const int em = m_of(m);
             const int len = C_LEN(ctl);
             IT srk[4];
-            {
+            uint32_t ne = 0;                                             // children that occur
+            if (req == 1) {
                 IT oc = 0;
 #pragma unroll
                 for (int c = 3; c >= 0; --c) {
@@ -1134,6 +1220,18 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                     srk[c] = (erl - oc) - (ob[c] - oa[c]);
                     oc += d;
                 }
+            } else if (req == 3) {
+                // children of fewer than ktd characters: trie nodes 4 idx + c
+#pragma unroll
+                for (int c = 0; c < 4; ++c) { oa[c] = ek * 4u + (IT)c; ob[c] = 0; srk[c] = 0; }
+                ne = tm;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) srk[c] = rkt[c];
+            }
+            if (req != 3) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) ne |= (oa[c] <= ob[c] ? 1u : 0u) << c;
             }
             int allow_diff = 1, allow_M = 1;
             if (i > 0) {
@@ -1164,9 +1262,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
                 const int ies = RG(indel_end_skip);
                 const int tmp = (R_MODE & MODE_LOGGAP) ? int_log2((uint32_t)(ege + ego)) / 2 + 1 : ego + ege;
                 if (i >= ies + tmp && len - i >= ies + tmp) {
-                    uint32_t dm = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) dm |= (oa[j] <= ob[j] ? 1u : 0u) << j;
+                    const uint32_t dm = ne;
                     const IT occ = el - ek + 1u;
                     if (est == ST_M) {
                         if (ego < R_MAXGO) cand = 1u | dm << 1;
@@ -1181,10 +1277,10 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
 #pragma unroll
                 for (int j = 1; j <= 4; ++j) {
                     const uint32_t c = (sc + (uint32_t)j) & 3u;
-                    cand |= (pick4(oa, c) <= pick4(ob, c) ? 1u : 0u) << (4 + j);
+                    cand |= ((ne >> c) & 1u) << (4 + j);
                 }
             } else if (sc < 4) {
-                cand |= (pick4(oa, sc) <= pick4(ob, sc) ? 1u : 0u) << 8;    // == bit 8: c = sc, no mismatch
+                cand |= ((ne >> sc) & 1u) << 8;                              // == bit 8: c = sc, no mismatch
             }
             // entry of candidate bit b
             auto entry = [&](uint32_t b) -> E {
@@ -1236,6 +1332,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     atomicAdd(&a.ctr[2], (unsigned long long)st_q);
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);
+    if (st_t) atomicAdd(&a.ctr[10], (unsigned long long)st_t);
     if (st_wq) {
         atomicAdd(&a.ctr[2], (unsigned long long)st_wq);
         atomicAdd(&a.ctr[7], (unsigned long long)st_wq);
@@ -1546,6 +1643,18 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.batch_idle = (uint32_t)g_batch_idle;
     A.ovf_list = nullptr; A.n_dev = nullptr; A.qctr = 0; A.ovf_ctr = 8;
     A.split = 0; A.sp_n = nullptr; A.sp_off = nullptr; A.sp_q = nullptr; A.sp_p = nullptr;
+    const char *te = getenv("HSA_TRIE");           // HSA_TRIE=0: rank steps only (A/B runs)
+    const bool tr = ix->trie_depth > 0 && ix->trie_wide == (sizeof(IT) == 8) && !(te && atoi(te) == 0);
+    A.kts = tr ? ix->d_trie_s : nullptr;
+    A.ktm = tr ? ix->d_trie_m : nullptr;
+    A.ktw = tr ? ix->d_trie_w : nullptr;
+    A.ktd = tr ? ix->trie_depth : 0u;
+    // the search trie (built only on request, HSA_TRIE_MODE >= 1 at index creation;
+    // HSA_TRIE_MODE=0 at search time turns it off again, 2 = one level per exact step)
+    const char *tm = getenv("HSA_TRIE_MODE");
+    const int mode = tm ? atoi(tm) : 1;
+    A.ksd = tr && mode ? ix->trie_sdepth : 0u;
+    A.kjm = mode == 2 ? 1u : HSA_TRIE_MAX_DEPTH;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg)) : nullptr;

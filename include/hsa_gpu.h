@@ -89,6 +89,12 @@ void hsa_index_free(hsa_index_t *ix);
 void *hsa_index_stream(const hsa_index_t *ix);
 size_t hsa_index_bytes(const hsa_index_t *ix);
 int  hsa_index_device(const hsa_index_t *ix);
+/* The index's root tries (hsa_amd/csrc/hsa_trie.h): every string of up to *depth
+ * characters with the interval k_widths' forward extension computes for it (0: none;
+ * HSA_TRIE_DEPTH at creation, default 12), and the search trie's levels (*sdepth; built
+ * only when HSA_TRIE_MODE >= 1 at creation); *bytes of device memory they take.  Their
+ * loads are counted in d_counters[10]. */
+int  hsa_index_trie(const hsa_index_t *ix, uint32_t *depth, uint32_t *sdepth, size_t *bytes);
 
 /* Rank/step/width primitives over host arrays (tests and tools). */
 int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t *pos, uint32_t *occ4_out);
@@ -179,6 +185,7 @@ long hsa_search_batch(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regime
  *        bidirectional step, 2 per width step of every strand it searches
  *        (bwtaln.c:343-359); a read re-run for capacity counts its work twice
  *   [3]  64-byte rank sectors fetched    [4] gap_pop calls
+ *   [10] steps answered by a root-trie load instead of rank queries (hsa_index_trie)
  *   [7]  the width queries among [2]
  *   [8]  reads that overflowed their lane's capacity in the main pass (8 192 pool
  *        slots, 32 768 with gap opens), re-run on the device in the BIG pass (65 535
@@ -212,7 +219,7 @@ int hsa_search_device(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regime
 /* Device time of the two kernels of the last pass on this index (k_widths, then
  * k_search with its overflow re-run); waits for that pass to finish. */
 int hsa_last_pass_ms(hsa_index_t *ix, float *widths_ms, float *search_ms);
-/* The same for each of the last n (<= 64) hsa_search_device passes, oldest first:
+/* The same for each of the last n (<= 1024) hsa_search_device passes, oldest first:
  * HIP events recorded on the launch stream around each kernel of every pass. */
 int hsa_pass_times(hsa_index_t *ix, int n, float *widths_ms, float *search_ms);
 /* Kernel geometry/capacity knobs: 0 leaves a knob unchanged; pool_entries < 0 restores

@@ -55,6 +55,30 @@ typedef struct {
  * sharing one index do not contend on a counter) */
 static __thread uint64_t tl_queries;
 
+#ifdef OR_DEPTH_HIST
+/* Experiment build only (liboracle_hist.so, tools/exp/depth_hist.py): rank steps by the
+ * length of the string they extend to (the trie depth), and how many of them touch two
+ * different 16-character rank blocks.  [0]/[1] search steps (expansions and exact
+ * tails), [2]/[3] bwt_cal_width steps (depth since the last reset). */
+static __thread uint64_t tl_hist[4][64];
+static __thread int tl_depth;
+#define HIST_DEPTH(d) (tl_depth = (d) < 63 ? (d) : 63)
+static void hist_pair(int which, bw_t i0, bw_t i1, bw_t isa0)
+{
+    i0 -= (i0 > isa0); i1 -= (i1 > isa0);
+    tl_hist[which][tl_depth]++;
+    if (i0 / 16 != i1 / 16) tl_hist[which + 1][tl_depth]++;
+}
+void OR(depth_hist)(uint64_t *out, int reset)
+{
+    memcpy(out, tl_hist, sizeof tl_hist);
+    if (reset) memset(tl_hist, 0, sizeof tl_hist);
+}
+#else
+#define HIST_DEPTH(d) ((void)0)
+#define hist_pair(w, a, b, c) ((void)0)
+#endif
+
 struct or_index {
     or_bwt_t f, r;
     int unused;
@@ -216,6 +240,7 @@ static void step_all(or_index_t *ix, bw_t k, bw_t l, bw_t rk, bw_t rl, bw_t ok[4
     occ4(&ix->f, k, oL);
     occ4(&ix->f, l + 1, oR);
     tl_queries += 2;
+    hist_pair(0, k, l + 1, ix->f.isa0);
     oC[3] = 0;
     for (int c = 2; c >= 0; --c) oC[c] = oC[c + 1] + oR[c + 1] - oL[c + 1];
     for (int c = 0; c < 4; ++c) {
@@ -247,6 +272,9 @@ static int match_exact(or_index_t *ix, const uint8_t *seq, int len, bw_t *sk, bw
     bw_t k = *sk, l = *sl, rk = *srk, rl = *srl;
     for (int i = len - 1; i >= 0; i--) {
         if (seq[i] > 3) return 0;
+#ifdef OR_DEPTH_HIST
+        HIST_DEPTH(tl_depth + 1);
+#endif
         step1(ix, seq[i], &k, &l, &rk, &rl);
         if (k > l) break;
     }
@@ -264,6 +292,9 @@ static int cal_width(or_index_t *ix, int len, const uint8_t *str, bw_t *w)
 {
     bw_t k = 0, l = ix->f.T;
     int bid = 0;
+#ifdef OR_DEPTH_HIST
+    int j0 = 0;
+#endif
     for (int i = 0; i < len; ++i) {
         uint8_t c = str[i];
         if (c < 4) {
@@ -271,10 +302,19 @@ static int cal_width(or_index_t *ix, int len, const uint8_t *str, bw_t *w)
             occ4(&ix->r, k, a);
             occ4(&ix->r, l + 1, b);
             tl_queries += 2;
+#ifdef OR_DEPTH_HIST
+            HIST_DEPTH(i - j0 + 1);
+            hist_pair(2, k, l + 1, ix->r.isa0);
+#endif
             k = ix->f.C[c] + a[c] + 1;
             l = ix->f.C[c] + b[c];
         }
-        if (k > l || c > 3) { k = 0; l = ix->f.T; ++bid; }
+        if (k > l || c > 3) {
+            k = 0; l = ix->f.T; ++bid;
+#ifdef OR_DEPTH_HIST
+            j0 = i + 1;
+#endif
+        }
         w[2 * i] = l - k + 1;
         w[2 * i + 1] = (bw_t)bid;
     }
@@ -496,6 +536,7 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
         if (i > 0 && m < (int)width[2 * (i - 1) + 1]) continue;
         if (i == 0) hit = 1;
         else if (m == 0 && (e.state == ST_M || (opt->mode & MODE_GAPE) || e.n_gape == opt->max_gape)) {
+            HIST_DEPTH(len - i);
             if (match_exact(ix, seq, i, &k, &l, &rk, &rl)) hit = 1;
             else continue;
         }
@@ -529,6 +570,7 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
             continue;
         }
         --i;
+        HIST_DEPTH(len - i);
         step_all(ix, k, l, rk, rl, sk, sl, srk, srl);
         occ = l - k + 1;
         allow_diff = allow_M = 1;

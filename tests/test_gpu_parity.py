@@ -117,17 +117,18 @@ def test_overflow_rerun_is_exact(name):
     _compare(name, pool_entries=64)
 
 
-def _device_run(case, pool_entries=0, cap=None):
+def _device_run(case, pool_entries=0, cap=None, ix=None, args=None):
     """One hsa_search_device call (device-resident batch, bench.py's path) on a golden
     case as a steady-state batch (GAPE already cleared: both regimes coincide), and
-    the oracle's bwa_cal_sa_reg_gap on the same reads."""
+    the oracle's bwa_cal_sa_reg_gap on the same reads.  ix: an index of the case's
+    genome (default: the cached one); args: options instead of the case's."""
     import torch
     from hsa_amd._lib import JOB_DTYPE, DeviceBatch, GapOpt, configure, pad_codes, regime_of
     from oracle_ctypes import Opt, OracleIndex, default_opt
     g = load_case(case)
     fwd, rev = index_io.read_index(INDEX[g["index"]])
-    ix = gpu_index(g["index"])
-    od = parse_opts(g["args"], default_opt())
+    ix = gpu_index(g["index"]) if ix is None else ix
+    od = parse_opts(g["args"] if args is None else args.split(), default_opt())
     od["mode"] &= ~0x01
     # the device path searches every job it is given: keep the reads that pass
     # bwa_cal_sa_reg_gap's filters (bwtaln.c:314-325; the drop-in applies them on the host)
