@@ -196,22 +196,44 @@ template <typename IT> struct Ent {
     IT x, y, z;
     uint32_t w;
 };
-// Slot s of a lane's pool: uint4 element base + s * 64 (32-bit entries) or the two
-// elements base + s * 128 and base + s * 128 + 64 (64-bit entries); base (pool_base)
-// is the lane's slot 0, computed once per launch.
+#ifndef HSA_POOL_CHUNK
+#define HSA_POOL_CHUNK 1
+#endif
+// Slot s of a lane's pool.  Default: uint4 element base + s * 64 (32-bit entries) or the
+// two elements base + s * 128 and base + s * 128 + 64 (64-bit entries); base (pool_base)
+// is the lane's slot 0, computed once per launch.  HSA_POOL_CHUNK: 64-byte chunks of
+// consecutive slots per lane (4 entries, or 2 of 64 bits), chunk q of lane l at
+// (q * 64 + l) * 64 B in the wave's region, so an expansion's burst of pushes
+// (consecutive slots) writes whole sectors; the links likewise, 32 per 64 B.  The wave's
+// region is sized for pcap rounded up to 32 slots (the scratch reservation does so).
 template <typename IT>
 __device__ __forceinline__ size_t pool_base(size_t wv, uint32_t pcap, int lane)
 {
+#if HSA_POOL_CHUNK
+    return (sizeof(IT) == 4 ? 1u : 2u) * wv * (size_t)((pcap + 31u) & ~31u) * 64 + (size_t)lane * 4;
+#else
     return (sizeof(IT) == 4 ? 1u : 2u) * wv * pcap * 64 + (size_t)lane;
+#endif
+}
+template <typename IT>
+__device__ __forceinline__ size_t ent_at(size_t base, uint32_t slot)
+{
+#if HSA_POOL_CHUNK
+    constexpr uint32_t EQ = sizeof(IT) == 4 ? 4u : 2u, U = sizeof(IT) == 4 ? 1u : 2u;
+    return base + (size_t)(slot / EQ) * 256 + (slot % EQ) * U;
+#else
+    return base + (size_t)slot * (sizeof(IT) == 4 ? 64 : 128);
+#endif
 }
 template <typename IT>
 __device__ __forceinline__ Ent<IT> ent_load(const uint4 *pool, size_t base, uint32_t slot)
 {
+    const size_t i = ent_at<IT>(base, slot);
     if constexpr (sizeof(IT) == 4) {
-        const uint4 v = pool[base + (size_t)slot * 64];
+        const uint4 v = pool[i];
         return Ent<IT>{v.x, v.y, v.z, v.w};
     } else {
-        const uint4 u = pool[base + (size_t)slot * 128], v = pool[base + (size_t)slot * 128 + 64];
+        const uint4 u = pool[i], v = pool[i + (HSA_POOL_CHUNK ? 1 : 64)];
         return Ent<IT>{(uint64_t)u.x | (uint64_t)u.y << 32, (uint64_t)u.z | (uint64_t)u.w << 32,
                        (uint64_t)v.x | (uint64_t)v.y << 32, v.z};
     }
@@ -219,11 +241,12 @@ __device__ __forceinline__ Ent<IT> ent_load(const uint4 *pool, size_t base, uint
 template <typename IT>
 __device__ __forceinline__ void ent_store(uint4 *pool, size_t base, uint32_t slot, const Ent<IT> &e)
 {
+    const size_t i = ent_at<IT>(base, slot);
     if constexpr (sizeof(IT) == 4) {
-        pool[base + (size_t)slot * 64] = make_uint4(e.x, e.y, e.z, e.w);
+        pool[i] = make_uint4(e.x, e.y, e.z, e.w);
     } else {
-        pool[base + (size_t)slot * 128] = make_uint4((uint32_t)e.x, (uint32_t)(e.x >> 32), (uint32_t)e.y, (uint32_t)(e.y >> 32));
-        pool[base + (size_t)slot * 128 + 64] = make_uint4((uint32_t)e.z, (uint32_t)(e.z >> 32), e.w, 0u);
+        pool[i] = make_uint4((uint32_t)e.x, (uint32_t)(e.x >> 32), (uint32_t)e.y, (uint32_t)(e.y >> 32));
+        pool[i + (HSA_POOL_CHUNK ? 1 : 64)] = make_uint4((uint32_t)e.z, (uint32_t)(e.z >> 32), e.w, 0u);
     }
 }
 // staged words per hit (HB) and words per output hit record: bwt_aln1_t (bwtaln.h:41-50)
@@ -607,9 +630,14 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
     // (w * cap + e) * 64 + l, so one wave's accesses stay inside one small region
     // (few pages) and lanes at equal e coalesce
     const size_t wv = gid >> 6;
+#if HSA_POOL_CHUNK
+    const size_t link0 = wv * (size_t)((a.pcap + 31u) & ~31u) * 64 + (size_t)lane * 32;   // the lane's slot-0 link
+#define NXT(s) reinterpret_cast<LT *>(a.nxt)[link0 + (size_t)((s) >> 5) * 2048 + ((s) & 31u)]
+#else
     const size_t link0 = wv * a.pcap * 64 + (size_t)lane;        // the lane's slot-0 link
-    const size_t pbase = pool_base<IT>(wv, a.pcap, lane);        // ... and slot-0 pool entry
 #define NXT(s) reinterpret_cast<LT *>(a.nxt)[link0 + (size_t)(s) * 64]
+#endif
+    const size_t pbase = pool_base<IT>(wv, a.pcap, lane);        // ... and slot-0 pool entry
 #define HB(i) r->hbuf[(wv * r->hcap * HW + (uint32_t)(i)) * 64 + lane]   // r = cold_args() in scope
 #define HEAD(b) s_heads[(uint32_t)(b) * NT + tid]
     // pruning elements in LDS, word-interleaved: the word holding elements
@@ -1691,7 +1719,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
     }
     // 64-bit intervals: two uint4 per pool entry, 10 staged words per hit (HitW)
     constexpr size_t EW = sizeof(IT) / 4;
-    int rc = hsa_scratch_reserve(S, P.lanes, P.pcap * EW, P.hcap * EW, P.huge ? 4 : 2);
+    int rc = hsa_scratch_reserve(S, P.lanes, (size_t)((P.pcap + 31u) & ~31u) * EW, P.hcap * EW, P.huge ? 4 : 2);
     if (rc) return rc;
     const uint32_t esz = P.wide ? 2u : 1u;
     const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;

@@ -11,6 +11,6 @@ make -C $S -s
 /opt/rocm/bin/hipcc $F $X -c $S/hsa_search.hip -o $D/s.o &
 /opt/rocm/bin/hipcc $F $X -c $S/hsa_search64.hip -o $D/s64.o &
 wait
-/opt/rocm/bin/hipcc $F -shared $D/s.o $D/s64.o $S/hsa_index.o $S/hsa_bwt_build.o $S/hsa_sa.o $S/bwtaln_gpu.o $S/bwtgap_gpu.o -lpthread -lm -o $S/../libhsa_gpu_$N.so
+/opt/rocm/bin/hipcc $F -shared $D/s.o $D/s64.o $S/hsa_index.o $S/hsa_bwt_build.o $S/hsa_sa.o $S/hsa_extend.o $S/bwtaln_gpu.o $S/bwtgap_gpu.o $S/bwtse_gpu.o $S/bwtext_gpu.o -lpthread -lm -o $S/../libhsa_gpu_$N.so
 rm -rf $D
 echo built hsa_amd/libhsa_gpu_$N.so
