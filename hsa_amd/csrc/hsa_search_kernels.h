@@ -196,6 +196,12 @@ template <typename IT> struct Ent {
     IT x, y, z;
     uint32_t w;
 };
+// The search trie in k_search (hsa_trie.h; ungapped regimes): measured slower than the
+// rank steps it replaces, so compiled only into experiment builds
+// (tools/build_variant.sh strie -DHSA_SEARCH_TRIE=1); k_widths' width trie is always in.
+#ifndef HSA_SEARCH_TRIE
+#define HSA_SEARCH_TRIE 0
+#endif
 #ifndef HSA_POOL_CHUNK
 #define HSA_POOL_CHUNK 1
 #endif
@@ -1112,7 +1118,7 @@ __global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
             // a trie node: ungapped, the strand longer than the trie (so no trie node is
             // ever a hit), fewer than ktd characters matched
             const uint32_t dep = (uint32_t)(C_LEN(ctl) - ei);
-            const bool tn = !GAPS && (uint32_t)C_LEN(ctl) > a.ksd && dep < a.ksd;
+            const bool tn = HSA_SEARCH_TRIE && !GAPS && (uint32_t)C_LEN(ctl) > a.ksd && dep < a.ksd;
             if (em == 0 && (M_ST(m) == ST_M || (R_MODE & MODE_GAPE) || M_GE(m) == R_MAXGE)) {
                 if (tn) {
                     // bwt_match_exact from a trie node: the read's next bases down to the
