@@ -202,6 +202,9 @@ template <typename IT> struct Ent {
 #ifndef HSA_SEARCH_TRIE
 #define HSA_SEARCH_TRIE 0
 #endif
+#ifndef HSA_WAVES_SIMD
+#define HSA_WAVES_SIMD 4      // k_search's launch bound: waves per SIMD its VGPRs must allow
+#endif
 #ifndef HSA_POOL_CHUNK
 #define HSA_POOL_CHUNK 1
 #endif
@@ -599,7 +602,7 @@ static __global__ void __launch_bounds__(BLOCK) k_split_finalize(SearchArgs a)
 // links and popped slots reused through a free list, so a lane's pool holds any
 // stack the reference can build (n_entries <= max_entries + 9, bwtgap.c:150-151).
 template <int MW, bool GAPS, typename WT, int NT, bool HUGE = false, typename IT = uint32_t>
-__global__ void __launch_bounds__(NT, 4) k_search(SearchArgs a)
+__global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
 {
     using F = WFmt<WT>;
     using E = Ent<IT>;
@@ -1516,7 +1519,7 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
         P.off_ws = P.off_wb + wbw * nt * 4u;
         P.lds = ((size_t)P.off_ws + (size_t)wsw * nt * 4u + 15) / 16 * 16;
         int per_cu = (int)((160u * 1024u) / P.lds);
-        const int cap = 16 / (int)(nt / 64);                 // 16 waves per CU
+        const int cap = 4 * HSA_WAVES_SIMD / (int)(nt / 64);  // 16 waves per CU
         const int want = g_waves_per_cu / (int)(nt / 64);
         if (per_cu > cap) per_cu = cap;
         if (per_cu > want) per_cu = want > 0 ? want : 1;
