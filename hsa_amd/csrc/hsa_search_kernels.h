@@ -127,6 +127,12 @@ struct SearchArgs {
     uint32_t ktd;                  // width trie levels
     uint32_t ksd;                  // search trie levels k_search uses (0: none)
     uint32_t kjm;                  // characters an exact tail jumps per trie load
+    // cost order (main pass of a batch larger than the chip): k_widths writes each row's
+    // final bid (wkey), k_order_* sort the list positions by it, most differences first,
+    // and k_search takes its reads in that order (perm), so the costly searches do not
+    // start last and set the launch's tail
+    uint8_t *wkey;
+    const int32_t *perm;
 };
 
 // The kernel's arguments re-read from the kernarg segment where a rare path uses them
@@ -482,6 +488,7 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
     }
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     if (st_t) atomicAdd(&a.ctr[10], (unsigned long long)st_t);
+    if (a.wkey) a.wkey[R] = (uint8_t)(f.bid < 255u ? f.bid : 255u);
 #ifdef HSA_DIAG
     atomicAdd(&g_dctr[18], (unsigned long long)du);
     atomicAdd(&g_dctr[19], (unsigned long long)dw);
@@ -549,6 +556,49 @@ static __global__ void __launch_bounds__(BLOCK) k_widths_export(SearchArgs a)
     }
 }
 
+
+// Cost order of a batch's reads (see SearchArgs::wkey): the lower bid of a read's two
+// strands -- a lower bound on the differences of its best strand (bwtaln.c:84-97) --
+// bucketed into 16 bins, most differences first; order within a bin is arbitrary (every
+// read's result is independent of when it is searched).
+__device__ __forceinline__ uint32_t order_bin(const SearchArgs &a, uint32_t q)
+{
+    const uint32_t k0 = a.wkey[2 * q], k1 = a.wkey[2 * q + 1];
+    const uint32_t k = k0 < k1 ? k0 : k1;
+    return 15u - (k < 15u ? k : 15u);
+}
+
+static __global__ void __launch_bounds__(BLOCK) k_order_hist(SearchArgs a, uint32_t *hist)
+{
+    __shared__ uint32_t h[16];
+    if (threadIdx.x < 16) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
+    if (q < (uint32_t)a.n_jobs) atomicAdd(&h[order_bin(a, q)], 1u);
+    __syncthreads();
+    if (threadIdx.x < 16 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// hist[16] -> exclusive offsets in hist[16..31] (one thread)
+static __global__ void k_order_scan(uint32_t *hist)
+{
+    uint32_t s = 0;
+    for (int b = 0; b < 16; ++b) { hist[16 + b] = s; s += hist[b]; }
+}
+
+static __global__ void __launch_bounds__(BLOCK) k_order_scatter(SearchArgs a, uint32_t *hist, int32_t *perm)
+{
+    __shared__ uint32_t h[16], base[16];
+    if (threadIdx.x < 16) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t b = 0, r = 0;
+    if (q < (uint32_t)a.n_jobs) { b = order_bin(a, q); r = atomicAdd(&h[b], 1u); }
+    __syncthreads();
+    if (threadIdx.x < 16 && h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&hist[16 + threadIdx.x], h[threadIdx.x]);
+    __syncthreads();
+    if (q < (uint32_t)a.n_jobs) perm[base[b] + r] = (int32_t)q;
+}
 
 // Strand-split mode, after k_search: per read, the rc strand's result if it has a hit,
 // else the fwd strand's (bwtaln.c:343-359), else the splice fallback; the fwd search and
@@ -1009,6 +1059,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                     if (j < (unsigned long long)n_jobs << (r->split ? 1 : 0)) {
                         const uint32_t item = (uint32_t)j;
                         qpos = r->split ? item >> 1 : item;
+                        if (r->perm) qpos = (uint32_t)r->perm[qpos];
                         const int job = r->job_list ? r->job_list[qpos] : (int)qpos;
                         const hsa_job_t J = r->jobs[job];
                         opt_max_diff = J.max_diff;
@@ -1692,6 +1743,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     const int mode = tm ? atoi(tm) : 1;
     A.ksd = tr && mode ? ix->trie_sdepth : 0u;
     A.kjm = mode == 2 ? 1u : HSA_TRIE_MAX_DEPTH;
+    A.wkey = nullptr; A.perm = nullptr;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg)) : nullptr;
@@ -1735,7 +1787,8 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
     const uint32_t rg = (uint32_t)max_len + 1u;
     const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
     const size_t row_bytes = rb + rs + sizeof(IT) * (size_t)rg + (mg ? 4 * (size_t)rg : 0);   // + full bids (caller widths)
-    if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * row_bytes + 4 * (size_t)n + 256))) return rc;
+    // + wq (4 n), cost keys (2 n), order (4 n) and its 32 counters
+    if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * row_bytes + 10 * (size_t)n + 1024))) return rc;
     if (mg) {
         if constexpr (sizeof(IT) != 4) {
             hsa_set_error("caller-width searches (bwt_match_gap) take 32-bit indexes");
@@ -1772,11 +1825,33 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
         A.sp_p = (uint32_t *)(d + 2 * al);
     }
     if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
+    // cost order: the main pass of a batch with more reads than the chip has lanes
+    // (HSA_ORDER=0/1 forbids / forces it)
+    const char *oe = getenv("HSA_ORDER");
+    const bool order = !split && !n_dev && qctr == 0 && n > 0 &&
+                       (oe ? atoi(oe) != 0 : (size_t)n > P.resident);
+    uint32_t *d_oh = nullptr;
+    if (order) {
+        char *tail = (char *)A.wq + 4 * (size_t)n;
+        A.wkey = (uint8_t *)tail;
+        const size_t ko = (2 * (size_t)n + 15) / 16 * 16;
+        d_oh = (uint32_t *)(tail + ko);
+        HSA_HIP(hipMemsetAsync(d_oh, 0, 32 * 4, st));
+    }
     size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
     if (wblocks < 1) wblocks = 1;
     if (P.wide) hipLaunchKernelGGL((k_widths<uint16_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
     else hipLaunchKernelGGL((k_widths<uint8_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
     HSA_HIP(hipGetLastError());
+    if (order) {
+        int32_t *d_perm = (int32_t *)(d_oh + 32);
+        const unsigned nb = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
+        hipLaunchKernelGGL(k_order_hist, dim3(nb), dim3(BLOCK), 0, st, A, d_oh);
+        hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(1), 0, st, d_oh);
+        hipLaunchKernelGGL(k_order_scatter, dim3(nb), dim3(BLOCK), 0, st, A, d_oh, d_perm);
+        HSA_HIP(hipGetLastError());
+        A.perm = d_perm;
+    }
     if (ix->ev_split && qctr == 0) HSA_HIP(hipEventRecord(ix->ev_split, st));   // the main pass only
     if (P.wide) launch_search<uint16_t, IT>(P, A, st);
     else launch_search<uint8_t, IT>(P, A, st);

@@ -111,6 +111,32 @@ def test_search_matches_reference_one_lane_per_read(name, monkeypatch):
     _compare(name)
 
 
+@pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "tiny_mm100_n4o0", "rep_gap60_default", "tiny_edge_default",
+                                  "tiny_gap100_n4o1_b400"])
+def test_search_matches_reference_cost_order(name, monkeypatch):
+    """Batches larger than the chip take their reads in cost order (k_order_*: the lower
+    strand bid first-highest), a permutation of the list positions k_search pulls; forced
+    here on the golden cases (one read per lane, no strand split)."""
+    monkeypatch.setenv("HSA_ORDER", "1")
+    monkeypatch.setenv("HSA_SPLIT", "0")
+    _compare(name)
+
+
+@pytest.mark.parametrize("case", ["tiny_mm100_n4o0", "tiny_gap100_n4o1"])
+def test_rank_queries_match_oracle_cost_order(case, monkeypatch):
+    """The device path in cost order: the same per-read hits and the oracle's rank-query
+    and pop counts."""
+    monkeypatch.setenv("HSA_ORDER", "1")
+    monkeypatch.setenv("HSA_SPLIT", "0")
+    got, (e_n, e_f, e_h, st) = _device_run(case)
+    assert np.array_equal(got["n"], e_n) and np.array_equal(got["f"] & 1, e_f & 1)
+    exp = split_hits(e_n, e_h)
+    bad = [i for i in range(len(exp)) if not np.array_equal(got["h"][got["o"][i]:got["o"][i] + max(got["n"][i], 0)],
+                                                             exp[i])]
+    assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
+    assert int(got["c"][2]) == int(st[0]) and int(got["c"][4]) == int(st[1])
+
+
 @pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "rep_mm100_n4o1"])
 def test_overflow_rerun_is_exact(name):
     """A tiny per-lane pool forces most reads through the large-capacity re-run."""
