@@ -454,11 +454,13 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
             raise RuntimeError(f"ref_probe_gpu: {j.stderr.decode()[-800:]}")
         t_gpu = float(j.stdout.decode().split()[-1])
         err = j.stderr.decode()
-        splice_s, n_fb = 0.0, 0
+        splice_s, n_fb, search_s, prefetch_s = 0.0, 0, 0.0, 0.0
         for ln in err.splitlines():
             if ln.startswith("[hsa] batch of"):
                 parts = ln.replace(",", "").split()
                 splice_s += float(parts[parts.index("path") + 1])
+                search_s += float(parts[parts.index("search") + 1])
+                prefetch_s += float(parts[parts.index("prefetch") + 1])
                 n_fb += int(ln.split("(")[-1].split()[0])
         # parity through the real entry point: rank 0's reads are a prefix of the first
         # 100 000-read batch in both runs, so their hits (splice path's included) agree
@@ -470,6 +472,7 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
         bad = [i for i in range(m) if g_n[i] != r_n[i] or not np.array_equal(g_h[go[i]:go[i + 1]], r_h[ro[i]:ro[i + 1]])]
         e2e = {"reads": e2e_reads, "reads_per_call": REF_BATCH, "value": round(e2e_reads / t_gpu, 1), "unit": "reads/s",
                "seconds": round(t_gpu, 3), "splice_fallback_reads": n_fb, "splice_path_s": round(splice_s, 3),
+               "main_search_s": round(search_s, 3), "splice_prefetch_s": round(prefetch_s, 3),
                "splice_path_us_per_fallback_read": round(1e6 * splice_s / n_fb, 1) if n_fb else None,
                "what": "the reference's driver (ref_probe.c) linked with every drop-in entry point of ours "
                        "(oracle/_ref/ref_probe_gpu, as HSA_gpu_all): bwa_cal_sa_reg_gap on bwa_seq_t batches from "
@@ -479,7 +482,8 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
                                        "fields": "n_aln and every bwt_aln1_t field of every hit, splice-path hits "
                                                  "included, hit order"}}
         log(f"[bench] drop-in end to end: {e2e['value']:.0f} reads/s ({e2e_reads} reads in calls of {REF_BATCH}, "
-            f"{n_fb} fallback reads, splice path {splice_s:.3f} s); {len(bad)} of {m} reads differ from the reference")
+            f"{n_fb} fallback reads; main search {search_s:.3f} s, splice prefetch {prefetch_s:.3f} s, splice path "
+            f"{splice_s:.3f} s); {len(bad)} of {m} reads differ from the reference")
         return {"reference": ref, "dropin_e2e": e2e}
     finally:
         shutil.rmtree(d, ignore_errors=True)

@@ -413,6 +413,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (ix->d_any) (void)hipFree(ix->d_any);
     if (ix->d_any_aux) (void)hipFree(ix->d_any_aux);
     if (ix->d_split) (void)hipFree(ix->d_split);
+    if (ix->d_fwd) (void)hipFree(ix->d_fwd);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
     (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
     (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m); (void)hipFree(ix->d_trie_w);

@@ -61,6 +61,7 @@ struct hsa_index {
     void *d_any = nullptr; size_t d_any_cap = 0;
     void *d_any_aux = nullptr; size_t d_any_aux_cap = 0;
     void *d_split = nullptr; size_t d_split_cap = 0;   // strand-split items' results (k_split_finalize)
+    void *d_fwd = nullptr; size_t d_fwd_cap = 0;       // lazy forward rows: count + reads for the forward pass
     // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;

@@ -133,6 +133,16 @@ struct SearchArgs {
     // start last and set the launch's tail
     uint8_t *wkey;
     const int32_t *perm;
+    // lazy forward rows (k_widths_reads): a read whose rc search found nothing and whose
+    // forward row was not computed goes to fwd_list (count *fwd_n); the forward pass
+    // (fwd_only) searches just that strand
+    int32_t *fwd_list;
+    unsigned long long *fwd_n;
+    uint32_t fwd_only;
+    // lazy main pass: rows in two planes, the rc row of list position q at row q and its
+    // forward row (when computed) at row rmap[q], so every width lane stores coalesced;
+    // null: row q * 2 + strand
+    int32_t *rmap;
 };
 
 // The kernel's arguments re-read from the kernarg segment where a rare path uses them
@@ -436,15 +446,15 @@ __device__ __forceinline__ void width_step(const SearchArgs &a, WChain<IT> &ch, 
     if (t == n) brow[(t / F::EPW) * 64] = ch.acc;
 }
 
-template <typename WT, typename IT = uint32_t>
-__global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
+// One width row: both chains (the whole strand sequence and its last seed_len bases) of
+// list position q's strand; returns the rank queries, 64-byte sectors and trie loads it
+// took, and the chain's final bid (width[len].bid = the bid of the last base + 1).
+struct WRow { uint32_t q, b, t, bid; };
+
+template <typename WT, typename IT>
+__device__ __forceinline__ WRow width_row(const SearchArgs &a, uint32_t R, uint32_t strand, const hsa_job_t &J)
 {
     using F = WFmt<WT>;
-    const uint32_t R = blockIdx.x * BLOCK + threadIdx.x;     // row = list position * 2 + strand
-    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
-    if (R >= 2u * n_jobs) return;
-    const uint32_t q = R >> 1, strand = R & 1u;
-    const hsa_job_t J = a.jobs[a.job_list ? a.job_list[q] : (int)q];
     const uint32_t len = J.len;
     const uint64_t off = J.off;
     const bool has_seed = (int)len > J.seed_len;
@@ -455,19 +465,12 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
     IT *const wrow = reinterpret_cast<IT *>(a.wg) + rb * a.rg * 64 + rl;
     WChain<IT> f{0, Ix<IT>::T(a), 0, 0, 0, 0, 0}, sd{0, Ix<IT>::T(a), 0, 0, 0, 0, 0};
     uint32_t st_q = 0, st_b = 0, st_t = 0;
-#ifdef HSA_DIAG
-    uint32_t du = 0, dw = 0;
-#endif
     const uint32_t s0 = len - slen;
     auto base = [&](uint32_t sp) -> uint32_t {
         const uint32_t c = a.codes[off + (strand ? len - 1u - sp : sp)];
         return strand && c < 4 ? 3u - c : c;
     };
     for (uint32_t t = 0; t <= len; ++t) {
-#ifdef HSA_DIAG
-        if (t < len) { ++dw; du += f.k == f.l; }
-        if (has_seed && t < slen) { ++dw; du += sd.k == sd.l; }
-#endif
         const uint32_t cf = t < len ? base(t) : 4u;
         // the read's elements also carry the strand sequence's base (k_search's getc)
         width_step<WT, IT>(a, f, t, len, cf, t < len ? F::code_bits(cf) : 0u, brow, wrow, st_q, st_b, st_t);
@@ -476,23 +479,92 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
             width_step<WT, IT>(a, sd, t, slen, cs, 0u, srow, nullptr, st_q, st_b, st_t);
         }
     }
-    // rank queries: the reverse-complement strand is always searched (bwtaln.c:343);
-    // the forward strand's widths are computed speculatively and count as the
-    // reference's work only when k_search searches that strand (ctr[13]: all of them)
-    if (strand) {
-        atomicAdd(&a.ctr[2], (unsigned long long)st_q);
-        atomicAdd(&a.ctr[7], (unsigned long long)st_q);
-    } else {
-        a.wq[q] = st_q;
-        atomicAdd(&a.ctr[13], (unsigned long long)st_q);
+    return WRow{st_q, st_b, st_t, f.bid};
+}
+
+// one atomic per wave and counter (the kernels' lanes all reach it)
+__device__ __forceinline__ void wave_add(unsigned long long *c, unsigned long long v)
+{
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(c, v);
+}
+
+#define HSA_NOFWD 0xFFFFFFFFu        // wq: this read's forward row was not computed
+#define HSA_F_NEEDFWD 0x100u         // k_search internal: rc had no hit, forward row missing
+
+// One lane per row (rows in order): row = list position * 2 + strand.  The forward
+// strand's rows are computed speculatively and count as the reference's work only
+// when k_search searches that strand (ctr[13]: all of them).
+template <typename WT, typename IT = uint32_t>
+__global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
+{
+    const uint32_t R = blockIdx.x * BLOCK + threadIdx.x;     // row = list position * 2 + strand
+    const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    const uint32_t q = R >> 1, strand = R & 1u;
+    WRow w{0, 0, 0, 0};
+    if (R < 2u * n_jobs) {
+        const hsa_job_t J = a.jobs[a.job_list ? a.job_list[q] : (int)q];
+        w = width_row<WT, IT>(a, R, strand, J);
+        if (!strand) a.wq[q] = w.q;
+        if (a.wkey) a.wkey[R] = (uint8_t)(w.bid < 255u ? w.bid : 255u);
     }
-    atomicAdd(&a.ctr[3], (unsigned long long)st_b);
-    if (st_t) atomicAdd(&a.ctr[10], (unsigned long long)st_t);
-    if (a.wkey) a.wkey[R] = (uint8_t)(f.bid < 255u ? f.bid : 255u);
-#ifdef HSA_DIAG
-    atomicAdd(&g_dctr[18], (unsigned long long)du);
-    atomicAdd(&g_dctr[19], (unsigned long long)dw);
-#endif
+    // rank queries: the reverse-complement strand is always searched (bwtaln.c:343)
+    wave_add(&a.ctr[2], strand ? w.q : 0u);
+    wave_add(&a.ctr[7], strand ? w.q : 0u);
+    wave_add(&a.ctr[13], strand ? 0u : w.q);
+    wave_add(&a.ctr[3], w.b);
+    wave_add(&a.ctr[10], w.t);
+}
+
+// One lane per read, one strand's row each.
+// mode 1 (main pass of a large batch): the rc row of every read; a read whose rc search
+//   cannot have a hit -- its root is pruned when the last base's bid exceeds max_diff
+//   (bwtgap.c:170) -- goes to list2 for its forward row; the others get wq = HSA_NOFWD
+//   and k_search hands them to the forward pass if rc finds nothing (bwtaln.c:343-359).
+// mode 3: the forward rows of list2 (the speculative count, as k_widths').
+// mode 2 (the forward pass): the forward rows of the reads k_search listed, the
+//   reference's work.
+template <typename WT, typename IT = uint32_t>
+__global__ void __launch_bounds__(BLOCK) k_widths_reads(SearchArgs a, uint32_t mode, int32_t *list2,
+                                                        unsigned long long *n2)
+{
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t n_jobs = mode == 3 ? (uint32_t)*n2 : a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
+    WRow w{0, 0, 0, 0};
+    bool more = false;
+    if (p < n_jobs) {
+        const uint32_t q = mode == 3 ? (uint32_t)list2[p] : p;
+        const hsa_job_t J = a.jobs[a.job_list ? a.job_list[q] : (int)q];
+        // mode 1: the rc plane (row q); mode 3: the forward plane after it (row n_al + p);
+        // mode 2 (forward pass, no plane map): row 2 p
+        const uint32_t R = mode == 1 ? q : mode == 3 ? (uint32_t)(((uint32_t)a.n_jobs + 63u) & ~63u) + p : 2u * q;
+        w = width_row<WT, IT>(a, R, mode == 1 ? 1u : 0u, J);
+        if (mode == 3) a.rmap[q] = (int32_t)R;
+        const uint8_t key = (uint8_t)(w.bid < 255u ? w.bid : 255u);
+        if (mode == 1) {
+            more = (int)w.bid - 1 > J.max_diff;
+            a.wq[q] = HSA_NOFWD;
+            if (a.wkey) { a.wkey[2 * q + 1] = key; a.wkey[2 * q] = 255u; }
+        } else if (mode == 3) {
+            a.wq[q] = w.q;
+            if (a.wkey) a.wkey[2 * q] = key;
+        }
+    }
+    if (mode == 1) {                                    // list2: one atomic per wave
+        const uint64_t m = __ballot(more);
+        const int lane = (int)(threadIdx.x & 63);
+        unsigned long long b = 0;
+        if (m && lane == __ffsll((unsigned long long)m) - 1) b = atomicAdd(n2, (unsigned long long)__popcll(m));
+        b = __shfl(b, __ffsll((unsigned long long)(m ? m : 1ull)) - 1);
+        if (more) list2[b + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
+    }
+    const uint32_t rq = mode == 1 ? w.q : 0u, fq = mode == 2 ? w.q : 0u, sq = mode == 3 ? w.q : 0u;
+    wave_add(&a.ctr[2], rq + fq);
+    wave_add(&a.ctr[7], rq + fq);
+    wave_add(&a.ctr[13], fq + sq);
+    wave_add(&a.ctr[14], fq);
+    wave_add(&a.ctr[3], w.b);
+    wave_add(&a.ctr[10], w.t);
 }
 
 // Caller-width mode: the width rows of each call from the caller's bwt_width_t pairs
@@ -813,7 +885,8 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     };
     // width row of the current strand: row qpos * 2 + strand, 64 rows interleaved
     auto row_base = [&](uint32_t cap_words) -> size_t {
-        const uint32_t r = qpos * 2u + C_STRAND(ctl);
+        const int32_t *const rm = cold_args()->rmap;
+        const uint32_t r = rm ? (C_STRAND(ctl) ? qpos : (uint32_t)rm[qpos]) : qpos * 2u + C_STRAND(ctl);
         return (size_t)(r >> 6) * cap_words * 64 + (r & 63u);
     };
     // copy the strand's pruning elements (k_widths) into the lane's LDS columns, then
@@ -883,6 +956,11 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             return;
         }
         const int job = r->job_list ? r->job_list[qpos] : (int)qpos;
+        if (fl & HSA_F_NEEDFWD) {                 // the forward pass writes its outputs
+            r->fwd_list[atomicAdd(r->fwd_n, 1ull)] = job;
+            SET_PH(ctl, PH_IDLE);
+            return;
+        }
         if (fl & HSA_F_OVERFLOW) {
             if (r->ovf_list) r->ovf_list[atomicAdd(&r->ctr[r->ovf_ctr], 1ull)] = job;   // re-run by the next pass
             else atomicAdd(&r->ctr[11], 1ull);                                  // the last pass: stays unfinished
@@ -934,9 +1012,14 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         } else if (cold_args()->mg || cold_args()->split) {
             finish_job(0, 0, 0);        // one call (or one split item), one strand
         } else if (C_STRAND(ctl)) {
-            ctl &= ~(1u << 3);          // strand 0
-            st_wq += cold_args()->wq[qpos];   // its widths are the reference's work now (bwtaln.c:344-348)
-            start_strand();
+            const uint32_t wq = cold_args()->wq[qpos];
+            if (wq == HSA_NOFWD) {
+                finish_job(HSA_F_NEEDFWD, 0, 0);   // its forward row is computed by the forward pass
+            } else {
+                ctl &= ~(1u << 3);          // strand 0
+                st_wq += wq;                // its widths are the reference's work now (bwtaln.c:344-348)
+                start_strand();
+            }
         } else {
             finish_job(HSA_F_FALLBACK, 0, 0);
         }
@@ -1076,7 +1159,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                             const uint32_t has_seed = (int)len > J.seed_len;
                             ctl = 8u | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 | len << 10 |
                                   (has_seed ? (uint32_t)J.seed_len : 0u) << 20;     // strand 1 (rc first, bwtaln.c:343)
-                            if (r->split && (item & 1u)) ctl &= ~8u;              // split: odd items search fwd
+                            if ((r->split && (item & 1u)) || r->fwd_only) ctl &= ~8u;   // split: odd items search fwd
                             sq0 = st_q; sp0 = st_p;
                         }
                         const hsa_regime_t *R = s_reg + (J.regime & 1);
@@ -1706,7 +1789,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     const uint32_t esz = P.wide ? 2u : 1u;
     const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;
     const uint32_t rg = (uint32_t)max_len + 1u;
-    const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
+    const size_t rows = ((size_t)n + 63) / 64 * 64 * 2;     // two 64-row-aligned planes (lazy widths)
     uint8_t *wr = (uint8_t *)ix->d_wrows;
     SearchArgs A;
     A.fwd = RankDir{ix->blk[0], ix->isa0};
@@ -1744,6 +1827,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.ksd = tr && mode ? ix->trie_sdepth : 0u;
     A.kjm = mode == 2 ? 1u : HSA_TRIE_MAX_DEPTH;
     A.wkey = nullptr; A.perm = nullptr;
+    A.fwd_list = nullptr; A.fwd_n = nullptr; A.fwd_only = 0; A.rmap = nullptr;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg)) : nullptr;
@@ -1785,7 +1869,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
     const uint32_t esz = P.wide ? 2u : 1u;
     const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;
     const uint32_t rg = (uint32_t)max_len + 1u;
-    const size_t rows = ((size_t)n * 2 + 63) / 64 * 64;
+    const size_t rows = ((size_t)n + 63) / 64 * 64 * 2;     // two 64-row-aligned planes (lazy widths)
     const size_t row_bytes = rb + rs + sizeof(IT) * (size_t)rg + (mg ? 4 * (size_t)rg : 0);   // + full bids (caller widths)
     // + wq (4 n), cost keys (2 n), order (4 n) and its 32 counters
     if ((rc = hsa_grow(&ix->d_wrows, &ix->d_wrows_cap, rows * row_bytes + 10 * (size_t)n + 1024))) return rc;
@@ -1838,10 +1922,43 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
         d_oh = (uint32_t *)(tail + ko);
         HSA_HIP(hipMemsetAsync(d_oh, 0, 32 * 4, st));
     }
-    size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
-    if (wblocks < 1) wblocks = 1;
-    if (P.wide) hipLaunchKernelGGL((k_widths<uint16_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
-    else hipLaunchKernelGGL((k_widths<uint8_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
+    // lazy forward rows: the main pass of a batch searched one read per lane computes a
+    // read's forward row only when its rc search cannot hit; the reads whose rc search
+    // finds nothing without one get it in the forward pass below.  It pays for long reads
+    // (config 5's 250 bp: k_widths 17.0 -> 15.7 ms); for 100 bp reads the second width
+    // launch costs more than the rows it saves (5.25 -> 5.68 ms), so by default reads of
+    // 200 bases or more (HSA_LAZY=0 / 1 forbids / forces it)
+    const char *le = getenv("HSA_LAZY");
+    const bool lazy = !split && !n_dev && qctr == 0 && n > 0 && (le ? atoi(le) != 0 : max_len >= 200);
+    unsigned long long *d_fwd_n = nullptr;
+    int32_t *d_list2 = nullptr;
+    unsigned long long *d_n2 = nullptr;
+    if (lazy) {
+        // [count, count2 | forward-pass list (n) | list2 (n)]
+        if ((rc = hsa_grow(&ix->d_fwd, &ix->d_fwd_cap, 512 + 12 * (size_t)n))) return rc;
+        d_fwd_n = (unsigned long long *)ix->d_fwd;
+        d_n2 = d_fwd_n + 1;
+        HSA_HIP(hipMemsetAsync(d_fwd_n, 0, 16, st));
+        A.fwd_n = d_fwd_n;
+        A.fwd_list = (int32_t *)((char *)ix->d_fwd + 128);
+        d_list2 = A.fwd_list + ((size_t)n + 31) / 32 * 32;
+        A.rmap = d_list2 + ((size_t)n + 31) / 32 * 32;
+    }
+    if (lazy) {
+        const unsigned rblocks = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
+        if (P.wide) {
+            hipLaunchKernelGGL((k_widths_reads<uint16_t, IT>), dim3(rblocks), dim3(BLOCK), 0, st, A, 1u, d_list2, d_n2);
+            hipLaunchKernelGGL((k_widths_reads<uint16_t, IT>), dim3(rblocks), dim3(BLOCK), 0, st, A, 3u, d_list2, d_n2);
+        } else {
+            hipLaunchKernelGGL((k_widths_reads<uint8_t, IT>), dim3(rblocks), dim3(BLOCK), 0, st, A, 1u, d_list2, d_n2);
+            hipLaunchKernelGGL((k_widths_reads<uint8_t, IT>), dim3(rblocks), dim3(BLOCK), 0, st, A, 3u, d_list2, d_n2);
+        }
+    } else {
+        size_t wblocks = ((size_t)n * 2 + BLOCK - 1) / BLOCK;
+        if (wblocks < 1) wblocks = 1;
+        if (P.wide) hipLaunchKernelGGL((k_widths<uint16_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
+        else hipLaunchKernelGGL((k_widths<uint8_t, IT>), dim3((unsigned)wblocks), dim3(BLOCK), 0, st, A);
+    }
     HSA_HIP(hipGetLastError());
     if (order) {
         int32_t *d_perm = (int32_t *)(d_oh + 32);
@@ -1856,6 +1973,21 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
     if (P.wide) launch_search<uint16_t, IT>(P, A, st);
     else launch_search<uint8_t, IT>(P, A, st);
     HSA_HIP(hipGetLastError());
+    if (lazy) {
+        // the forward pass: the forward rows and the forward-strand searches of the reads
+        // the main pass listed (count on the device; queue head ctr[6]); its overflows go
+        // to the same re-run list as the main pass's
+        SearchArgs F = A;
+        F.job_list = A.fwd_list; F.n_dev = d_fwd_n; F.qctr = 6; F.fwd_only = 1;
+        F.fwd_list = nullptr; F.fwd_n = nullptr; F.wkey = nullptr; F.perm = nullptr; F.rmap = nullptr;
+        const unsigned rblocks = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
+        if (P.wide) hipLaunchKernelGGL((k_widths_reads<uint16_t, IT>), dim3(rblocks), dim3(BLOCK), 0, st, F, 2u, d_list2, d_n2);
+        else hipLaunchKernelGGL((k_widths_reads<uint8_t, IT>), dim3(rblocks), dim3(BLOCK), 0, st, F, 2u, d_list2, d_n2);
+        HSA_HIP(hipGetLastError());
+        if (P.wide) launch_search<uint16_t, IT>(P, F, st);
+        else launch_search<uint8_t, IT>(P, F, st);
+        HSA_HIP(hipGetLastError());
+    }
     if (split) {
         const unsigned nb = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
         hipLaunchKernelGGL(k_split_finalize, dim3(nb), dim3(BLOCK), 0, st, A);

@@ -137,6 +137,32 @@ def test_rank_queries_match_oracle_cost_order(case, monkeypatch):
     assert int(got["c"][2]) == int(st[0]) and int(got["c"][4]) == int(st[1])
 
 
+@pytest.mark.parametrize("lazy", ["0", "1"])
+@pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "tiny_mm100_n4o0", "rep_gap60_default", "tiny_opts_seed"])
+def test_search_matches_reference_lazy_forward_rows(name, lazy, monkeypatch):
+    """The main pass of a batch searched one read per lane computes a read's forward
+    width row only when its rc search cannot hit (the root is pruned: last bid >
+    max_diff); the reads whose rc search finds nothing without one go through the
+    forward pass (k_widths_reads mode 2 + a fwd-only k_search).  HSA_LAZY=0: every row
+    up front."""
+    monkeypatch.setenv("HSA_LAZY", lazy)
+    monkeypatch.setenv("HSA_SPLIT", "0")
+    _compare(name)
+
+
+@pytest.mark.parametrize("lazy", ["0", "1"])
+@pytest.mark.parametrize("case", ["tiny_mm100_n4o0", "tiny_gap100_n4o1", "rep_mm100_n4o1"])
+def test_rank_queries_match_oracle_lazy_forward_rows(case, lazy, monkeypatch):
+    """Lazy forward rows keep the reference's rank-query and pop counts: a forward row
+    counts when the forward strand is searched, in either pass."""
+    monkeypatch.setenv("HSA_LAZY", lazy)
+    monkeypatch.setenv("HSA_SPLIT", "0")
+    got, (e_n, e_f, e_h, st) = _device_run(case)
+    assert np.array_equal(got["n"], e_n) and np.array_equal(got["f"] & 1, e_f & 1)
+    assert int(got["c"][2]) == int(st[0]) and int(got["c"][4]) == int(st[1])
+    assert got["c"][13] >= got["c"][14]
+
+
 @pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "rep_mm100_n4o1"])
 def test_overflow_rerun_is_exact(name):
     """A tiny per-lane pool forces most reads through the large-capacity re-run."""
