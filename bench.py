@@ -161,7 +161,7 @@ def host_oracle_index(res, T):
 # kernel-trace summaries next to them (tools/trace_summary.py) give the same runs'
 # per-launch durations
 TRAFFIC_SRCS = {2: "profiles/r03_pmc_summary_config2.json", 3: "profiles/r03_pmc_summary_config3.json",
-                4: "profiles/r03_pmc_summary_config4.json", 5: "profiles/r02_pmc_summary_config5.json"}
+                4: "profiles/r03_pmc_summary_config4.json", 5: "profiles/r03_pmc_summary_config5.json"}
 
 
 def traffic_per_kernel(config):
@@ -775,7 +775,7 @@ def main():
                                       "frac_of_random_sector": round(ach_widths / rand_gbs, 4),
                                       "rank_queries_per_read": round(q_widths / reads_local, 1),
                                       "issued_queries_per_read": round(q_widths_issued / reads_local, 1),
-                                      "traffic": pk.get("k_widths")},
+                                      "traffic": (pk.get("k_widths", 0) + pk.get("k_widths_reads", 0)) or None},
                          "step": {"ms": round(mean_kms, 3), "achieved": round(ach_step, 1),
                                   "frac": round(ach_step / HBM_PEAK_GBS, 4),
                                   "frac_of_random_sector": round(ach_step / rand_gbs, 4)},

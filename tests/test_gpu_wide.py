@@ -358,17 +358,24 @@ def test_search_past_2_32_matches_oracle(big_index):
     assert (e_n > 0).mean() > 0.9
 
 
-def test_config5_kernel_past_2_32_matches_oracle(big_index, monkeypatch, capfd):
+@pytest.mark.parametrize("one_lane", [False, True])
+def test_config5_kernel_past_2_32_matches_oracle(big_index, monkeypatch, capfd, one_lane):
     """Config 5's own kernel instantiation: 250 bp reads, -n 4 -o 0, 64-bit intervals
     AND 4-bit pruning rows (the planner picks them by itself for long ungapped reads,
     as in the config-5 bench).  2 000 reads from the whole 4.3 Gbp text with 0-4
     substitutions, half reverse-complemented (make_reads), 1 in 50 with an N; every
     hsa_aln64_t field of every hit, the splice-fallback flags and the rank-query and pop
-    counts equal the 64-bit restatement's, and hits with SA bounds past 2^32 occur."""
+    counts equal the 64-bit restatement's, and hits with SA bounds past 2^32 occur.
+    one_lane: the main pass of a large batch -- one read per lane, the lazy forward
+    rows and their forward pass, the cost order -- forced on this small one."""
     from hsa_amd import synth
     from oracle_ctypes import default_opt
     monkeypatch.setenv("HSA_VERBOSE", "1")
     monkeypatch.delenv("HSA_WFMT", raising=False)
+    if one_lane:
+        monkeypatch.setenv("HSA_SPLIT", "0")
+        monkeypatch.setenv("HSA_LAZY", "1")
+        monkeypatch.setenv("HSA_ORDER", "1")
     gi, ox, genome = big_index
     reads, _ = synth.make_reads(genome, [(0, BIG_T)], 2000, 250, 8 * 1_000_000 + 77, max_mm=4)
     reads = reads.copy()

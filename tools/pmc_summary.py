@@ -25,7 +25,7 @@ import statistics
 import sys
 
 
-STEP_KERNELS = ("k_widths", "k_search", "k_seed_prep", "k_widths_import", "k_widths_export")
+STEP_KERNELS = ("k_widths", "k_widths_reads", "k_search", "k_seed_prep", "k_widths_import", "k_widths_export")
 
 
 def counters(d, kernel, every=False):
@@ -76,21 +76,23 @@ def main():
     launches = len(args) > 2 and args[2] == "step"
     if launches:
         out["per_kernel"] = {}
+        # steps: the full-size launches (>= half the longest) of the longest-running
+        # k_search instantiation, the step's main pass; every kernel's dispatches (overflow
+        # re-runs, the lazy widths' two launches, the forward pass) are summed over them
+        f0, dur0, names0 = counters(os.path.join(src, "pmc_fetch"), "k_search", every=True)
+        main = max(set(names0.values()), key=lambda nm: sum(dur0[d] for d in names0 if names0[d] == nm))
+        ds0 = [d for d in names0 if names0[d] == main]
+        top0 = max(dur0[d] for d in ds0)
+        nsteps = sum(1 for d in ds0 if dur0[d] >= 0.5 * top0)
+        out["steps"] = nsteps
         for k in STEP_KERNELS:
             f, dur, names = counters(os.path.join(src, "pmc_fetch"), k, every=True)
             w, _, _ = counters(os.path.join(src, "pmc_write"), k, every=True)
             if not f:
                 continue
-            # per instantiation: all its dispatches (incl. overflow re-runs) over its
-            # full-size launches (>= half its longest dispatch)
-            fb = wb = ms = 0.0
-            for nm in set(names.values()):
-                ds = [d for d in names if names[d] == nm]
-                top = max(dur[d] for d in ds)
-                nl = sum(1 for d in ds if dur[d] >= 0.5 * top)
-                fb += sum(f[d]["FETCH_SIZE"] for d in ds) * 1024 / cal / nl
-                wb += sum(w[d]["WRITE_SIZE"] for d in ds if d in w) * 1024 / nl
-                ms += sum(dur[d] for d in ds) / nl
+            fb = sum(v["FETCH_SIZE"] for v in f.values()) * 1024 / cal / nsteps
+            wb = sum(v["WRITE_SIZE"] for v in w.values()) * 1024 / nsteps
+            ms = sum(dur.values()) / nsteps
             out["per_kernel"][k] = {"fetch_bytes": fb, "write_bytes": wb, "ms_per_step_pmc_pass": ms}
     else:
         # one step = k_widths + k_search launches: per-kernel medians, summed
