@@ -454,6 +454,9 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
             raise RuntimeError(f"ref_probe_gpu: {j.stderr.decode()[-800:]}")
         t_gpu = float(j.stdout.decode().split()[-1])
         err = j.stderr.decode()
+        if os.environ.get("HSA_E2E_LOG"):                  # the drop-in's stage timings, whole
+            with open(os.environ["HSA_E2E_LOG"], "w") as f:
+                f.write(err)
         splice_s, n_fb, search_s, prefetch_s = 0.0, 0, 0.0, 0.0
         for ln in err.splitlines():
             if ln.startswith("[hsa] batch of"):

@@ -145,6 +145,48 @@ static void read_infos(const uint8_t *codes, const uint64_t *offs, const uint32_
     for (int k = 1; k < nt; ++k) if (started[k]) pthread_join(th[k], NULL);
 }
 
+/* The per-read outputs of the reads the search settled (bwtaln.c:314-373): a read's own
+ * calloc'd aln array (capacity >= 10, as bwt_match_gap's) with its hits, the fields
+ * cleared; reads [r0, r1), a host thread's share. */
+typedef struct {
+    bwa_seq_t *seqs; const int32_t *n_aln; const uint32_t *flags; const uint64_t *hoff; const uint32_t *hits;
+    int r0, r1;
+} out_part_t;
+
+static void *out_run(void *arg)
+{
+    const out_part_t *o = (const out_part_t *)arg;
+    for (int i = o->r0; i < o->r1; ++i) {
+        bwa_seq_t *p = o->seqs + i;
+        if (o->flags[i] & HSA_RF_NFILTER) continue;             /* untouched (:314-317) */
+        p->sa = 0; p->type = 0; p->c1 = p->c2 = 0; p->n_aln = 0; p->aln = 0;
+        if ((o->flags[i] & HSA_RF_POLYAT) || o->n_aln[i] <= 0) continue;
+        const int cap = o->n_aln[i] > 10 ? o->n_aln[i] : 10;    /* bwt_match_gap's calloc'd array */
+        p->aln = (bwt_aln1_t *)calloc(cap, sizeof(bwt_aln1_t));
+        memcpy(p->aln, o->hits + o->hoff[i] * 9, sizeof(bwt_aln1_t) * o->n_aln[i]);
+        p->n_aln = o->n_aln[i];
+    }
+    return NULL;
+}
+
+/* out_run over every read, on up to 8 host threads for large calls */
+static void write_outputs(bwa_seq_t *seqs, int n, const int32_t *n_aln, const uint32_t *flags, const uint64_t *hoff,
+                          const uint32_t *hits)
+{
+    enum { MAXT = 8 };
+    const int nt = n >= (1 << 14) ? MAXT : 1;
+    out_part_t part[MAXT];
+    pthread_t th[MAXT];
+    int started[MAXT] = {0};
+    for (int k = 0; k < nt; ++k) {
+        part[k] = (out_part_t){seqs, n_aln, flags, hoff, hits, (int)((long)n * k / nt), (int)((long)n * (k + 1) / nt)};
+        if (k > 0) started[k] = pthread_create(&th[k], NULL, out_run, &part[k]) == 0;
+        if (k > 0 && !started[k]) out_run(&part[k]);
+    }
+    out_run(&part[0]);
+    for (int k = 1; k < nt; ++k) if (started[k]) pthread_join(th[k], NULL);
+}
+
 /* One read of the bwtaln.c:303-337 prologue under regime `cur` (0 = A, 1 = B). */
 static int plan_read(const gap_opt_t *caller, int cur, optstate_t *st, const readinfo_t *ri, int len,
                      int32_t *max_diff, int32_t *seed_len)
@@ -671,18 +713,10 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
         sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)n_seqs + 1));
         sr_idx = (int *)malloc(sizeof(int) * ((size_t)n_seqs + 1));
     }
-    for (int i = 0; i < n_seqs; ++i) {
+    write_outputs(seqs, n_seqs, n_aln, flags, hoff, hits);
+    for (int i = 0; i < n_seqs; ++i) {                          /* the splice path's reads, in order */
         bwa_seq_t *p = seqs + i;
-        if (flags[i] & HSA_RF_NFILTER) continue;               /* untouched (:314-317) */
-        p->sa = 0; p->type = 0; p->c1 = p->c2 = 0; p->n_aln = 0; p->aln = 0;
-        if (flags[i] & HSA_RF_POLYAT) continue;
-        if (n_aln[i] > 0) {
-            int cap = n_aln[i] > 10 ? n_aln[i] : 10;           /* bwt_match_gap's calloc'd array */
-            p->aln = (bwt_aln1_t *)calloc(cap, sizeof(bwt_aln1_t));
-            memcpy(p->aln, hits + hoff[i] * 9, sizeof(bwt_aln1_t) * n_aln[i]);
-            p->n_aln = n_aln[i];
-            continue;
-        }
+        if ((flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) || n_aln[i] > 0) continue;
         if (!(flags[i] & HSA_F_FALLBACK) || !have_splice) continue;
         gap_opt_t lo = local;                                   /* aux->opt = &local_opt (:363) */
         lo.max_diff = sp[2 * i];
