@@ -78,31 +78,39 @@ def build_index(T, seed, device, with_files=False):
     _lib.check(L.hsa_synth_genome_device(device, T, seed, text.data_ptr()))
     res = {}
     extra = {}
+    sa = None
     for rev in (0, 1):
         bw = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
         isa0 = C.c_uint32()
         Cc = np.zeros(5, np.uint32)
         t0 = time.time()
-        if with_files and rev == 0:
+        if rev == 0:
+            # the forward BWT with its whole suffix array (the same sort): the walk's SA,
+            # and every SA_INTERVAL-th value for the reference's .sa
             i64 = C.c_uint64()
             C64 = np.zeros(5, np.uint64)
-            ns = (T + SA_INTERVAL) // SA_INTERVAL
-            sa = torch.zeros(ns, dtype=torch.int32, device="cuda")
+            sa = torch.zeros(T + 1, dtype=torch.int32, device="cuda")
             _lib.check(L.hsa_build_bwt_index_device(device, T, text.data_ptr(), bw.data_ptr(), C.byref(i64), C64,
-                                                    SA_INTERVAL, sa.data_ptr()))
+                                                    1, sa.data_ptr()))
             isa0.value = int(i64.value)
             Cc[:] = C64.astype(np.uint32)
-            extra["sa"] = sa.cpu().numpy().view(np.uint32)
-            del sa
+            if with_files:
+                extra["sa"] = sa[::SA_INTERVAL].cpu().numpy().view(np.uint32)
         else:
             _lib.check(L.hsa_build_bwt_device(device, T, text.data_ptr(), rev, bw.data_ptr(), C.byref(isa0), Cc))
         log(f"[bench] BWT{' (reverse)' if rev else ''} of {T} bp built on the device in {time.time() - t0:.1f} s")
         res[rev] = (bw, int(isa0.value), Cc)
     if with_files:
         extra["text"] = text[:nw].cpu().numpy().view(np.uint32)
-    del text
     gi = _lib.GpuIndex.from_device_codes(T, res[0][1], res[0][2], res[0][0].data_ptr(), T, res[1][1], res[1][2],
                                          res[1][0].data_ptr(), device=device)
+    if os.environ.get("HSA_WALK") == "1":                   # experiment builds only
+        t0 = time.time()
+        gi.build_walk(sa.data_ptr(), text.data_ptr())      # the unique-interval walk's SA, ISA, text
+        log(f"[bench] unique-interval walk arrays (SA, ISA, text: {(8 * (T + 1) + T // 4) / 2**30:.1f} GiB) "
+            f"in {time.time() - t0:.1f} s")
+    del text, sa
+    torch.cuda.empty_cache()
     return gi, res, extra
 
 

@@ -417,6 +417,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
     (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
     (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m); (void)hipFree(ix->d_trie_w);
+    (void)hipFree(ix->d_wsa); (void)hipFree(ix->d_wisa); (void)hipFree(ix->d_wtext);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
     if (ix->evm) (void)hipEventDestroy(ix->evm);

@@ -65,6 +65,8 @@ struct hsa_index {
     // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;
+    // the unique-interval walk (hsa_index_build_walk): full SA, its inverse, packed text
+    uint32_t *d_wsa = nullptr, *d_wisa = nullptr, *d_wtext = nullptr;
     uint64_t *d_ctr = nullptr;
     // root tries (hsa_trie.h): every string of up to trie_depth characters; built with
     // the index's interval width (trie_wide: 64-bit entries), 0 = none

@@ -59,7 +59,7 @@
 #define HSA_CTL_LOOP 0    // 1: loop the control code until every lane needs a rank step
 #endif
 
-enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END };
+enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END, PH_WALK, PH_WEXP };
 
 struct SearchArgs {
     RankDir fwd, rev;
@@ -143,6 +143,12 @@ struct SearchArgs {
     // forward row (when computed) at row rmap[q], so every width lane stores coalesced;
     // null: row q * 2 + strand
     int32_t *rmap;
+    // unique-interval walk (ungapped 32-bit searches, hsa_index_build_walk): the full
+    // suffix array, its inverse and the packed text; a node whose interval holds one
+    // suffix (k = l) and at least wmin positions still to match
+    const uint32_t *wsa, *wisa, *wtext;
+    uint32_t wmin;
+    uint32_t wstreak;              // ... reached by at least this many one-suffix match steps in a row
 };
 
 // The kernel's arguments re-read from the kernarg segment where a rare path uses them
@@ -220,6 +226,12 @@ template <typename IT> struct Ent {
 #endif
 #ifndef HSA_WAVES_SIMD
 #define HSA_WAVES_SIMD 4      // k_search's launch bound: waves per SIMD its VGPRs must allow
+#endif
+// The unique-interval walk (PH_WALK; hsa_index_build_walk): bit-exact, measured slower
+// than the rank steps it replaces, so compiled only into experiment builds
+// (tools/build_variant.sh walk -DHSA_UNIQUE_WALK=1).
+#ifndef HSA_UNIQUE_WALK
+#define HSA_UNIQUE_WALK 0
 #endif
 #ifndef HSA_POOL_CHUNK
 #define HSA_POOL_CHUNK 1
@@ -838,6 +850,12 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     // step needs, loaded in the control phase so that its latency overlaps the rank load
     const uint8_t *rowp = nullptr;
     uint32_t cur_c = 0;
+    // the walk of a unique interval (PH_WALK): stage 0 the suffix's text position SA[k],
+    // 1 text chunks compared with the read, 2 the row ISA[p] of the last matched suffix;
+    // ik = the current suffix's text position, il = positions matched
+    constexpr bool WALK = HSA_UNIQUE_WALK && !GAPS && sizeof(IT) == 4 && !F::NIB;
+    uint32_t wstage = 0;
+    uint32_t wstreak = 0;          // one-suffix match steps in a row (virtual tops): the walk's trigger
     // base of the current strand's sequence at p (from the LDS element, or the HBM row)
     auto getc = [&](int p) -> uint32_t {
         if constexpr (F::NIB) return WFmt<uint8_t>::code(rowp[((uint32_t)p >> 2) * 256u + ((uint32_t)p & 3u)]);
@@ -1206,6 +1224,25 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 break;
             }
             const uint32_t ph = C_PH(ctl);
+            if constexpr (WALK) {
+                if (ph == PH_WALK) {
+                    req = 5 + (int)wstage;                                // SA[k], a text chunk, ISA[p]
+                    rp1 = wstage == 0 ? e.x : ik;
+                    break;
+                }
+                if (ph == PH_WEXP) {
+                    // the walk's last matched node (popped as the run's last virtual top): a
+                    // hit at position 0 (bwtgap.c:176), else its expansion's rank step
+                    if (M_I(e.w) == 0) {
+                        SET_PH(ctl, PH_POP);
+                        if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
+                        continue;
+                    }
+                    req = 1; rp1 = e.x; rp2 = e.y + 1u;
+                    SET_PH(ctl, PH_EXPAND);
+                    break;
+                }
+            }
             if (ph == PH_EXACT) {
                 if constexpr (F::NIB) {
                     // the rank step goes out with the base load; an N (c > 3) drops it in (D)
@@ -1225,6 +1262,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 ctl &= ~(1u << 6);                                        // e already holds it
             } else {
                 DC(4);
+                wstreak = 0;
                 // pop the head of the lowest non-empty bucket
                 const int b = mask.lowest();
                 const uint32_t slot = HEAD(b);
@@ -1281,6 +1319,16 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 SET_PH(ctl, PH_EXACT);
                 continue;
             }
+            if constexpr (WALK) {
+                // a unique interval (one suffix) with enough read left: walk it against the
+                // text instead of one rank step per matched position
+                if (e.x == e.y && cold_args()->wsa && wstreak >= cold_args()->wstreak && (uint32_t)ei >= cold_args()->wmin) {
+                    wstage = 0;
+                    req = 5; rp1 = e.x;
+                    SET_PH(ctl, PH_WALK);
+                    break;
+                }
+            }
             if (tn) {
                 req = dep + 1u < a.ksd ? 3 : 4;
                 rp1 = (IT)(req == 3 ? trie_mbase(dep) + e.x : trie_base(a.ksd) + 4ull * e.x);
@@ -1325,6 +1373,20 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             for (int c = 0; c < 4; ++c) trie_s_load<IT>(a.kts, (uint64_t)rp1 + c, oa[c], ob[c], rkt[c], tL);
             st_q += 2u; ++st_t;
         }
+        uint32_t wv = 0, wt0 = 0, wt1 = 0, wt2 = 0;
+        if constexpr (WALK) {
+            if (req == 5 || req == 7) {
+                const ColdArgs r = cold_args();
+                wv = (req == 5 ? r->wsa : r->wisa)[(uint32_t)rp1];
+            } else if (req == 6) {
+                // the text words of positions [ik - 48, ik): the next 32 characters before ik
+                const uint32_t *tx = cold_args()->wtext;
+                const uint32_t wb = ((uint32_t)rp1 - 1u) >> 4;
+                wt2 = tx[wb];
+                wt1 = wb >= 1 ? tx[wb - 1] : 0u;
+                wt0 = wb >= 2 ? tx[wb - 2] : 0u;
+            }
+        }
 
 #ifdef HSA_DIAG
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1332,7 +1394,47 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
 #endif
         // ---------------- (D) apply
         const uint32_t ph = C_PH(ctl);
-        if (F::NIB && req == 1 && ph == PH_EXACT && cur_c > 3) {
+        if (WALK && req == 5) {
+            ik = wv; il = 0;                                             // the suffix's text position
+            if (ik == 0) SET_PH(ctl, PH_WEXP);                           // nothing before it ('$')
+            else wstage = 1;
+        } else if (WALK && req == 6) {
+            // compare the read's next bases with the text before the suffix, up to 32
+            const uint32_t np = (uint32_t)M_I(e.w) - il, q = ik;
+            uint32_t m = np < q ? np : q;
+            m = m < 32u ? m : 32u;
+            const uint32_t wb = (q - 1u) >> 4;
+            const int em = m_of(e.w);
+            uint32_t tm = 0;
+            bool pruned = false;
+            for (; tm < m; ++tm) {
+                const uint32_t tp = q - 1u - tm, d = wb - (tp >> 4);
+                const uint32_t tw = d == 0 ? wt2 : d == 1 ? wt1 : wt0;
+                const uint32_t tc = (tw >> (2u * (tp & 15u))) & 3u;
+                if (getc((int)(np - 1u - tm)) != tc) break;              // an N (> 3) never matches
+                // the matched child is the next pop: pruned when gap_shadow has raised a
+                // bid it reads (bwtgap.c:170), and the run ends with it
+                const int cp = (int)(np - 1u - tm);
+                if (cp > 0 && em < (int)(wbg(cp - 1) & F::BIDM)) { pruned = true; ++tm; break; }
+            }
+            il += tm; ik -= tm;
+            if (pruned) {
+                st_q += 2u * il; st_b += il; st_p += il;                 // its expansions and pops, the last pruned
+                SET_PH(ctl, PH_POP);
+            } else if (tm == 32u && np > 32u && q > 32u) {
+                // every one matched: the next chunk
+            } else if (il == 0) {
+                SET_PH(ctl, PH_WEXP);                                    // no match: the node's own expansion
+            } else {
+                wstage = 2;                                              // the row of the last matched suffix
+            }
+        } else if (WALK && req == 7) {
+            // il matched positions: il expansions (two rank queries each) and il virtual-top
+            // pops the reference makes; the node il positions on, one suffix at row ISA[p]
+            st_q += 2u * il; st_b += il; st_p += il;
+            e = E{(IT)wv, (IT)wv, e.z, meta_pack((uint32_t)M_I(e.w) - il, ST_M, 0u, (uint32_t)M_MM(e.w), 0u, 0u)};
+            SET_PH(ctl, PH_WEXP);
+        } else if (F::NIB && req == 1 && ph == PH_EXACT && cur_c > 3) {
             st_q -= 2u; st_b -= 1u + two;                                // not a step (2BWT-Interface.c:377)
             SET_PH(ctl, PH_POP);
         } else if (req == 2) {
@@ -1481,6 +1583,8 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 if (bk <= mask.lowest()) { e = v; ctl |= 1u << 6; }
                 else flush(v, bk);
             }
+            if constexpr (WALK)     // a one-suffix node whose match child is the next pop
+                wstreak = (ek == el && C_VT(ctl) && !M_ISD(e.w)) ? wstreak + 1u : 0u;
             SET_PH(ctl, PH_POP);
         }
 #ifdef HSA_DIAG
@@ -1828,6 +1932,11 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.kjm = mode == 2 ? 1u : HSA_TRIE_MAX_DEPTH;
     A.wkey = nullptr; A.perm = nullptr;
     A.fwd_list = nullptr; A.fwd_n = nullptr; A.fwd_only = 0; A.rmap = nullptr;
+    const char *we = getenv("HSA_WALK");          // HSA_WALK=0: rank steps only (A/B runs)
+    const bool walk = sizeof(IT) == 4 && ix->d_wsa && !(we && atoi(we) == 0);
+    A.wsa = walk ? ix->d_wsa : nullptr; A.wisa = walk ? ix->d_wisa : nullptr; A.wtext = walk ? ix->d_wtext : nullptr;
+    A.wmin = getenv("HSA_WALK_MIN") ? (uint32_t)atoi(getenv("HSA_WALK_MIN")) : 8u;
+    A.wstreak = getenv("HSA_WALK_STREAK") ? (uint32_t)atoi(getenv("HSA_WALK_STREAK")) : 2u;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg)) : nullptr;

@@ -95,6 +95,14 @@ int  hsa_index_device(const hsa_index_t *ix);
  * only when HSA_TRIE_MODE >= 1 at creation); *bytes of device memory they take.  Their
  * loads are counted in d_counters[10]. */
 int  hsa_index_trie(const hsa_index_t *ix, uint32_t *depth, uint32_t *sdepth, size_t *bytes);
+/* The unique-interval walk of ungapped 32-bit searches (hsa_amd/csrc/hsa_sa.hip): the
+ * full suffix array, its inverse and the packed forward text resident on the device
+ * (about 8 T + T / 4 bytes), so that k_search matches a one-suffix interval against the
+ * text instead of one rank pair per position (the same hits, rank-query and pop counts).
+ * d_sa_full: device SA[r] for rows 1..T as hsa_build_bwt_index_device(sa_interval 1)
+ * leaves it, or NULL to derive it from the sampled SA of hsa_index_set_sa; d_text_lsb:
+ * the text as the builder takes it, or NULL to derive it from the SA and the BWT. */
+int  hsa_index_build_walk(hsa_index_t *ix, const uint32_t *d_sa_full, const uint32_t *d_text_lsb);
 
 /* Rank/step/width primitives over host arrays (tests and tools). */
 int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t *pos, uint32_t *occ4_out);
