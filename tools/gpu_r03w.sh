@@ -1,0 +1,16 @@
+# Round 3 final validation (1 of 2): the whole GPU suite, smoke, the default bench at 200
+# steps with every leg, and the profiling recipe of config 2 on the final build
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    > gpurun_out/r03w_pytest.log 2>&1 || { tail -40 gpurun_out/r03w_pytest.log; exit 1; }
+tail -2 gpurun_out/r03w_pytest.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03w_smoke.log 2>&1 || { tail -20 gpurun_out/r03w_smoke.log; exit 2; }
+cat gpurun_out/r03w_smoke.log
+timeout -k 10 900 python -u bench.py --steps 200 --warmup 5 > gpurun_out/r03w_bench.json 2> gpurun_out/r03w_bench.err \
+    || { tail -40 gpurun_out/r03w_bench.err; exit 3; }
+grep -v "per-step device ms" gpurun_out/r03w_bench.err | tail -9
+bash tools/profile_run.sh r03f_c2 || exit 4
+echo profiled
