@@ -320,7 +320,8 @@ def spawn_ranks(n, argv, script=None):
                     procs[q].terminate()
         time.sleep(0.2)
     outs[0].seek(0)
-    sys.stdout.write(outs[0].read().decode())
+    for line in outs[0].read().decode().splitlines(keepends=True):   # the JSON line; the rest to stderr
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
     sys.stdout.flush()
     return rc
 
@@ -521,6 +522,12 @@ def main():
                          "and 32 with config 5's reads on one are A/B runs of the two instantiations")
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0)
+    ap.add_argument("--roofline-steps", type=int, default=-1,
+                    help="serialized steps after the timed region that the kernel roofline is taken over "
+                         "(-1: 20 when --streams > 1, else none: the timed launches themselves)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="handles on the index (hsa_index_clone) that consecutive steps alternate over, so step "
+                         "s+1's kernels fill the last waves of step s's k_search")
     ap.add_argument("--ref-sample", type=int, default=-1,
                     help="reads the REFERENCE's own CPU path (oracle/_ref/ref_probe) searches, over --ref-procs "
                          "processes (-1: 128 000 for config 2, 32 000 for config 3; 0: skip the reference legs)")
@@ -542,9 +549,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL over xGMI, one GPU per rank.  HSA_BENCH_BACKEND=gloo is a rehearsal of the
+    # N-rank path on a box with fewer GPUs: ranks share GPUs round-robin and the
+    # collectives go over gloo on host tensors (its timings say nothing about scaling).
+    backend = os.environ.get("HSA_BENCH_BACKEND", "nccl")
+    comm = None
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        gpu = local % torch.cuda.device_count() if backend == "gloo" else local
+        torch.cuda.set_device(gpu)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+            comm = torch.device("cpu")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            comm = torch.device("cuda", gpu)
     device = torch.cuda.current_device()
     _lib.configure(a.waves, a.pool, 0)
 
@@ -624,9 +642,12 @@ def main():
         so_opt = splice.seed_options(opt.as_dict())
         srg = regime_of(so_opt, n_stacks, so_opt["max_diff"])
 
-    def launch(j):
+    handles = [gi] + [gi.clone() for _ in range(max(1, a.streams) - 1)]
+
+    def launch(j, hi=0):
         j %= nd
         o = outs[j]
+        gi = handles[hi]
         b = DeviceBatch(d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[j].data_ptr(),
                         d_n_aln=o["n"].data_ptr(), d_flags=o["f"].data_ptr(), d_hit_off=o["o"].data_ptr(),
                         d_hits=o["h"].data_ptr(), hit_cap=hit_cap, d_counters=o["c"].data_ptr(),
@@ -646,9 +667,10 @@ def main():
     log(f"[bench] rank {rank}: random-sector gather probe over {gi.nbytes() / 2**30:.2f} GiB: {rand_gbs:.0f} GB/s "
         f"(16-B loads), {coop_gbs:.0f} GB/s (4 lanes x 16 B per sector), {rand64_gbs:.0f} GB/s (whole sectors per lane)")
 
-    lib_stream = torch.cuda.ExternalStream(gi.stream_handle())
-    for j in range(a.warmup):
-        launch(j)
+    S = len(handles)
+    lib_streams = [torch.cuda.ExternalStream(h.stream_handle()) for h in handles]
+    for j in range(max(a.warmup, S)):         # every handle's scratch is allocated before the timed region
+        launch(j if j < a.warmup else 0, j % S)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -658,9 +680,12 @@ def main():
         _lib.check(_lib.lib().hsa_diag_counters((C.c_ulonglong * 32)(), 1))
     t0 = time.perf_counter()
     for s in range(a.steps):
-        ev[s][0].record(lib_stream)
-        launch(a.warmup + s)
-        ev[s][1].record(lib_stream)
+        st = lib_streams[s % S]
+        if S > 1 and s >= nd:                 # read set (warmup + s) % nd's outputs: its last writer is done
+            st.wait_event(ev[s - nd][1])
+        ev[s][0].record(st)
+        launch(a.warmup + s, s % S)
+        ev[s][1].record(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -668,17 +693,35 @@ def main():
     kms = [e0.elapsed_time(e1) for e0, e1 in ev]
     # per-kernel device time of every timed step: HIP events the library records on
     # its stream around k_widths and k_search (+ its overflow re-run) of each pass
-    n_pt = min(a.steps, PASS_RING)             # the library keeps the newest PASS_RING passes
-    w_ms, s_ms = gi.pass_times(n_pt)
-    w_ms, s_ms = w_ms.astype(float), s_ms.astype(float)
-    seeds_ms = np.array(kms[-n_pt:]) - w_ms - s_ms if a.config == 4 else None
+    n_pt = min(a.steps, PASS_RING)             # the library keeps the newest PASS_RING passes per handle
+    per_h = [len(range(h, a.steps, S)) for h in range(S)]
+    pt = [handles[h].pass_times(min(per_h[h], PASS_RING)) for h in range(S) if per_h[h]]
+    w_ms = np.concatenate([p[0] for p in pt]).astype(float)
+    s_ms = np.concatenate([p[1] for p in pt]).astype(float)
+    n_pt = len(w_ms)
+    seeds_ms = float(np.mean(kms[-n_pt:]) - np.mean(w_ms) - np.mean(s_ms)) if a.config == 4 else None
     log(f"[bench] rank {rank}: per-step kernels: k_widths {np.mean(w_ms):.2f} ms, k_search {np.mean(s_ms):.2f} ms"
         + (f", splice seeds {np.mean(seeds_ms):.2f} ms" if a.config == 4 else ""))
     if os.environ.get("HSA_DIAG_OUT"):
         diag_dump(os.environ["HSA_DIAG_OUT"])
     log(f"[bench] rank {rank}: per-step device ms {[round(x, 2) for x in kms]}, wall {elapsed * 1e3:.1f} ms")
+    # With S > 1 handles the timed launches overlap, so their event times are not one
+    # launch's device time: the kernel roofline is then taken over R more steps of the
+    # same read sets, one after another on one stream, right after the timed region.
+    R = (min(a.steps, 20) if S > 1 else 0) if a.roofline_steps < 0 else a.roofline_steps
+    ovl_w, ovl_s = w_ms, s_ms
+    roof_sets = [(a.warmup + s) % nd for s in range(a.steps)]
+    if R:
+        torch.cuda.synchronize()
+        for s in range(R):
+            launch(a.warmup + s, 0)
+        torch.cuda.synchronize()
+        w_ms, s_ms = (x.astype(float) for x in handles[0].pass_times(min(R, PASS_RING)))
+        roof_sets = [(a.warmup + s) % nd for s in range(R)][-len(w_ms):]
+        log(f"[bench] rank {rank}: {R} serialized steps: k_widths {np.mean(w_ms):.2f} ms, k_search "
+            f"{np.mean(s_ms):.2f} ms (overlapped in the timed region: {np.mean(ovl_w):.2f} / {np.mean(ovl_s):.2f} ms)")
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -727,7 +770,7 @@ def main():
             mine[gidx] = (n_j, f_j, ho_j, h_j)
             digests[gidx] = batch_digest(n_j, f_j, hits_in_read_order(n_j, ho_j, h_j))
         t0 = time.perf_counter()
-        g = shard.gather_to_root(mine, dist, torch.device("cuda", local), per_batch=True)
+        g = shard.gather_to_root(mine, dist, comm, per_batch=True)
         t_gather = time.perf_counter() - t0
         all_dig = [None] * world
         dist.all_gather_object(all_dig, digests)
@@ -739,7 +782,7 @@ def main():
                       "batches_differing_from_rank_digest": bad, "backend": dist.get_backend()}
             log(f"[bench] gathered {gather['batches']} batches / {gather['reads']} reads / {gather['hits']} hits from "
                 f"{world} ranks in {gather['ms']} ms; {len(bad)} differ from their rank's digest")
-        cnt = torch.tensor([total_hits_local, mapped, fallback], dtype=torch.int64, device="cuda")
+        cnt = torch.tensor([total_hits_local, mapped, fallback], dtype=torch.int64, device=comm)
         dist.all_reduce(cnt)
         mapped_all, fallback_all = int(cnt[1].item()), int(cnt[2].item())
     else:
@@ -755,9 +798,16 @@ def main():
         # the dominant kernel: k_search, its algorithmic bytes per launch (the
         # reference's rank queries it answers x one 64-byte sector) over its mean
         # launch time from the per-pass HIP events
-        ach_search = q_search / a.steps * BYTES_PER_QUERY / (ms_search / 1e3) / 1e9
-        ach_widths = q_widths / a.steps * BYTES_PER_QUERY / (ms_widths / 1e3) / 1e9
-        ach_step = q_per_launch * BYTES_PER_QUERY / (mean_kms / 1e3) / 1e9
+        # the launches the kernel times above belong to (the timed ones, or the serialized
+        # roofline steps): their read sets' counters
+        cset = {j: outs[j]["c"].cpu().numpy() for j in set(roof_sets)}
+        qs_launch = float(np.mean([cset[j][2] - cset[j][7] for j in roof_sets]))
+        qw_launch = float(np.mean([cset[j][7] for j in roof_sets]))
+        ach_search = qs_launch * BYTES_PER_QUERY / (ms_search / 1e3) / 1e9
+        ach_widths = qw_launch * BYTES_PER_QUERY / (ms_widths / 1e3) / 1e9
+        # the whole step in the timed region: its algorithmic bytes over the wall time per step
+        ms_step = elapsed * 1e3 / a.steps
+        ach_step = q_per_launch * BYTES_PER_QUERY / (ms_step / 1e3) / 1e9
         pk = traffic_per_kernel(a.config)
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
@@ -773,12 +823,17 @@ def main():
                                    f"{RECORDS} records), {opt_str} (BASELINE configs[{a.config - 1}]); "
                                    f"{a.steps} timed steps",
                        "genome_bp": T, "reads_per_step": a.batch, "read_len": RL, "options": opt_str,
-                       "parallelism": f"reads sharded over {world} GPU(s), index replicated"},
+                       "parallelism": f"reads sharded over {world} GPU(s), index replicated",
+                       "streams": S},
             "roofline": {"bound": "hbm", "kernel": "k_search", "achieved": round(ach_search, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(ach_search / HBM_PEAK_GBS, 4),
                          "traffic": pk.get("k_search"),
                          "k_search_ms": round(ms_search, 3),
-                         "k_search_algorithmic_bytes_per_launch": q_search / a.steps * BYTES_PER_QUERY,
+                         "k_search_algorithmic_bytes_per_launch": qs_launch * BYTES_PER_QUERY,
+                         "kernel_times_from": (f"{len(s_ms)} serialized launches after the timed region (one stream; "
+                                               f"the {S} streams' timed launches overlap: k_widths "
+                                               f"{np.mean(ovl_w):.3f} ms, k_search {np.mean(ovl_s):.3f} ms per launch "
+                                               "there)") if R else "the timed launches",
                          "k_search_frac_of_random_sector": round(ach_search / rand_gbs, 4),
                          "k_search_frac_of_random_sector_coop": round(ach_search / coop_gbs, 4),
                          "k_widths": {"ms": round(ms_widths, 3), "achieved": round(ach_widths, 1),
@@ -787,7 +842,8 @@ def main():
                                       "rank_queries_per_read": round(q_widths / reads_local, 1),
                                       "issued_queries_per_read": round(q_widths_issued / reads_local, 1),
                                       "traffic": (pk.get("k_widths", 0) + pk.get("k_widths_reads", 0)) or None},
-                         "step": {"ms": round(mean_kms, 3), "achieved": round(ach_step, 1),
+                         "step": {"ms": round(ms_step, 3), "event_ms": round(mean_kms, 3),
+                                  "achieved": round(ach_step, 1),
                                   "frac": round(ach_step / HBM_PEAK_GBS, 4),
                                   "frac_of_random_sector": round(ach_step / rand_gbs, 4)},
                          "rank_queries_per_read": round(queries / reads_local, 1),

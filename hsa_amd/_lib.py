@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -31,6 +32,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
     "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced", "hsa_index_trie", "hsa_index_build_walk",
+    "hsa_index_clone",
 ]
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
@@ -169,6 +171,7 @@ def lib():
     L.hsa_index_bytes.argtypes = [vp]
     L.hsa_index_trie.argtypes = [vp, C.c_void_p, C.c_void_p, C.c_void_p]
     L.hsa_index_build_walk.argtypes = [vp, C.c_void_p, C.c_void_p]
+    L.hsa_index_clone.argtypes = [vp, C.POINTER(vp)]
     L.hsa_index_stream.restype = vp
     L.hsa_index_stream.argtypes = [vp]
     L.hsa_occ4_batch.argtypes = [vp, C.c_int, C.c_size_t, u32, u32]
@@ -300,7 +303,24 @@ class GpuIndex:
         rg = (Regime * len(regimes))(*regimes)
         check(lib().hsa_search_device64(self.h, rg, len(regimes), C.byref(batch), None))
 
+    def clone(self) -> "GpuIndex":
+        """A second handle on this resident index (hsa_index_clone): the rank blocks,
+        tries and SA are shared, the stream and search scratch are its own, so passes on
+        the two handles run concurrently.  Closing this index closes its clones first."""
+        h = C.c_void_p()
+        check(lib().hsa_index_clone(self.h, C.byref(h)))
+        c = GpuIndex.__new__(GpuIndex)
+        c.T, c.h, c._parent = self.T, h, self
+        if hasattr(self, "fwd_meta"):
+            c.fwd_meta = self.fwd_meta
+        if not hasattr(self, "_clones"):
+            self._clones = weakref.WeakSet()
+        self._clones.add(c)
+        return c
+
     def close(self):
+        for c in list(getattr(self, "_clones", ())):
+            c.close()
         if getattr(self, "h", None):
             lib().hsa_index_free(self.h)
             self.h = None

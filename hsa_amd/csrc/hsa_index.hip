@@ -403,10 +403,55 @@ extern "C" int hsa_index_create(int device, uint32_t T, uint32_t isa0, const uin
     return rc;
 }
 
+// A second handle on the same resident index for concurrent passes: the read-only
+// arrays are shared, the stream, events, scratch and staging are the clone's own.
+extern "C" int hsa_index_clone(hsa_index_t *src, hsa_index_t **out)
+{
+    if (!src || !out) { hsa_set_error("null argument"); return HSA_E_ARG; }
+    hsa_index *root = src->parent ? src->parent : src;
+    hsa_index *ix = nullptr;
+    int rc = index_init(root->device, &ix);
+    if (rc) return rc;
+    ix->T = root->T; ix->isa0 = root->isa0; memcpy(ix->C, root->C, sizeof ix->C);
+    ix->rT = root->rT; ix->risa0 = root->risa0; memcpy(ix->rC, root->rC, sizeof ix->rC);
+    for (int d = 0; d < 2; ++d) {
+        ix->blk[d] = root->blk[d]; ix->blk_base[d] = root->blk_base[d]; ix->nblk[d] = root->nblk[d];
+        ix->any_wrap[d] = root->any_wrap[d];
+    }
+    ix->wide = root->wide; ix->is64 = root->is64;
+    ix->T64 = root->T64; ix->isa0_64 = root->isa0_64; memcpy(ix->C64, root->C64, sizeof ix->C64);
+    ix->rT64 = root->rT64; ix->risa0_64 = root->risa0_64; memcpy(ix->rC64, root->rC64, sizeof ix->rC64);
+    ix->d_sa = root->d_sa; ix->d_blocks = root->d_blocks;
+    ix->sa_interval = root->sa_interval; ix->n_blocks = root->n_blocks;
+    ix->d_wsa = root->d_wsa; ix->d_wisa = root->d_wisa; ix->d_wtext = root->d_wtext;
+    ix->d_trie_s = root->d_trie_s; ix->d_trie_m = root->d_trie_m; ix->d_trie_w = root->d_trie_w;
+    ix->trie_depth = root->trie_depth; ix->trie_sdepth = root->trie_sdepth;
+    ix->trie_wide = root->trie_wide; ix->trie_bytes = root->trie_bytes;
+    ix->parent = root;
+    ++root->n_clones;
+    *out = ix;
+    return 0;
+}
+
+int hsa_need_unshared(const hsa_index *ix, const char *what)
+{
+    if (!ix->parent && !ix->n_clones) return 0;
+    hsa_set_error("%s: %s", what, ix->parent ? "not on a clone (call it on the index before cloning)"
+                                              : "the index has live clones (free them first)");
+    return HSA_E_ARG;
+}
+
 extern "C" void hsa_index_free(hsa_index_t *ix)
 {
     if (!ix) return;
     (void)hipSetDevice(ix->device);
+    if (ix->parent) {           // the shared arrays stay with the parent
+        --ix->parent->n_clones;
+        ix->blk_base[0] = ix->blk_base[1] = nullptr;
+        ix->d_sa = ix->d_blocks = nullptr;
+        ix->d_wsa = ix->d_wisa = ix->d_wtext = nullptr;
+        ix->d_trie_s = nullptr; ix->d_trie_m = nullptr; ix->d_trie_w = nullptr;
+    }
     (void)hipFree(ix->blk_base[0]); (void)hipFree(ix->blk_base[1]);
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big); hsa_scratch_free(ix->huge);
     if (ix->d_ovf2) (void)hipFree(ix->d_ovf2);

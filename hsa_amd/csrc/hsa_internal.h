@@ -89,7 +89,14 @@ struct hsa_index {
     hipEvent_t pev[PASS_RING][3] = {};
     uint64_t pev_n = 0;
     hipEvent_t ev_split = nullptr;      // recorded by launch_pass between k_widths and k_search
+    // hsa_index_clone: a clone shares the parent's read-only device arrays (rank blocks
+    // and wrap tables, tries, SA, walk arrays) and owns its stream, events and scratch
+    hsa_index *parent = nullptr;
+    int n_clones = 0;                   // live clones of this index
 };
+// HSA_E_ARG when an index's shared arrays may not be replaced (a clone, or an index with
+// live clones)
+int hsa_need_unshared(const hsa_index *ix, const char *what);
 
 int hsa_grow(void **p, size_t *cap, size_t need);
 int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap, size_t link_bytes = 2);

@@ -80,6 +80,7 @@ extern "C" int hsa_index_set_sa(hsa_index_t *ix, const uint32_t *sa_values, uint
         return HSA_E_ARG;
     }
     if (int rc0 = hsa_need32(ix)) return rc0;
+    if (int rc0 = hsa_need_unshared(ix, "hsa_index_set_sa")) return rc0;
     if (n_values < ((uint64_t)ix->T + interval) / interval) {
         hsa_set_error("hsa_index_set_sa: %llu values < (T + s) / s", (unsigned long long)n_values);
         return HSA_E_ARG;
@@ -179,6 +180,7 @@ extern "C" int hsa_index_build_walk(hsa_index_t *ix, const uint32_t *d_sa_full, 
 {
     if (int rc0 = hsa_need32(ix)) return rc0;
     if (ix->wide) { hsa_set_error("hsa_index_build_walk: 32-bit indexes only"); return HSA_E_ARG; }
+    if (int rc0 = hsa_need_unshared(ix, "hsa_index_build_walk")) return rc0;
     if (!d_sa_full && !ix->d_sa) { hsa_set_error("hsa_index_build_walk: no suffix array (hsa_index_set_sa)"); return HSA_E_ARG; }
     HSA_HIP(hipSetDevice(ix->device));
     (void)hipFree(ix->d_wsa); (void)hipFree(ix->d_wisa); (void)hipFree(ix->d_wtext);

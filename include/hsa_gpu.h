@@ -103,6 +103,14 @@ int  hsa_index_trie(const hsa_index_t *ix, uint32_t *depth, uint32_t *sdepth, si
  * leaves it, or NULL to derive it from the sampled SA of hsa_index_set_sa; d_text_lsb:
  * the text as the builder takes it, or NULL to derive it from the SA and the BWT. */
 int  hsa_index_build_walk(hsa_index_t *ix, const uint32_t *d_sa_full, const uint32_t *d_text_lsb);
+/* A second handle on the same resident index, for passes that run concurrently: the
+ * clone shares src's read-only device arrays (rank blocks, wrap tables, tries, SA, walk
+ * arrays) and has its own stream, events and search scratch, so hsa_search_device on
+ * the two handles may overlap (the next batch's k_widths fills the last waves of this
+ * one's k_search).  Free every clone before src; hsa_index_set_sa and
+ * hsa_index_build_walk refuse a clone and an index with live clones.  No reference
+ * counterpart: the reference searches one batch at a time (bwtaln.c:477, :506). */
+int  hsa_index_clone(hsa_index_t *src, hsa_index_t **out);
 
 /* Rank/step/width primitives over host arrays (tests and tools). */
 int hsa_occ4_batch(hsa_index_t *ix, int dir, size_t n, const uint32_t *pos, uint32_t *occ4_out);

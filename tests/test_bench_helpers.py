@@ -72,11 +72,12 @@ def test_shard_pack_roundtrip_scrambled():
 
 def test_spawn_ranks_sets_rank_env(tmp_path):
     """`bench.py --gpus N` without a launcher starts N ranks with the rendezvous
-    environment and relays rank 0's stdout (a stand-in script here: no GPU)."""
+    environment and relays rank 0's JSON line alone to stdout (a stand-in script here: no GPU)."""
     script = tmp_path / "rank.py"
     script.write_text("import json, os, sys\n"
                       "r = int(os.environ['RANK'])\n"
                       "assert os.environ['LOCAL_RANK'] == str(r) and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "if r == 0: print('[Gloo] Rank 0 is connected to 2 peer ranks.')\n"
                       "if r == 0: print(json.dumps({'world': int(os.environ['WORLD_SIZE']), 'argv': sys.argv[1:]}))\n")
     import contextlib
     import io

@@ -83,3 +83,77 @@ def test_hg19_sized_batch_matches_oracle(config):
     assert (o_n > 0).mean() > 0.9                     # the batch really maps (not a vacuous pass)
     if c[8] == 0:                                     # no capacity re-run: every query counted once
         assert int(c[2]) == int(o_q), (int(c[2]), int(o_q))
+
+
+def _device_batch(reads, max_gapo):
+    """Jobs, outputs and the DeviceBatch of one fixed-length 100 bp batch (bench.py's layout)."""
+    import torch
+
+    from hsa_amd import _lib
+    from hsa_amd._lib import DeviceBatch, GapOpt, Regime
+    n = len(reads)
+    opt = GapOpt.default()
+    opt.max_diff, opt.fnr, opt.max_gapo = 4, -1.0, max_gapo
+    opt.mode &= ~0x01
+    n_stacks = (opt.max_diff + 1) * opt.s_mm + (opt.max_gapo + 1) * opt.s_gapo + (opt.max_gape + 1) * opt.s_gape
+    rg = Regime(s_mm=opt.s_mm, s_gapo=opt.s_gapo, s_gape=opt.s_gape, mode=0, indel_end_skip=opt.indel_end_skip,
+                max_del_occ=opt.max_del_occ, max_entries=opt.max_entries, max_gapo=max_gapo, max_gape=opt.max_gape,
+                max_seed_diff=opt.max_seed_diff, max_top2=opt.max_top2, n_stacks=n_stacks, max_diff=opt.max_diff)
+    jobs = np.zeros(n, _lib.JOB_DTYPE)
+    jobs["off"] = np.arange(n, dtype=np.uint64) * 100
+    jobs["len"] = 100
+    jobs["max_diff"] = opt.max_diff
+    jobs["seed_len"] = opt.seed_len
+    t = dict(j=torch.from_numpy(jobs.view(np.uint8).copy()).cuda(),
+             r=torch.from_numpy(_lib.pad_codes(reads.reshape(-1))).cuda(),
+             n=torch.zeros(n, dtype=torch.int32, device="cuda"), f=torch.zeros(n, dtype=torch.int32, device="cuda"),
+             o=torch.zeros(n, dtype=torch.int64, device="cuda"), h=torch.zeros(n * 8 * 9, dtype=torch.int32, device="cuda"),
+             c=torch.zeros(16, dtype=torch.int64, device="cuda"))
+    b = DeviceBatch(d_jobs=t["j"].data_ptr(), n_jobs=n, d_codes=t["r"].data_ptr(), d_n_aln=t["n"].data_ptr(),
+                    d_flags=t["f"].data_ptr(), d_hit_off=t["o"].data_ptr(), d_hits=t["h"].data_ptr(), hit_cap=n * 8,
+                    d_counters=t["c"].data_ptr(), max_len=100, max_seed=opt.seed_len)
+    return rg, b, t
+
+
+def test_hg19_sized_clones_search_concurrently():
+    """hsa_index_clone: three batches of 100 000 reads issued back to back on two handles
+    of the same resident index without a synchronisation between them (bench.py
+    --streams 2), so the second handle's launches overlap the first's.  Every batch is
+    compared with the restatement, and its counters with a serialized run on one handle."""
+    import torch
+
+    import bench
+    from hsa_amd import synth
+    from hsa_amd._lib import HsaError
+    from oracle_ctypes import default_opt
+    gi, ox = _index()
+    cl = gi.clone()
+    genome = synth.PackedGenome(bench.GENOME_T, bench.GENOME_SEED)
+    recs = synth.record_layout(bench.GENOME_T, bench.RECORDS)
+    n = 100_000
+    sets = [synth.make_reads(genome, recs, n, 100, 5 * 1_000_000 + 91 + i, max_mm=4)[0] for i in range(3)]
+    bat = [_device_batch(r, 0) for r in sets]
+    for i, (rg, b, _) in enumerate(bat):
+        (gi if i % 2 == 0 else cl).search_device([rg], b)
+    torch.cuda.synchronize()
+    conc = [{k: t[k].cpu().numpy().copy() for k in "nfohc"} for _, _, t in bat]
+    od = default_opt()
+    od.update(max_diff=4, fnr=-1.0, max_gapo=0, mode=od["mode"] & ~0x01)
+    for i, (rg, b, t) in enumerate(bat):
+        o_n, o_f, o_h, o_q = bench.oracle_threaded(ox, sets[i], 100, od, bench.cpu_info()["threads"])
+        g = conc[i]
+        assert g["c"][11] == 0
+        bad, first = bench.compare_batch(g["n"], g["f"].astype(np.uint32), g["o"], g["h"].view(np.uint32).reshape(-1, 9),
+                                         o_n, o_f, o_h)
+        assert bad == 0, f"batch {i}: {bad} of {n} reads differ; first {first}"
+        if g["c"][8] == 0:
+            assert int(g["c"][2]) == int(o_q)
+        cl.search_device([rg], b)                     # serialized, on the clone alone
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(t["c"].cpu().numpy()[[1, 2, 4, 7, 8, 11]], g["c"][[1, 2, 4, 7, 8, 11]])
+    # the shared arrays cannot be replaced under a clone
+    with pytest.raises(HsaError, match="clone"):
+        cl.build_walk()
+    with pytest.raises(HsaError, match="clone"):
+        gi.build_walk()
+    cl.close()
