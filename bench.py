@@ -528,6 +528,8 @@ def main():
     ap.add_argument("--roofline-steps", type=int, default=-1,
                     help="serialized steps after the timed region that the kernel roofline is taken over "
                          "(-1: 20 when --streams > 1, else none: the timed launches themselves)")
+    ap.add_argument("--dropin-slots", type=int, default=1,
+                    help="also time the drop-in leg with its reads split over this many handles of the index")
     ap.add_argument("--streams", type=int, default=2,
                     help="handles on the index (hsa_index_clone) that consecutive steps alternate over, so step "
                          "s+1's kernels fill the last waves of step s's k_search")
@@ -879,19 +881,31 @@ def main():
     if rank == 0 and world == 1 and a.config in (2, 3) and a.dropin:
         src = batches[0]
         dres = {}
-        for per_call in (100_000, a.batch):
-            per_call = min(per_call, a.batch)
-            o = GapOpt.from_dict(opt.as_dict())
-            gi.cal_sa_reg_gap(np.full(per_call, RL, np.uint32), src[:per_call].reshape(-1), o)   # warm
-            t0 = time.perf_counter()
-            done = 0
-            while done < a.batch:
-                m = min(per_call, a.batch - done)
-                gi.cal_sa_reg_gap(np.full(m, RL, np.uint32), src[done:done + m].reshape(-1), o)
-                done += m
-            dt = time.perf_counter() - t0
-            dres[str(per_call)] = round(a.batch / dt, 1)
-            log(f"[bench] drop-in path: {a.batch} reads in calls of {per_call}: {a.batch / dt:.0f} reads/s")
+        for k_slots in sorted({1, a.dropin_slots}):
+            others = [gi.clone() for _ in range(k_slots - 1)]   # slots on this GPU: handles of one index
+            for per_call in (100_000, a.batch):
+                per_call = min(per_call, a.batch)
+                o = GapOpt.from_dict(opt.as_dict())
+
+                def call(m, r0):
+                    if others:
+                        gi.cal_sa_reg_gap_slots(others, np.full(m, RL, np.uint32), src[r0:r0 + m].reshape(-1), o)
+                    else:
+                        gi.cal_sa_reg_gap(np.full(m, RL, np.uint32), src[r0:r0 + m].reshape(-1), o)
+                call(per_call, 0)   # warm
+                t0 = time.perf_counter()
+                done = 0
+                while done < a.batch:
+                    m = min(per_call, a.batch - done)
+                    call(m, done)
+                    done += m
+                dt = time.perf_counter() - t0
+                key = str(per_call) + (f"_slots{k_slots}" if k_slots > 1 else "")
+                dres[key] = round(a.batch / dt, 1)
+                log(f"[bench] drop-in path: {a.batch} reads in calls of {per_call} over {k_slots} slot(s): "
+                    f"{a.batch / dt:.0f} reads/s")
+            for h in others:
+                h.close()
         result["dropin"] = {"unit": "reads/s", "reads_per_call": dres,
                             "what": "hsa_cal_sa_reg_gap_flat on host arrays: H2D reads, widths + search + "
                                     "re-runs, D2H hits, per-read unpacking (PCIe and host work included)"}

@@ -496,12 +496,15 @@ int hsa_gpu_set_devices(int n)
     return 0;
 }
 
-/* Upload one slot's copy of the bidirectional BWT (and SA, blocks). */
-static int attach_slot(const Idx2BWT *bi, int slot, hsa_index_t **out)
+/* Upload one slot's copy of the bidirectional BWT (and SA, blocks).  A slot on a device
+ * that already holds one (slot >= device count) is a clone of that slot's index: the
+ * same resident arrays, its own stream and scratch (hsa_index_clone). */
+static int attach_slot(const Idx2BWT *bi, int slot, hsa_index_t *const *have, hsa_index_t **out)
 {
     const BWT *f = bi->bwt, *r = bi->rev_bwt;
     const int nd = hsa_device_count();
     if (nd < 1) return HSA_E_NODEV;
+    if (slot >= nd) return hsa_index_clone(have[slot % nd], out);
     hsa_index_t *ix = NULL;
     int rc = hsa_index_create(slot % nd, f->textLength, f->inverseSa0, f->cumulativeFreq, f->bwtCode,
                               r->textLength, r->inverseSa0, r->cumulativeFreq, r->bwtCode, &ix);
@@ -535,7 +538,7 @@ int hsa_gpu_attach(const Idx2BWT *bi)
     int rc = 0;
     while (g_att[e].n < want && rc == 0) {
         hsa_index_t *ix = NULL;
-        rc = attach_slot(bi, g_att[e].n, &ix);
+        rc = attach_slot(bi, g_att[e].n, g_att[e].ix, &ix);
         if (rc == 0) g_att[e].ix[g_att[e].n++] = ix;
     }
     if (g_att[e].n == 0) g_att[e].key = NULL;
@@ -548,7 +551,7 @@ void hsa_gpu_detach(const Idx2BWT *bi)
     pthread_mutex_lock(&g_att_mu);
     const int e = find_entry(bi);
     if (e >= 0) {
-        for (int k = 0; k < g_att[e].n; ++k) hsa_index_free(g_att[e].ix[k]);
+        for (int k = g_att[e].n - 1; k >= 0; --k) hsa_index_free(g_att[e].ix[k]);   /* clones first */
         memset(&g_att[e], 0, sizeof g_att[e]);
     }
     pthread_mutex_unlock(&g_att_mu);

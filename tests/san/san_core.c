@@ -32,7 +32,29 @@ int hsa_index_create(int device, uint32_t T, uint32_t isa0, const uint32_t C[5],
     return *out ? 0 : HSA_E_MEM;
 }
 
-void hsa_index_free(hsa_index_t *ix) { or_index_free((or_index_t *)ix); }
+/* hsa_index_clone: the same restatement index under a reference count (a clone shares
+ * everything here; the drop-in makes one for a second slot on a device) */
+static struct { hsa_index_t *ix; int refs; } g_refs[32];
+
+int hsa_index_clone(hsa_index_t *src, hsa_index_t **out)
+{
+    for (int i = 0; i < 32; ++i)
+        if (g_refs[i].ix == src) { ++g_refs[i].refs; *out = src; return 0; }
+    for (int i = 0; i < 32; ++i)
+        if (!g_refs[i].ix) { g_refs[i].ix = src; g_refs[i].refs = 2; *out = src; return 0; }
+    return HSA_E_MEM;
+}
+
+void hsa_index_free(hsa_index_t *ix)
+{
+    for (int i = 0; i < 32; ++i)
+        if (g_refs[i].ix == ix) {
+            if (--g_refs[i].refs > 0) return;
+            g_refs[i].ix = NULL;
+            break;
+        }
+    or_index_free((or_index_t *)ix);
+}
 
 /* the sampled SA and chromosome blocks of the (one) attached index */
 static uint32_t *g_sa_vals, *g_sa_blocks, g_sa_interval;
