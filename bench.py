@@ -532,7 +532,8 @@ def main():
                     help="also time the drop-in leg with its reads split over this many handles of the index")
     ap.add_argument("--streams", type=int, default=2,
                     help="handles on the index (hsa_index_clone) that consecutive steps alternate over, so step "
-                         "s+1's kernels fill the last waves of step s's k_search")
+                         "s+1's kernels fill the last waves of step s's k_search; handles past the second whose "
+                         "search scratch does not fit are dropped")
     ap.add_argument("--ref-sample", type=int, default=-1,
                     help="reads the REFERENCE's own CPU path (oracle/_ref/ref_probe) searches, over --ref-procs "
                          "processes (-1: 128 000 for config 2, 32 000 for config 3; 0: skip the reference legs)")
@@ -672,6 +673,20 @@ def main():
     log(f"[bench] rank {rank}: random-sector gather probe over {gi.nbytes() / 2**30:.2f} GiB: {rand_gbs:.0f} GB/s "
         f"(16-B loads), {coop_gbs:.0f} GB/s (4 lanes x 16 B per sector), {rand64_gbs:.0f} GB/s (whole sectors per lane)")
 
+    # a handle past the second whose search scratch does not fit (a gapped regime's pool
+    # is ~95 GB per handle at config 3) is dropped before the timed region
+    for hi in range(len(handles)):              # in order: the first two must fit
+        try:
+            launch(0, hi)
+            torch.cuda.synchronize()
+        except _lib.HsaError as ex:
+            if hi < 2 or "allocation" not in str(ex):
+                raise
+            log(f"[bench] rank {rank}: {len(handles) - hi} handle(s) dropped: {ex}")
+            for h in handles[hi:]:
+                h.close()
+            del handles[hi:]
+            break
     S = len(handles)
     lib_streams = [torch.cuda.ExternalStream(h.stream_handle()) for h in handles]
     for j in range(max(a.warmup, S)):         # every handle's scratch is allocated before the timed region

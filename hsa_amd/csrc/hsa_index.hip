@@ -95,6 +95,7 @@ int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap
         hipMalloc(&s.nxt, pe * link_bytes) != hipSuccess ||
         hipMalloc(&s.hbuf, he * 9 * sizeof(uint32_t)) != hipSuccess) {
         hsa_set_error("scratch allocation failed (lanes %zu, pool %zu, hits %zu)", lanes, pcap, hcap);
+        (void)hipGetLastError();    // not sticky: a caller may free memory and go on
         hsa_scratch_free(s);
         return HSA_E_MEM;
     }
