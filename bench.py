@@ -284,6 +284,14 @@ def compare_batch(g_n, g_f, g_o, g_h, o_n, o_f, o_h):
     nb = int(bad.sum())
     return nb, (int(np.flatnonzero(bad)[0]) if nb else None)
 
+def step_plan(steps, warmup, nd, S):
+    """The timed loop's schedule: per step (handle, read set, step whose end it waits
+    for).  Steps on one handle run in issue order; a step that reuses a read set's
+    output buffers on another handle waits for that set's previous step, so no two
+    steps that may run at once write the same outputs (tests/test_bench_helpers.py)."""
+    return [(s % S, (warmup + s) % nd, s - nd if S > 1 and s >= nd else None) for s in range(steps)]
+
+
 # ---------------------------------------------------------------- N ranks from --gpus N
 def spawn_ranks(n, argv, script=None):
     """`bench.py --gpus N` without a launcher: start N ranks of this script (RANK,
@@ -699,12 +707,12 @@ def main():
     if os.environ.get("HSA_DIAG_OUT"):
         _lib.check(_lib.lib().hsa_diag_counters((C.c_ulonglong * 32)(), 1))
     t0 = time.perf_counter()
-    for s in range(a.steps):
-        st = lib_streams[s % S]
-        if S > 1 and s >= nd:                 # read set (warmup + s) % nd's outputs: its last writer is done
-            st.wait_event(ev[s - nd][1])
+    for s, (hi, _, after) in enumerate(step_plan(a.steps, a.warmup, nd, S)):
+        st = lib_streams[hi]
+        if after is not None:                 # read set (warmup + s) % nd's outputs: its last writer is done
+            st.wait_event(ev[after][1])
         ev[s][0].record(st)
-        launch(a.warmup + s, s % S)
+        launch(a.warmup + s, hi)
         ev[s][1].record(st)
     torch.cuda.synchronize()
     if world > 1:

@@ -4,6 +4,7 @@ import os
 import sys
 
 import numpy as np
+import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
@@ -95,3 +96,27 @@ def test_spawn_ranks_reports_a_failing_rank(tmp_path):
                       "if os.environ['RANK'] == '1': sys.exit(3)\n"
                       "time.sleep(30)\n")
     assert bench.spawn_ranks(2, [], script=str(script)) == 3
+
+
+@pytest.mark.parametrize("S,nd,warmup", [(1, 3, 1), (2, 3, 1), (2, 3, 5), (3, 3, 2), (2, 2, 0), (4, 3, 1), (3, 1, 1)])
+def test_step_plan_never_overlaps_writers_of_one_read_set(S, nd, warmup):
+    """bench.py's timed loop over S handles: any two steps writing the same read set's
+    outputs are ordered (same handle, or an event wait, transitively)."""
+    steps = 40
+    plan = bench.step_plan(steps, warmup, nd, S)
+    before = [set() for _ in range(steps)]          # steps known to finish before step s starts
+    last_on = {}
+    for s, (hi, _, after) in enumerate(plan):
+        preds = set()
+        if hi in last_on:
+            preds.add(last_on[hi])
+        if after is not None:
+            preds.add(after)
+        for p in preds:
+            before[s] |= before[p] | {p}
+        last_on[hi] = s
+    for b in range(steps):
+        for a in range(b):
+            if plan[a][1] == plan[b][1]:
+                assert a in before[b], (a, b, plan[a], plan[b])
+    assert [h for h, _, _ in plan[:S]] == list(range(S))
