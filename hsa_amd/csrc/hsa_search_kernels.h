@@ -133,6 +133,7 @@ struct SearchArgs {
     // start last and set the launch's tail
     uint8_t *wkey;
     const int32_t *perm;
+    uint32_t okey;                  // cost key with the tail length (default; HSA_ORDER_KEY=0: bid only)
     // lazy forward rows (k_widths_reads): a read whose rc search found nothing and whose
     // forward row was not computed goes to fwd_list (count *fwd_n); the forward pass
     // (fwd_only) searches just that strand
@@ -415,6 +416,7 @@ template <typename IT> struct WChain {
     IT prevw;
     uint32_t acc;
     uint32_t tl, tix;              // width trie: characters since the last reset, and their node
+    uint32_t lr;                   // position of the last reset (the cost order's tail length)
 };
 
 template <typename WT, typename IT>
@@ -442,7 +444,7 @@ __device__ __forceinline__ void width_step(const SearchArgs &a, WChain<IT> &ch, 
             }
             st_q += 2;
         }
-        if (ch.k > ch.l || c > 3) { ch.k = 0; ch.l = Ix<IT>::T(a); ++ch.bid; ch.tl = 0; ch.tix = 0; }
+        if (ch.k > ch.l || c > 3) { ch.k = 0; ch.l = Ix<IT>::T(a); ++ch.bid; ch.tl = 0; ch.tix = 0; ch.lr = t; }
         w = ch.l - ch.k + 1u;
     } else {
         w = 0; ++ch.bid;                                         // width[len] = {0, ++bid}
@@ -461,7 +463,17 @@ __device__ __forceinline__ void width_step(const SearchArgs &a, WChain<IT> &ch, 
 // One width row: both chains (the whole strand sequence and its last seed_len bases) of
 // list position q's strand; returns the rank queries, 64-byte sectors and trie loads it
 // took, and the chain's final bid (width[len].bid = the bid of the last base + 1).
-struct WRow { uint32_t q, b, t, bid; };
+struct WRow { uint32_t q, b, t, bid, tail; };
+
+// The cost key of a row (SearchArgs::wkey): its final bid, and with okey the length of
+// its last segment (positions after the last reset, where the search starts with the
+// least slack): a short one lets the search branch sooner.
+__device__ __forceinline__ uint8_t cost_key(const SearchArgs &a, const WRow &w)
+{
+    const uint32_t b = w.bid < 15u ? w.bid : 15u;
+    if (!a.okey) return (uint8_t)(w.bid < 255u ? w.bid : 255u);
+    return (uint8_t)(b << 4 | (w.tail < 16u ? 2u : w.tail < 48u ? 1u : 0u));
+}
 
 template <typename WT, typename IT>
 __device__ __forceinline__ WRow width_row(const SearchArgs &a, uint32_t R, uint32_t strand, const hsa_job_t &J)
@@ -491,7 +503,7 @@ __device__ __forceinline__ WRow width_row(const SearchArgs &a, uint32_t R, uint3
             width_step<WT, IT>(a, sd, t, slen, cs, 0u, srow, nullptr, st_q, st_b, st_t);
         }
     }
-    return WRow{st_q, st_b, st_t, f.bid};
+    return WRow{st_q, st_b, st_t, f.bid, len - f.lr};
 }
 
 // one atomic per wave and counter (the kernels' lanes all reach it)
@@ -518,7 +530,7 @@ __global__ void __launch_bounds__(BLOCK) k_widths(SearchArgs a)
         const hsa_job_t J = a.jobs[a.job_list ? a.job_list[q] : (int)q];
         w = width_row<WT, IT>(a, R, strand, J);
         if (!strand) a.wq[q] = w.q;
-        if (a.wkey) a.wkey[R] = (uint8_t)(w.bid < 255u ? w.bid : 255u);
+        if (a.wkey) a.wkey[R] = cost_key(a, w);
     }
     // rank queries: the reverse-complement strand is always searched (bwtaln.c:343)
     wave_add(&a.ctr[2], strand ? w.q : 0u);
@@ -552,7 +564,7 @@ __global__ void __launch_bounds__(BLOCK) k_widths_reads(SearchArgs a, uint32_t m
         const uint32_t R = mode == 1 ? q : mode == 3 ? (uint32_t)(((uint32_t)a.n_jobs + 63u) & ~63u) + p : 2u * q;
         w = width_row<WT, IT>(a, R, mode == 1 ? 1u : 0u, J);
         if (mode == 3) a.rmap[q] = (int32_t)R;
-        const uint8_t key = (uint8_t)(w.bid < 255u ? w.bid : 255u);
+        const uint8_t key = cost_key(a, w);
         if (mode == 1) {
             more = (int)w.bid - 1 > J.max_diff;
             a.wq[q] = HSA_NOFWD;
@@ -649,6 +661,10 @@ __device__ __forceinline__ uint32_t order_bin(const SearchArgs &a, uint32_t q)
 {
     const uint32_t k0 = a.wkey[2 * q], k1 = a.wkey[2 * q + 1];
     const uint32_t k = k0 < k1 ? k0 : k1;
+    if (a.okey) {                   // bid x 3 tail classes, costly first
+        const uint32_t v = (k >> 4) * 3u + (k & 15u);
+        return 15u - (v < 15u ? v : 15u);
+    }
     return 15u - (k < 15u ? k : 15u);
 }
 
@@ -1930,7 +1946,7 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     const int mode = tm ? atoi(tm) : 1;
     A.ksd = tr && mode ? ix->trie_sdepth : 0u;
     A.kjm = mode == 2 ? 1u : HSA_TRIE_MAX_DEPTH;
-    A.wkey = nullptr; A.perm = nullptr;
+    A.wkey = nullptr; A.perm = nullptr; A.okey = 0;
     A.fwd_list = nullptr; A.fwd_n = nullptr; A.fwd_only = 0; A.rmap = nullptr;
     const char *we = getenv("HSA_WALK");          // HSA_WALK=0: rank steps only (A/B runs)
     const bool walk = sizeof(IT) == 4 && ix->d_wsa && !(we && atoi(we) == 0);
@@ -2027,6 +2043,10 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
     if (order) {
         char *tail = (char *)A.wq + 4 * (size_t)n;
         A.wkey = (uint8_t *)tail;
+        // the tail-length key: config 2 k_search 18.5-18.9 -> 17.9-18.0 ms, config 3 and 5 1-2 %
+        // (profiles/r03_ab2_okey_*); HSA_ORDER_KEY=0: the final bid alone
+        static const uint32_t okey = getenv("HSA_ORDER_KEY") ? (uint32_t)atoi(getenv("HSA_ORDER_KEY")) : 1u;
+        A.okey = okey;
         const size_t ko = (2 * (size_t)n + 15) / 16 * 16;
         d_oh = (uint32_t *)(tail + ko);
         HSA_HIP(hipMemsetAsync(d_oh, 0, 32 * 4, st));

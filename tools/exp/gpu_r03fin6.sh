@@ -1,0 +1,14 @@
+# Closing run on the build with the tail-length cost key: GPU suite, smoke, config 2 at
+# 200 steps with every leg
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    > gpurun_out/fin6_pytest.log 2>&1 || { tail -40 gpurun_out/fin6_pytest.log; exit 1; }
+tail -2 gpurun_out/fin6_pytest.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/fin6_smoke.log 2>&1 || { tail -20 gpurun_out/fin6_smoke.log; exit 2; }
+cat gpurun_out/fin6_smoke.log
+timeout -k 10 900 python -u bench.py --steps 200 --warmup 5 > gpurun_out/fin6_bench.json 2> gpurun_out/fin6_bench.err \
+    || { tail -40 gpurun_out/fin6_bench.err; exit 3; }
+grep -v "per-step device ms" gpurun_out/fin6_bench.err | tail -12
