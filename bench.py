@@ -37,6 +37,7 @@ import json
 import os
 import sys
 import time
+from datetime import timedelta
 
 import numpy as np
 
@@ -461,6 +462,8 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
                          f"single-threaded), index files from the device-built BWTs; search seconds per process "
                          f"{min(ts):.1f}-{max(ts):.1f} (index load excluded)"}
         log(f"[bench] reference CPU path: {ref['value']:.0f} reads/s on {procs} cores ({ref['value_1core']:.0f} per core)")
+        if e2e_reads <= 0:
+            return {"reference": ref, "dropin_e2e": None}
         # the drop-in end to end on the same files: bwa_seq_t batches of 100 000 reads
         rb = os.path.join(d, "e2e_reads.bin")
         write_reads_bin(rb, reads_all[:e2e_reads])
@@ -544,8 +547,10 @@ def main():
                          "search scratch does not fit are dropped")
     ap.add_argument("--ref-sample", type=int, default=-1,
                     help="reads the REFERENCE's own CPU path (oracle/_ref/ref_probe) searches, over --ref-procs "
-                         "processes (-1: 128 000 for config 2, 32 000 for config 3; 0: skip the reference legs)")
-    ap.add_argument("--ref-procs", type=int, default=0, help="reference processes (0: the CPU threads of the share)")
+                         "processes (-1: 8 000 per process for config 2, 2 000 for config 3; 0: skip the reference "
+                         "legs)")
+    ap.add_argument("--ref-procs", type=int, default=0,
+                    help="reference processes (0: the CPU threads of the job's share, 16 per GPU rank)")
     ap.add_argument("--e2e-reads", type=int, default=1_000_000,
                     help="reads of the drop-in end-to-end leg (oracle/_ref/ref_probe_gpu, 100 000 per call)")
     ap.add_argument("--rank-parity", type=int, default=100_000,
@@ -584,9 +589,12 @@ def main():
     T = a.genome or (GENOME5_T if a.config == 5 else GENOME_T)
     RL = {4: 150, 5: 250}.get(a.config, READ_LEN)
     HW = _lib.ALN64_WORDS if wide else 9      # u32 words per hit record
+    # the reference's CPU path runs on rank 0 after the gather, one process per thread of
+    # the job's CPU share (16 per GPU rank: the whole share of the node at N = 8)
+    ref_procs = a.ref_procs or cpu_info()["threads"] * world
     if a.ref_sample < 0:
-        a.ref_sample = {2: 128_000, 3: 32_000}.get(a.config, 0)
-    ref_legs = rank == 0 and world == 1 and a.config in (2, 3) and not wide and a.ref_sample > 0 and T < (1 << 32)
+        a.ref_sample = {2: 8_000, 3: 2_000}.get(a.config, 0) * ref_procs
+    ref_legs = rank == 0 and a.config in (2, 3) and not wide and a.ref_sample > 0 and T < (1 << 32)
     t0 = time.time()
     if wide:
         gi, res, extra = build_index64(T, GENOME_SEED, device)
@@ -818,23 +826,28 @@ def main():
     else:
         mapped_all, fallback_all = mapped, fallback
 
+    # the dominant kernel: k_search, its algorithmic bytes per launch (the reference's
+    # rank queries it answers x one 64-byte sector) over its mean launch time from the
+    # per-pass HIP events of the launches the kernel times above belong to (the timed
+    # ones, or the serialized roofline steps): their read sets' counters.  Every rank
+    # measures its own; rank 0 reports them all.
+    ms_search, ms_widths = float(np.mean(s_ms)), float(np.mean(w_ms))
+    cset = {j: outs[j]["c"].cpu().numpy() for j in set(roof_sets)}
+    qs_launch = float(np.mean([cset[j][2] - cset[j][7] for j in roof_sets]))
+    qw_launch = float(np.mean([cset[j][7] for j in roof_sets]))
+    ach_search = qs_launch * BYTES_PER_QUERY / (ms_search / 1e3) / 1e9
+    ach_widths = qw_launch * BYTES_PER_QUERY / (ms_widths / 1e3) / 1e9
+    per_rank_roof = [(rank, ms_search, ach_search, rand_gbs)]
+    if world > 1:
+        per_rank_roof = [None] * world
+        dist.all_gather_object(per_rank_roof, (rank, ms_search, ach_search, rand_gbs))
+
     result = None
     if rank == 0:
         reads_all = reads_local * world
         value = reads_all / elapsed
         mean_kms = float(np.mean(kms))
         q_per_launch = queries / a.steps
-        ms_search, ms_widths = float(np.mean(s_ms)), float(np.mean(w_ms))
-        # the dominant kernel: k_search, its algorithmic bytes per launch (the
-        # reference's rank queries it answers x one 64-byte sector) over its mean
-        # launch time from the per-pass HIP events
-        # the launches the kernel times above belong to (the timed ones, or the serialized
-        # roofline steps): their read sets' counters
-        cset = {j: outs[j]["c"].cpu().numpy() for j in set(roof_sets)}
-        qs_launch = float(np.mean([cset[j][2] - cset[j][7] for j in roof_sets]))
-        qw_launch = float(np.mean([cset[j][7] for j in roof_sets]))
-        ach_search = qs_launch * BYTES_PER_QUERY / (ms_search / 1e3) / 1e9
-        ach_widths = qw_launch * BYTES_PER_QUERY / (ms_widths / 1e3) / 1e9
         # the whole step in the timed region: its algorithmic bytes over the wall time per step
         ms_step = elapsed * 1e3 / a.steps
         ach_step = q_per_launch * BYTES_PER_QUERY / (ms_step / 1e3) / 1e9
@@ -887,7 +900,11 @@ def main():
                          "peak_random_sector_measured": round(rand_gbs, 1),
                          "peak_random_sector_measured_coop4x16": round(coop_gbs, 1),
                          "peak_random_sector_measured_64B_loads": round(rand64_gbs, 1),
-                         "traffic_source": TRAFFIC_SRCS.get(a.config)},
+                         "traffic_source": TRAFFIC_SRCS.get(a.config),
+                         "per_rank": {str(r): {"k_search_ms": round(m, 3), "achieved": round(x, 1),
+                                               "frac": round(x / HBM_PEAK_GBS, 4),
+                                               "frac_of_random_sector": round(x / g, 4)}
+                                      for r, m, x, g in per_rank_roof}},
             "mapped_frac": round(mapped_all / reads_all, 4), "fallback_frac": round(fallback_all / reads_all, 4),
             "pops_per_read": round(pops / reads_local, 1),
         }
@@ -1054,13 +1071,16 @@ def main():
                                                 f"the 6 seed searches of its {int((fl & 1).sum())} fallback reads, "
                                                 f"1 thread, in {dt1:.1f} s"}
     # the reference's own CPU path, and the drop-in end to end (rank 0, N=1, configs 2, 3)
+    # With N ranks it runs after the gather on rank 0, over the CPU share of all N ranks
+    # (the other ranks wait on the rendezvous store meanwhile, without spinning a core);
+    # the drop-in end to end needs a GPU of its own and runs at N = 1 only.
     if ref_legs:
-        procs = a.ref_procs or cpu_info()["threads"]
+        procs = ref_procs
         j0 = a.warmup % nd
         opt_args = ["-n", "4", "-o", str(max_gapo)]
         try:
             legs = reference_legs(T, res, extra, batches[j0], opt_args, min(a.ref_sample, a.batch), procs,
-                                  min(a.e2e_reads, a.batch))
+                                  min(a.e2e_reads, a.batch) if world == 1 else 0)
         except Exception as ex:                       # reported, never fatal: a baseline
             legs = {"error": f"{type(ex).__name__}: {ex}"[:400]}
             log(f"[bench] reference legs failed: {legs['error']}")
@@ -1071,12 +1091,18 @@ def main():
                 result["cpu_baseline"].update(cpu_model=port["cpu_model"],
                                               physical_cores_visible=port["physical_cores_visible"],
                                               port={k: port[k] for k in ("value", "cores", "value_1core", "sample")})
-            result["dropin_e2e"] = legs["dropin_e2e"]
+            if legs.get("dropin_e2e"):
+                result["dropin_e2e"] = legs["dropin_e2e"]
         else:
             result["reference_legs"] = legs
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("hsa_bench_done", "1")
+        else:
+            store.wait(["hsa_bench_done"], timedelta(minutes=30))
         dist.barrier()
         dist.destroy_process_group()
 

@@ -32,7 +32,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
     "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced", "hsa_index_trie", "hsa_index_build_walk",
-    "hsa_index_clone",
+    "hsa_index_clone", "hsa_splice_prefetch_batch",
 ]
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
@@ -129,6 +129,14 @@ class SeedBatch(C.Structure):
                 ("d_counters", C.c_void_p), ("max_len", C.c_int32)]
 
 
+class SplicePf(C.Structure):
+    """hsa_splice_pf_t (include/hsa_gpu.h): the splice prefetch's outputs."""
+    _fields_ = [("n", C.c_int), ("max_len", C.c_int), ("row_stride", C.c_int), ("cw_stride", C.c_int),
+                ("rows", C.c_void_p), ("call_n", C.c_void_p), ("call_hit", C.c_void_p), ("hits", C.c_void_p),
+                ("wafter", C.c_void_p), ("call_sa", C.c_void_p), ("sa", C.c_void_p), ("n_hits", C.c_uint64),
+                ("n_sa", C.c_uint64), ("kernel_ms", C.c_double)]
+
+
 _lib = None
 
 
@@ -194,6 +202,9 @@ def lib():
     L.hsa_match_gap_batch.argtypes = [vp, C.POINTER(Regime), C.c_int, vp, vp, C.c_int, u8, C.c_size_t, i32, C.c_size_t,
                                       i32, i32, u64, C.POINTER(C.POINTER(C.c_uint32)), C.POINTER(Stats)]
     L.hsa_splice_seeds_device.argtypes = [vp, C.POINTER(Regime), C.POINTER(SeedBatch), vp]
+    if hasattr(L, "hsa_splice_prefetch_batch"):
+        L.hsa_splice_prefetch_batch.argtypes = [vp, C.POINTER(Regime), C.POINTER(Regime), C.c_int, u32, u64, u8,
+                                                C.c_size_t, i32, C.POINTER(SplicePf)]
     if hasattr(L, "hsa_search_device64"):           # (older A/B builds lack the 64-bit path)
         L.hsa_index_create_device64.argtypes = [C.c_int, C.c_uint64, C.c_uint64, u64, vp, C.c_uint64, C.c_uint64,
                                                 u64, vp, C.POINTER(vp)]
@@ -342,6 +353,31 @@ class GpuIndex:
         """The six splice seed searches of every fallback read of a device batch
         (hsa_splice_seeds_device); records 6 r + i on the device."""
         check(lib().hsa_splice_seeds_device(self.h, C.byref(seed_regime), C.byref(batch), None))
+
+    def splice_prefetch(self, seed_regime, anchor_regime, lens, codes, anchor_max_diff):
+        """hsa_splice_prefetch_batch over host reads: numpy copies of its outputs
+        (rows (n, 6, row_stride, 2), call_n (n, 8), call_hit, hits (m, 9), wafter
+        (n, 8, cw_stride, 2), call_sa, sa (k, 4))."""
+        lens = np.ascontiguousarray(lens, np.uint32)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
+        amd = np.ascontiguousarray(anchor_max_diff, np.int32)
+        o = SplicePf()
+        check(lib().hsa_splice_prefetch_batch(self.h, C.byref(seed_regime), C.byref(anchor_regime), len(lens), lens,
+                                              offs, codes, len(codes), amd, C.byref(o)))
+        n, rs, cws = o.n, o.row_stride, o.cw_stride
+
+        def arr(ptr, ct, count):
+            if not ptr or count == 0:
+                return np.zeros(0, ct)
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(ct))), (count,)).copy()
+        return dict(rows=arr(o.rows, np.int32, n * 6 * rs * 2).reshape(n, 6, rs, 2),
+                    call_n=arr(o.call_n, np.int32, n * 8).reshape(n, 8),
+                    call_hit=arr(o.call_hit, np.uint64, n * 8).reshape(n, 8),
+                    hits=arr(o.hits, np.uint32, int(o.n_hits) * 9).reshape(-1, 9),
+                    wafter=arr(o.wafter, np.int32, n * 8 * cws * 2).reshape(n, 8, cws, 2),
+                    call_sa=arr(o.call_sa, np.uint64, n * 8).reshape(n, 8) if o.call_sa else None,
+                    sa=arr(o.sa, np.uint32, int(o.n_sa) * 4).reshape(-1, 4), kernel_ms=o.kernel_ms)
 
     def set_sa(self, sa, blocks):
         """Upload the sampled SA (index_io.SaFile) and the block table (rows of

@@ -33,12 +33,8 @@
 #pragma weak hsa_splice_memo_stats
 #pragma weak hsa_splice_extend_active
 #pragma weak hsa_splice_run
-#pragma weak hsa_splice_width_active
-#pragma weak hsa_splice_widths_prefetch
-#pragma weak hsa_splice_wmemo_clear
-#pragma weak hsa_splice_wmemo_stats
-#pragma weak hsa_splice_take_sa_list
-#pragma weak hsa_splice_sa_prefetch
+#pragma weak hsa_splice_table_stats
+#pragma weak hsa_splice_set_read
 #pragma weak hsa_splice_sa_clear
 #pragma weak hsa_splice_sa_stats
 
@@ -185,6 +181,18 @@ static void write_outputs(bwa_seq_t *seqs, int n, const int32_t *n_aln, const ui
     }
     out_run(&part[0]);
     for (int k = 1; k < nt; ++k) if (started[k]) pthread_join(th[k], NULL);
+}
+
+/* write_outputs on a thread of its own (while the splice prefetch runs on the device) */
+typedef struct {
+    bwa_seq_t *seqs; int n; const int32_t *n_aln; const uint32_t *flags; const uint64_t *hoff; const uint32_t *hits;
+} out_job_t;
+
+static void *out_job_run(void *arg)
+{
+    const out_job_t *j = (const out_job_t *)arg;
+    write_outputs(j->seqs, j->n, j->n_aln, j->flags, j->hoff, j->hits);
+    return NULL;
 }
 
 /* One read of the bwtaln.c:303-337 prologue under regime `cur` (0 = A, 1 = B). */
@@ -605,6 +613,26 @@ static void ref_stack_free(gap_stack_t *s)
     free(s);
 }
 
+static pthread_mutex_t g_call_mu;
+static pthread_once_t g_call_once = PTHREAD_ONCE_INIT;
+
+static void call_mu_init(void)
+{
+    pthread_mutexattr_t a;
+    pthread_mutexattr_init(&a);
+    pthread_mutexattr_settype(&a, PTHREAD_MUTEX_RECURSIVE);
+    pthread_mutex_init(&g_call_mu, &a);
+    pthread_mutexattr_destroy(&a);
+}
+
+void hsa_gpu_lock(void)
+{
+    pthread_once(&g_call_once, call_mu_init);
+    pthread_mutex_lock(&g_call_mu);
+}
+
+void hsa_gpu_unlock(void) { pthread_mutex_unlock(&g_call_mu); }
+
 double hsa_now(void)
 {
     struct timespec t;
@@ -654,62 +682,55 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     memset(&aux, 0, sizeof aux);
     int have_splice = bwt_splice_match != NULL;
     const int n_stacks = hsa_aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
-    /* the splice path's seed searches of every fallback read in one GPU batch, when
-     * the host's bwt_splice_match calls our bwt_match_gap (bwtgap_gpu.c) */
-    int prefetched = 0, wprefetched = 0, saprefetched = 0;
+    /* the splice path's widths, seed and anchor searches and SA lookups of every fallback
+     * read in one device pass (hsa_splice_prefetch, bwtgap_gpu.c), when the host's
+     * bwt_splice_match calls our bwt_match_gap; the per-read output arrays are written on
+     * host threads meanwhile */
+    int prefetched = 0;
     double t_pf = 0.0;
     const double t1 = hsa_now();
-    if (have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active()) {
-        int nf = 0;
-        for (int i = 0; i < n_seqs; ++i)
-            nf += !(flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) && n_aln[i] == 0 && (flags[i] & HSA_F_FALLBACK);
-        if (nf > 0) {
-            bwt_aux_t *fa = (bwt_aux_t *)calloc((size_t)nf, sizeof(bwt_aux_t));
-            bwt_aux_t **fp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)nf);
-            gap_opt_t *fo = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nf);
-            ubyte_t *rc = (ubyte_t *)malloc(tot + 1);
-            gap_stack_t st_shape;                       /* only n_stacks is read */
-            memset(&st_shape, 0, sizeof st_shape);
-            st_shape.n_stacks = n_stacks;
-            int q = 0;
-            for (int i = 0; i < n_seqs; ++i) {
-                if ((flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) || n_aln[i] != 0 || !(flags[i] & HSA_F_FALLBACK)) continue;
-                const bwa_seq_t *p = seqs + i;
-                ubyte_t *r = rc + offs[i];
-                for (int j = 0; j < (int)p->len; ++j) {
-                    ubyte_t c = p->seq[p->len - 1 - j];
-                    r[j] = c < 4 ? (ubyte_t)(3 - c) : c;
-                }
-                fo[q] = local;
-                fo[q].max_diff = sp[2 * i];
-                fo[q].seed_len = sp[2 * i + 1];
-                fa[q].bi_bwt = (Idx2BWT *)bi_bwt; fa[q].arr = arr; fa[q].max_len = max_len;
-                fa[q].seq = p->seq; fa[q].rc_seq = r; fa[q].len = (int)p->len; fa[q].opt = fo + q;
-                fa[q].stack = &st_shape;
-                fp[q] = fa + q;
-                ++q;
+    /* HSA_SPLICE_PREFETCH=0: no table, every splice-path call goes to the GPU on its own
+     * (tests: misses from several runner threads at once) */
+    const char *pfe = getenv("HSA_SPLICE_PREFETCH");
+    const int want_pf = !pfe || atoi(pfe) != 0;
+    int nf = 0;
+    for (int i = 0; i < n_seqs; ++i)
+        nf += !(flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) && n_aln[i] == 0 && (flags[i] & HSA_F_FALLBACK);
+    out_job_t oj = {seqs, n_seqs, n_aln, flags, hoff, hits};
+    pthread_t oth;
+    int out_async = 0;
+    if (want_pf && nf > 0 && have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active()) {
+        out_async = pthread_create(&oth, NULL, out_job_run, &oj) == 0;
+        bwt_aux_t *fa = (bwt_aux_t *)calloc((size_t)nf, sizeof(bwt_aux_t));
+        bwt_aux_t **fp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)nf);
+        gap_opt_t *fo = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nf);
+        ubyte_t *rc = (ubyte_t *)malloc(tot + 1);
+        gap_stack_t st_shape;                       /* only n_stacks is read */
+        memset(&st_shape, 0, sizeof st_shape);
+        st_shape.n_stacks = n_stacks;
+        int q = 0;
+        for (int i = 0; i < n_seqs; ++i) {
+            if ((flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) || n_aln[i] != 0 || !(flags[i] & HSA_F_FALLBACK)) continue;
+            const bwa_seq_t *p = seqs + i;
+            ubyte_t *r = rc + offs[i];
+            for (int j = 0; j < (int)p->len; ++j) {
+                ubyte_t c = p->seq[p->len - 1 - j];
+                r[j] = c < 4 ? (ubyte_t)(3 - c) : c;
             }
-            t_pf = hsa_now();
-            hsa_splice_prefetch(bi_bwt, nf, fp);
-            /* and the widths the splice path computes (bwtext_gpu.c), when the host calls
-             * our bwt_cal_width */
-            if (hsa_splice_width_active && hsa_splice_width_active()) {
-                hsa_splice_widths_prefetch(bi_bwt, nf, fp);
-                wprefetched = 1;
-            }
-            /* and, with the whole splice path on the device (bwtext_gpu.c), the SA ->
-             * position lookups its correlation makes on the prefetched hits */
-            uint32_t *sal = NULL;
-            const size_t nsal = hsa_splice_take_sa_list ? hsa_splice_take_sa_list(&sal) : 0;
-            if (hsa_splice_sa_prefetch && hsa_splice_extend_active && hsa_splice_extend_active() && nsal) {
-                hsa_splice_sa_prefetch(bi_bwt, nsal, sal);
-                saprefetched = 1;
-            }
-            free(sal);
-            t_pf = hsa_now() - t_pf;
-            prefetched = 1;
-            free(fa); free(fp); free(fo); free(rc);
+            fo[q] = local;
+            fo[q].max_diff = sp[2 * i];
+            fo[q].seed_len = sp[2 * i + 1];
+            fa[q].bi_bwt = (Idx2BWT *)bi_bwt; fa[q].arr = arr; fa[q].max_len = max_len;
+            fa[q].seq = p->seq; fa[q].rc_seq = r; fa[q].len = (int)p->len; fa[q].opt = fo + q;
+            fa[q].stack = &st_shape;
+            fp[q] = fa + q;
+            ++q;
         }
+        t_pf = hsa_now();
+        hsa_splice_prefetch(bi_bwt, nf, fp);
+        t_pf = hsa_now() - t_pf;
+        prefetched = 1;
+        free(fa); free(fp); free(fo); free(rc);
     }
     /* the host's splice path for the fallback reads: all of them at once as coroutines
      * whose seed extensions run batched on the GPU, when the host calls our
@@ -721,11 +742,14 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
         sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)n_seqs + 1));
         sr_idx = (int *)malloc(sizeof(int) * ((size_t)n_seqs + 1));
     }
-    write_outputs(seqs, n_seqs, n_aln, flags, hoff, hits);
+    if (out_async) pthread_join(oth, NULL);
+    else write_outputs(seqs, n_seqs, n_aln, flags, hoff, hits);
+    int q_fb = 0;                                               /* the read's prefetch-table number */
     for (int i = 0; i < n_seqs; ++i) {                          /* the splice path's reads, in order */
         bwa_seq_t *p = seqs + i;
         if ((flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) || n_aln[i] > 0) continue;
         if (!(flags[i] & HSA_F_FALLBACK) || !have_splice) continue;
+        const int q_this = q_fb++;
         gap_opt_t lo = local;                                   /* aux->opt = &local_opt (:363) */
         lo.max_diff = sp[2 * i];
         lo.seed_len = sp[2 * i + 1];
@@ -754,7 +778,9 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
             aux.rc_seq[j] = c < 4 ? (ubyte_t)(3 - c) : c;
         }
         int na = 0;
+        if (hsa_splice_set_read) hsa_splice_set_read(prefetched ? q_this : -1);
         p->aln = bwt_splice_match(&aux, &na);
+        if (hsa_splice_set_read) hsa_splice_set_read(-1);
         p->n_aln = na;
         if (na == 0) { free(p->aln); p->aln = NULL; }
     }
@@ -784,25 +810,19 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     }
     if (prefetched) {
         if (getenv("HSA_VERBOSE") && hsa_splice_memo_stats) {
-            uint64_t mh = 0, mm = 0;
+            uint64_t mh = 0, mm = 0, wh = 0, wm = 0, sh = 0, sm = 0;
             hsa_splice_memo_stats(&mh, &mm);
-            fprintf(stderr, "[hsa] splice prefetch: %llu bwt_match_gap calls answered from the batch, %llu run alone\n",
-                    (unsigned long long)mh, (unsigned long long)mm);
+            if (hsa_splice_table_stats) hsa_splice_table_stats(&wh, &wm, &sh, &sm);
+            fprintf(stderr, "[hsa] splice prefetch: %llu bwt_match_gap calls answered from the batch, %llu run alone; "
+                            "%llu bwt_cal_width calls from the batch, %llu alone; %llu SA lookups from the batch, %llu "
+                            "not\n", (unsigned long long)mh, (unsigned long long)mm, (unsigned long long)wh,
+                    (unsigned long long)wm, (unsigned long long)sh, (unsigned long long)sm);
         }
         hsa_splice_memo_clear();
     }
-    if (wprefetched) {
-        if (getenv("HSA_VERBOSE")) {
-            uint64_t wh = 0, wm = 0;
-            hsa_splice_wmemo_stats(&wh, &wm);
-            fprintf(stderr, "[hsa] splice widths: %llu bwt_cal_width calls answered from the batch, %llu run alone\n",
-                    (unsigned long long)wh, (unsigned long long)wm);
-        }
-        hsa_splice_wmemo_clear();
-    }
-    /* the runner's rounds add their lookups to the SA table too: clear it after every
-     * batch that prefetched or ran the coroutine runner, so it never outgrows a batch */
-    if (saprefetched || (n_sr > 0 && hsa_splice_sa_clear)) {
+    /* the runner's rounds add their lookups to the SA table: clear it after every batch
+     * that ran the coroutine runner, so it never outgrows a batch */
+    if (n_sr > 0 && hsa_splice_sa_clear) {
         if (getenv("HSA_VERBOSE") && hsa_splice_sa_stats) {
             uint64_t sh = 0, sm = 0;
             hsa_splice_sa_stats(&sh, &sm);

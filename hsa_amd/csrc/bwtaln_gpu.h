@@ -13,6 +13,12 @@ hsa_index_t *hsa_gpu_index_of(const Idx2BWT *bi);
 hsa_index_t *const *hsa_gpu_slots_of(const Idx2BWT *bi, int *n);
 /* an error message for hsa_last_error() set from C (the library's buffer is per thread) */
 void hsa_gpu_set_error_text(const char *msg);
+/* Direct calls into slot 0's index from the reference-ABI entry points (a splice
+ * table miss, a one-off extension or SA lookup, the SAM stage's lookups) share that
+ * index's staging buffers, events and stream: they hold this (recursive) lock, so that
+ * the splice runner's worker threads never interleave two of them. */
+void hsa_gpu_lock(void);
+void hsa_gpu_unlock(void);
 /* the reference's convention for unrecoverable errors: message + exit(1) */
 void hsa_gpu_fatal(const char *what, long rc) __attribute__((noreturn));
 /* A bump allocator for the per-batch splice tables: entries live until the table is
@@ -51,6 +57,11 @@ int hsa_splice_prefetch_active(void);
 int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux);
 void hsa_splice_memo_clear(void);
 void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses);
+void hsa_splice_table_stats(uint64_t *w_hits, uint64_t *w_misses, uint64_t *sa_hits, uint64_t *sa_misses);
+/* the prefetch table's answers for the read the calling thread works on */
+void hsa_splice_set_read(int r);
+int hsa_splice_table_width(const Idx2BWT *bi, int len, const ubyte_t *str, bwt_width_t *width, int type, int *ret);
+int hsa_splice_table_sa(const Idx2BWT *bi, uint32_t idx, uint32_t o[3]);
 
 /* the splice path's seed extensions and its batched runner (bwtext_gpu.c; referred to
  * weakly as well) */
@@ -60,16 +71,11 @@ typedef struct {
     gap_opt_t opt;             /* local_opt as bwt_splice_match receives it for this read */
 } hsa_splice_read_t;
 int hsa_splice_extend_active(void);
-size_t hsa_splice_take_sa_list(uint32_t **idx);
-int hsa_splice_sa_prefetch(const Idx2BWT *bi, size_t n, const uint32_t *idx);
 void hsa_splice_sa_clear(void);
 void hsa_splice_sa_stats(uint64_t *hits, uint64_t *misses);
 void hsa_splice_sa_position(Idx2BWT *bi, unsigned int sa_index, unsigned int *seq_id, unsigned int *ori_pos,
                             unsigned int *occ_pos);
 int hsa_splice_width_active(void);
-int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux);
-void hsa_splice_wmemo_clear(void);
-void hsa_splice_wmemo_stats(uint64_t *hits, uint64_t *misses);
 long hsa_splice_run(const Idx2BWT *bi, struct bwt_array_t *arr, int max_len, int n_stacks, int n,
                     const hsa_splice_read_t *reads, bwt_aln1_t **out, int *n_out);
 

@@ -17,9 +17,9 @@
  * the reads' order does not change any result.
  *
  * The same object answers the splice path's bwt_cal_width calls (bwtaln.c:73, called at
- * bwtgap.c:807, :867-868, :871-872, :915) from a table the drop-in fills on the GPU
- * ahead of the splice path (hsa_splice_widths_prefetch): every width array those calls
- * can ask for, per fallback read and strand, keyed by (type, length, sequence).
+ * bwtgap.c:807, :867-868, :871-872, :915) from the per-read table the drop-in fills on
+ * the GPU ahead of the splice path (hsa_splice_prefetch, bwtgap_gpu.c): every width array
+ * those calls can ask for, per fallback read and strand.
  *
  * Its own object: a host opts in by linking bwtext_gpu.o and weakening its own
  * bwt_extend_backward / bwt_extend_foreward / bwt_cal_width.
@@ -169,7 +169,9 @@ static void run_reqs(hsa_index_t *ix, ext_req_t *const *q, int n)
     int32_t *ret = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
     int32_t *mp = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
     uint32_t *aln = (uint32_t *)malloc(sizeof(bwt_aln1_t) * (size_t)n);
+    hsa_gpu_lock();
     int rc = hsa_extend_batch(ix, rg, nr, jobs, n, codes, bids, tot, ret, mp, aln);
+    hsa_gpu_unlock();
     if (rc) hsa_gpu_fatal("GPU seed extension", rc);
     for (int j = 0; j < n; ++j) {
         memcpy(q[j]->aln, aln + 9 * (size_t)j, sizeof(bwt_aln1_t));
@@ -211,7 +213,9 @@ static int run_slices(hsa_index_t *ix, ext_req_t *const *q, const int32_t *slot,
     int32_t *ret = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
     int32_t *mp = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
     uint32_t *aln = (uint32_t *)malloc(sizeof(bwt_aln1_t) * (size_t)n);
+    hsa_gpu_lock();
     int rc = hsa_extend_sliced(ix, rg, nr, jobs, slot, res, n, codes, bids, tot, n_slots, SLICE_POPS, ret, mp, aln);
+    hsa_gpu_unlock();
     if (rc) hsa_gpu_fatal("GPU seed extension", rc);
     int nd = 0;
     for (int j = 0; j < n; ++j) {
@@ -274,130 +278,28 @@ int hsa_splice_extend_active(void)
     return resolved == hsa_own_extend_backward;
 }
 
-/* ------------------------------------------------------------ width table
- * bwt_cal_width(bi, len, str, width, type) depends on (type, len, str[0..len)) only
- * (and the index).  Type 1 writes entries 0..len, type 0 entries 1..len (bwtaln.c:85-115);
- * the table stores the written entries and the return value. */
-typedef struct {
-    uint64_t h;
-    uint8_t *key;            /* type, len, the sequence */
-    size_t key_len;
-    bwt_width_t *w;          /* entries 0..len (entry 0 unused for type 0) */
-    int len, type, ret;
-} wm_ent_t;
-
-static wm_ent_t *g_wm;
-static size_t g_wm_cap, g_wm_n;
-static uint64_t g_wm_hits, g_wm_misses;
-static pthread_rwlock_t g_wm_mu = PTHREAD_RWLOCK_INITIALIZER;
-static hsa_arena_t g_wm_arena;          /* keys and widths of the entries */
-
-static size_t wkey(int type, int len, const ubyte_t *str, uint8_t *buf)
-{
-    buf[0] = (uint8_t)type;
-    memcpy(buf + 1, &len, 4);
-    memcpy(buf + 5, str, (size_t)len);
-    return 5 + (size_t)len;
-}
-
-static uint64_t key_hash(const uint8_t *p, size_t n)
-{
-    /* 8 bytes per step (multiply-rotate), the tail byte by byte */
-    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
-    size_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-        uint64_t w;
-        memcpy(&w, p + i, 8);
-        h = (h ^ w) * 0xFF51AFD7ED558CCDull;
-        h ^= h >> 29;
-    }
-    for (; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
-    h ^= h >> 32;
-    return h | 1;                          /* 0 marks an empty slot */
-}
-
-static void wm_put(int type, int len, const ubyte_t *str, const uint32_t *w, int ret)   /* caller holds g_wm_mu */
-{
-    if (2 * (g_wm_n + 1) > g_wm_cap) {
-        size_t cap = g_wm_cap ? g_wm_cap * 2 : 4096;
-        wm_ent_t *t = (wm_ent_t *)calloc(cap, sizeof(wm_ent_t));
-        for (size_t i = 0; i < g_wm_cap; ++i) {
-            if (!g_wm[i].h) continue;
-            size_t j = g_wm[i].h & (cap - 1);
-            while (t[j].h) j = (j + 1) & (cap - 1);
-            t[j] = g_wm[i];
-        }
-        free(g_wm);
-        g_wm = t;
-        g_wm_cap = cap;
-    }
-    uint8_t *key = (uint8_t *)hsa_arena_alloc(&g_wm_arena, (size_t)len + 5);
-    const size_t kl = wkey(type, len, str, key);
-    const uint64_t h = key_hash(key, kl);
-    size_t j = h & (g_wm_cap - 1);
-    while (g_wm[j].h) {
-        if (g_wm[j].h == h && g_wm[j].key_len == kl && !memcmp(g_wm[j].key, key, kl)) return;
-        j = (j + 1) & (g_wm_cap - 1);
-    }
-    wm_ent_t *e = g_wm + j;
-    e->h = h; e->key = key; e->key_len = kl; e->len = len; e->type = type; e->ret = ret;
-    e->w = (bwt_width_t *)hsa_arena_alloc(&g_wm_arena, sizeof(bwt_width_t) * ((size_t)len + 1));
-    for (int i = 0; i <= len; ++i) { e->w[i].w = w[2 * i]; e->w[i].bid = (int)w[2 * i + 1]; }
-    ++g_wm_n;
-}
-
-void hsa_splice_wmemo_clear(void)
-{
-    pthread_rwlock_wrlock(&g_wm_mu);
-    hsa_arena_free(&g_wm_arena);
-    free(g_wm);
-    g_wm = NULL;
-    g_wm_cap = g_wm_n = 0;
-    pthread_rwlock_unlock(&g_wm_mu);
-}
-
-void hsa_splice_wmemo_stats(uint64_t *hits, uint64_t *misses)
-{
-    pthread_rwlock_wrlock(&g_wm_mu);
-    *hits = g_wm_hits; *misses = g_wm_misses;
-    g_wm_hits = g_wm_misses = 0;
-    pthread_rwlock_unlock(&g_wm_mu);
-}
+#pragma weak hsa_splice_set_read
+#pragma weak hsa_splice_table_width
+#pragma weak hsa_splice_table_sa
 
 /* bwt_cal_width on the GPU for n sequences of one type; w: 2 * (len + 1) words each */
 static void widths_gpu(hsa_index_t *ix, int type, int n, const uint64_t *offs, const uint32_t *lens,
                        const uint8_t *codes, size_t codes_len, uint32_t *w)
 {
+    hsa_gpu_lock();
     const int rc = type == 1 ? hsa_width_batch(ix, (size_t)n, offs, lens, codes, codes_len, w)
                              : hsa_width0_batch(ix, (size_t)n, offs, lens, codes, codes_len, w);
+    hsa_gpu_unlock();
     if (rc) hsa_gpu_fatal("GPU bwt_cal_width", rc);
 }
 
-/* bwt_cal_width (bwtaln.c:73-116): from the table, or one GPU call. */
+/* bwt_cal_width (bwtaln.c:73-116): from the splice table of the thread's read, or one
+ * GPU call. */
 int bwt_cal_width(const Idx2BWT *bi_bwt, int len, const ubyte_t *str, bwt_width_t *width, int type)
 {
     if (len < 0) len = 0;
-    uint8_t stackbuf[1024];
-    uint8_t *key = (size_t)len + 5 <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc((size_t)len + 5);
-    const size_t kl = wkey(type == 1, len, str, key);
-    const uint64_t h = key_hash(key, kl);
-    int found = 0, ret = 0;
-    pthread_rwlock_rdlock(&g_wm_mu);
-    if (g_wm_n)
-        for (size_t j = h & (g_wm_cap - 1); g_wm[j].h; j = (j + 1) & (g_wm_cap - 1))
-            if (g_wm[j].h == h && g_wm[j].key_len == kl && !memcmp(g_wm[j].key, key, kl)) {
-                const wm_ent_t *e = g_wm + j;
-                memcpy(width + (type == 1 ? 0 : 1), e->w + (type == 1 ? 0 : 1),
-                       sizeof(bwt_width_t) * (size_t)(type == 1 ? len + 1 : len));
-                ret = e->ret;
-                found = 1;
-                break;
-            }
-    if (found) __atomic_fetch_add(&g_wm_hits, 1, __ATOMIC_RELAXED);
-    else if (g_wm_n) __atomic_fetch_add(&g_wm_misses, 1, __ATOMIC_RELAXED);
-    pthread_rwlock_unlock(&g_wm_mu);
-    if (key != stackbuf) free(key);
-    if (found) return ret;
+    int ret = 0;
+    if (hsa_splice_table_width && hsa_splice_table_width(bi_bwt, len, str, width, type == 1, &ret)) return ret;
     uint64_t off = 0;
     uint32_t l32 = (uint32_t)len;
     uint32_t *w = (uint32_t *)calloc(2 * ((size_t)len + 1), sizeof(uint32_t));
@@ -416,79 +318,14 @@ int hsa_splice_width_active(void)
     return resolved == hsa_own_cal_width;
 }
 
-/* The widths bwt_splice_match can ask for, per fallback read (aux[r] as it receives
- * it) and strand s (seq_s: the read or its reverse complement, length L, seed length
- * sl = L / 3): type 1 of the prefixes of length sl and sl + L % 3 (the seed calls,
- * bwtgap.c:807), of the whole read and of its last 12 bases (:867/:871, :915), and type
- * 0 of the whole read (:868/:872).  Two GPU launches; the answers go to the table. */
-int hsa_splice_widths_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
-{
-    if (n <= 0) return 0;
-    const double t_start = hsa_now();
-    double t_gpu = 0.0;
-    hsa_index_t *ix = hsa_gpu_index_of(bi);
-    for (int type = 1; type >= 0; --type) {
-        const int per = type == 1 ? 4 : 1;
-        size_t nc = 0, nrow = 0;
-        for (int r = 0; r < n; ++r) {
-            const int L = aux[r]->len;
-            nrow += 2 * (size_t)per;
-            nc += 2 * (type == 1 ? (size_t)(2 * (L / 3) + L % 3 + L + (L >= 12 ? 12 : 0)) : (size_t)L);
-        }
-        uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * nrow);
-        uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * nrow);
-        const ubyte_t **src = (const ubyte_t **)malloc(sizeof(ubyte_t *) * nrow);
-        uint8_t *codes = (uint8_t *)malloc(nc + 1);
-        size_t co = 0, wo = 0, q = 0;
-        for (int r = 0; r < n; ++r) {
-            const int L = aux[r]->len, sl = L / 3;
-            for (int s = 0; s < 2; ++s) {
-                const ubyte_t *sq = s ? aux[r]->rc_seq : aux[r]->seq;
-                int rl[4], nr = 0;
-                const ubyte_t *rs[4];
-                if (type == 1) {
-                    rl[nr] = sl; rs[nr++] = sq;
-                    rl[nr] = sl + L % 3; rs[nr++] = sq;
-                    rl[nr] = L; rs[nr++] = sq;
-                    if (L >= 12) { rl[nr] = 12; rs[nr++] = sq + L - 12; }
-                } else {
-                    rl[nr] = L; rs[nr++] = sq;
-                }
-                for (int k = 0; k < nr; ++k) {
-                    offs[q] = co; lens[q] = (uint32_t)rl[k]; src[q] = rs[k];
-                    memcpy(codes + co, rs[k], (size_t)rl[k]);
-                    co += (size_t)rl[k];
-                    wo += 2 * ((size_t)rl[k] + 1);
-                    ++q;
-                }
-            }
-        }
-        uint32_t *w = (uint32_t *)calloc(wo + 2, sizeof(uint32_t));
-        const double tg = hsa_now();
-        widths_gpu(ix, type, (int)q, offs, lens, codes, co, w);
-        t_gpu += hsa_now() - tg;
-        pthread_rwlock_wrlock(&g_wm_mu);
-        size_t o = 0;
-        for (size_t j = 0; j < q; ++j) {
-            wm_put(type, (int)lens[j], src[j], w + o, (int)w[o + 2 * lens[j] + 1]);
-            o += 2 * ((size_t)lens[j] + 1);
-        }
-        pthread_rwlock_unlock(&g_wm_mu);
-        free(offs); free(lens); free(src); free(codes); free(w);
-    }
-    if (getenv("HSA_VERBOSE"))
-        fprintf(stderr, "[hsa] width prefetch: %.3f s (GPU %.3f s)\n", hsa_now() - t_start, t_gpu);
-    return 0;
-}
-
 /* ------------------------------------------------------------ SA -> position
  * The splice path's BWTRetrievePositionFromSAIndex calls (bwt_aln_corelate_check,
  * bwtgap.c:699, :712; check_site_by_intron_end, :615), redirected to
  * hsa_splice_sa_position by the host's link recipe (its bwtgap.o's reference renamed,
- * INTEGRATION.md; the SAM stage keeps the host's own).  Answers come from a table filled
- * on the GPU before the runner (the ranges the correlation reads of every prefetched
- * seed and anchor hit); a lookup the table misses parks its coroutine, and each round's
- * parked lookups are one GPU launch. */
+ * INTEGRATION.md; the SAM stage keeps the host's own).  Answers come from the read's
+ * splice table (the ranges the correlation reads of every prefetched seed and anchor hit,
+ * bwtgap_gpu.c), then from this table of the runner's earlier rounds; a lookup both miss
+ * parks its coroutine, and each round's parked lookups are one GPU launch. */
 typedef struct { uint32_t key, sid, ori, occ; } sa_ent_t;   /* key = sa index + 1 (0: empty) */
 static sa_ent_t *g_sa;
 static size_t g_sa_cap2, g_sa_n2;
@@ -541,31 +378,6 @@ static void sa_write(uint32_t occ, uint32_t sid, uint32_t ori, unsigned int *sid
     if (sid != 0xFFFFFFFFu) { *sid_p = sid; *ori_p = ori; }
 }
 
-/* GPU lookups of idx[0..n) into the table (duplicates and known ones skipped). */
-int hsa_splice_sa_prefetch(const Idx2BWT *bi, size_t n, const uint32_t *idx)
-{
-    if (n == 0) return 0;
-    const double t_start = hsa_now();
-    uint32_t *todo = (uint32_t *)malloc(sizeof(uint32_t) * n);
-    size_t m = 0;
-    pthread_rwlock_rdlock(&g_sa_mu);
-    for (size_t i = 0; i < n; ++i) if (!sa_get(idx[i])) todo[m++] = idx[i];
-    pthread_rwlock_unlock(&g_sa_mu);
-    if (m) {
-        uint32_t *o4 = (uint32_t *)malloc(sizeof(uint32_t) * 4 * m);
-        const int rc = hsa_sa_position_batch(hsa_gpu_index_of(bi), m, todo, o4);
-        if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
-        pthread_rwlock_wrlock(&g_sa_mu);
-        for (size_t i = 0; i < m; ++i) sa_put(todo[i], o4 + 4 * i);
-        pthread_rwlock_unlock(&g_sa_mu);
-        free(o4);
-    }
-    free(todo);
-    if (getenv("HSA_VERBOSE"))
-        fprintf(stderr, "[hsa] SA prefetch: %zu indices, %zu looked up, %.3f s\n", n, m, hsa_now() - t_start);
-    return 0;
-}
-
 void hsa_splice_sa_clear(void)
 {
     pthread_rwlock_wrlock(&g_sa_mu);
@@ -587,6 +399,11 @@ void hsa_splice_sa_stats(uint64_t *hits, uint64_t *misses)
 void hsa_splice_sa_position(Idx2BWT *bi, unsigned int sa_index, unsigned int *seq_id, unsigned int *ori_pos,
                             unsigned int *occ_pos)
 {
+    uint32_t o3[3];
+    if (hsa_splice_table_sa && hsa_splice_table_sa(bi, sa_index, o3)) {
+        sa_write(o3[0], o3[1], o3[2], seq_id, ori_pos, occ_pos);
+        return;
+    }
     pthread_rwlock_rdlock(&g_sa_mu);
     const sa_ent_t *e = sa_get(sa_index);
     sa_ent_t v = e ? *e : (sa_ent_t){0, 0, 0, 0};
@@ -605,7 +422,10 @@ void hsa_splice_sa_position(Idx2BWT *bi, unsigned int sa_index, unsigned int *se
     }
     const uint32_t one = sa_index;
     uint32_t o4[4];
-    const int rc = hsa_sa_position_batch(hsa_gpu_index_of(bi), 1, &one, o4);
+    hsa_index_t *ix = hsa_gpu_index_of(bi);
+    hsa_gpu_lock();
+    const int rc = hsa_sa_position_batch(ix, 1, &one, o4);
+    hsa_gpu_unlock();
     if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
     sa_write(o4[0], o4[1], o4[2], seq_id, ori_pos, occ_pos);
 }
@@ -770,11 +590,13 @@ static void worker_round(worker_t *w)
         co_t *c = w->co + k;
         while (c->read >= 0 && c->state == 0) {
             tl_co = c;
+            if (hsa_splice_set_read) hsa_splice_set_read(c->read);   /* its splice table entries */
             if (!_setjmp(w->sched)) {
                 if (!c->entered) { c->entered = 1; setcontext(&c->uc); }
                 _longjmp(c->jb, 1);
             }
             tl_co = NULL;
+            if (hsa_splice_set_read) hsa_splice_set_read(-1);
             if (c->state == 2) {
                 R->out[c->read] = c->result;
                 R->n_out[c->read] = c->n_aln;
@@ -804,7 +626,9 @@ static void leader_round(runner_t *R)
     if (live == 0) { R->done = 1; return; }
     if (nsa > 0) {                    /* the round's SA -> position lookups: one launch */
         const double ts = hsa_now();
+        hsa_gpu_lock();
         const int rc = hsa_sa_position_batch(R->ix, (size_t)nsa, R->sa_idx, R->sa_o4);
+        hsa_gpu_unlock();
         if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
         pthread_rwlock_wrlock(&g_sa_mu);
         for (int j = 0; j < nsa; ++j) {
@@ -879,12 +703,11 @@ static int runner_threads(int n)
 {
     const char *e = getenv("HSA_SPLICE_THREADS");
     int t = e ? atoi(e) : 0;
-    if (t <= 0) {
-        cpu_set_t cs;
-        CPU_ZERO(&cs);
-        t = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) : 1;
-        if (t > 16) t = 16;                 /* one GPU's share of a shared host */
-    }
+    if (t > 0) return t < n ? t : n;        /* as asked (tests: several threads on few reads) */
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    t = sched_getaffinity(0, sizeof cs, &cs) == 0 ? CPU_COUNT(&cs) : 1;
+    if (t > 16) t = 16;                     /* one GPU's share of a shared host */
     const int by_reads = (n + 63) / 64;     /* at least 64 reads a thread */
     if (t > by_reads) t = by_reads;
     return t < 1 ? 1 : t;

@@ -50,6 +50,7 @@ int bwt_match_gap_batch(bwt_aux_t *const *aux, int n, bwt_aln1_t **out, int *n_o
 {
     if (n <= 0) return 0;
     hsa_index_t *ix = hsa_gpu_index_of(aux[0]->bi_bwt);
+    hsa_gpu_lock();
     hsa_regime_t *rg = (hsa_regime_t *)malloc(sizeof(hsa_regime_t) * (size_t)n);
     int *gid = (int *)malloc(sizeof(int) * (size_t)n);
     int ng = 0;
@@ -125,378 +126,272 @@ int bwt_match_gap_batch(bwt_aux_t *const *aux, int n, bwt_aln1_t **out, int *n_o
         free(jobs); free(mg); free(map); free(codes); free(w); free(n_aln); free(hoff);
     }
     free(rg); free(gid);
+    hsa_gpu_unlock();
     return 0;
 }
 
 /* ------------------------------------------------------------ splice prefetch
- * bwt_splice_match (bwtgap.c:748) asks for its six seed searches one call at a time
- * (bwtgap.c:797-848), each a GPU round trip.  Which seeds it asks for depends on
- * earlier answers, but every seed it can ask for is known in advance: so
- * bwa_cal_sa_reg_gap runs all six of every fallback read in one batch first
- * (hsa_splice_prefetch) and bwt_match_gap answers from that table.  A table entry
- * is keyed by everything the search reads -- index, strand, length, sequence,
- * width_back (and an own width_seed), the width_seed kind, the option block and the
- * stack's bucket count -- and compared in full, so an answer from the table is the
- * answer the search would give.  Any other call (the 12-mer anchors, :919 and
- * :1192) misses and runs on its own. */
+ * bwt_splice_match (bwtgap.c:748) asks for its widths, seed searches, anchor searches and
+ * SA -> position lookups one call at a time, each a GPU round trip.  Which of them it
+ * asks for depends on earlier answers, but everything it can ask for before its first
+ * seed extension is determined by its read alone: bwa_cal_sa_reg_gap runs all of that for
+ * every fallback read of a batch in one device pass first (hsa_splice_prefetch ->
+ * hsa_splice_prefetch_batch, include/hsa_gpu.h) and the entry points answer from the
+ * result.  The table is per read: the runner (bwtext_gpu.c) and the serial loop
+ * (bwtaln_gpu.c) name the read a thread is working on (hsa_splice_set_read), and a call
+ * is answered only by that read's entries, after comparing every input of the call with
+ * the entry's -- options, strand, length, the sequence, widths, width_seed kind, the
+ * stack's bucket count -- so an answer from the table is the answer the call would
+ * compute.  Anything else (a call after an extension, another read's) is searched on its
+ * own.  The table is filled before the splice path starts and read-only while it runs: no
+ * locks. */
 typedef struct {
-    uint64_t h;
-    uint8_t *key;          /* the call's inputs, serialised */
-    size_t key_len;
-    int n_aln;
-    bwt_aln1_t *hits;
-    bwt_width_t *wout;     /* width_back after the search */
-    int len;
-} memo_ent_t;
+    int n, n_stacks;
+    hsa_splice_pf_t pf;            /* the device pass's outputs (pinned; valid until the next batch) */
+    const ubyte_t **seq;           /* per read: the read (strand 0) */
+    ubyte_t *rc;                   /* per read: its reverse complement (strand 1), at 2 * max_len * r */
+    int *len;
+    gap_opt_t *aopt;               /* per read: the anchors' options (bwtgap.c:777-782) */
+    gap_opt_t sopt;                /* the seed options without seed_len (bwtgap.c:769-774) */
+    const Idx2BWT *bi;
+} pf_tab_t;
 
-/* The table is process-global (the reference's host calls bwt_splice_match from one
- * thread, but the entry points may be called from several): every access holds
- * g_memo_mu, and a lookup copies its answer out before releasing it. */
-static memo_ent_t *g_memo;
-static size_t g_memo_cap, g_memo_n;
-static uint64_t g_memo_hits, g_memo_misses;
-static pthread_rwlock_t g_memo_mu = PTHREAD_RWLOCK_INITIALIZER;   /* lookups share it */
-static hsa_arena_t g_memo_arena;        /* keys, hits and widths of the entries */
+static pf_tab_t g_pf;
+static int g_pf_live;
+static __thread int tl_pf_read = -1;
+static uint64_t g_memo_hits, g_memo_misses, g_w_hits, g_w_misses, g_sa_hits, g_sa_misses;
 
-static size_t key_of(const bwt_aux_t *a, uint8_t *buf)
+/* The fallback read (prefetch order) the calling thread's bwt_splice_match works on, or -1. */
+void hsa_splice_set_read(int r) { tl_pf_read = r; }
+
+static const pf_tab_t *tab_of(const Idx2BWT *bi, int *r)
 {
-    const ubyte_t *seq = a->strand == 1 ? a->rc_seq : a->seq;
-    const int seed = !a->width_seed ? 0 : a->width_seed == a->width_back ? 2 : 1;
-    const int n_stacks = a->stack ? a->stack->n_stacks : -1;
-    size_t o = 0;
-#define PUT(p, n) do { if (buf) memcpy(buf + o, (p), (n)); o += (n); } while (0)
-    PUT(&a->bi_bwt, sizeof a->bi_bwt);
-    PUT(&a->strand, 4); PUT(&a->len, 4); PUT(&seed, 4); PUT(&n_stacks, 4);
-    PUT(a->opt, sizeof(gap_opt_t));
-    PUT(seq, (size_t)a->len);
-    PUT(a->width_back, sizeof(bwt_width_t) * ((size_t)a->len + 1));
-    if (seed == 1 && a->opt->seed_len >= 0) PUT(a->width_seed, sizeof(bwt_width_t) * ((size_t)a->opt->seed_len + 1));
-#undef PUT
-    return o;
+    *r = tl_pf_read;
+    if (!g_pf_live || *r < 0 || *r >= g_pf.n || bi != g_pf.bi) return NULL;
+    return &g_pf;
 }
 
-static uint64_t key_hash(const uint8_t *p, size_t n)
+static const ubyte_t *strand_seq(const pf_tab_t *t, int r, int s)
 {
-    /* 8 bytes per step (multiply-rotate), the tail byte by byte */
-    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
-    size_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-        uint64_t w;
-        memcpy(&w, p + i, 8);
-        h = (h ^ w) * 0xFF51AFD7ED558CCDull;
-        h ^= h >> 29;
+    return s ? t->rc + (size_t)2 * (size_t)t->pf.max_len * (size_t)r : t->seq[r];
+}
+
+static const int32_t *row_of(const pf_tab_t *t, int r, int j)
+{
+    return t->pf.rows + 2 * ((size_t)6 * (size_t)r + (size_t)j) * (size_t)t->pf.row_stride;
+}
+
+/* width_back[0..n] equals row[0..n) and then {0, bid of row[n - 1] + 1} (a prefix's widths) */
+static int same_prefix_widths(const bwt_width_t *w, const int32_t *row, int n)
+{
+    for (int i = 0; i < n; ++i)
+        if ((int32_t)w[i].w != row[2 * i] || w[i].bid != row[2 * i + 1]) return 0;
+    return w[n].w == 0 && w[n].bid == (n ? row[2 * (n - 1) + 1] : 0) + 1;
+}
+
+static int same_widths(const bwt_width_t *w, const int32_t *row, int n)
+{
+    for (int i = 0; i < n; ++i)
+        if ((int32_t)w[i].w != row[2 * i] || w[i].bid != row[2 * i + 1]) return 0;
+    return 1;
+}
+
+/* The table's answer to bwt_match_gap(aux), or NULL. */
+static bwt_aln1_t *table_match_gap(const bwt_aux_t *aux, int *n_out)
+{
+    int r;
+    const pf_tab_t *t = tab_of(aux->bi_bwt, &r);
+    if (!t || !aux->stack || aux->stack->n_stacks != t->n_stacks || (aux->strand != 0 && aux->strand != 1)) return NULL;
+    const int s = aux->strand, n = aux->len, L = t->len[r], sl = L / 3;
+    const ubyte_t *sq = s ? aux->rc_seq : aux->seq, *ss = strand_seq(t, r, s);
+    const int32_t *cn = t->pf.call_n + 8 * (size_t)r;
+    int call = -1;
+    if (aux->width_seed == aux->width_back) {                 /* a seed (bwtgap.c:797-812) */
+        for (int tt = 0; tt < 3 && call < 0; ++tt) {
+            const int la = sl + (tt == 2 ? L % 3 : 0), c = 3 * s + tt;
+            if (la != n || cn[c] < 0 || memcmp(sq, ss + tt * sl, (size_t)n)) continue;
+            gap_opt_t o = t->sopt;
+            o.seed_len = la;
+            if (memcmp(aux->opt, &o, sizeof o) || !same_prefix_widths(aux->width_back, row_of(t, r, s), la)) continue;
+            call = c;
+        }
+    } else if (!aux->width_seed && n == 12 && cn[6 + s] >= 0) {     /* an anchor (bwtgap.c:911-919, :1187-1192) */
+        const int tail = cn[3 * s] > 0 && cn[3 * s + 1] > 0;           /* pattern 3: the last 12 bases */
+        if (!memcmp(sq, ss + (tail ? L - 12 : 0), 12) && !memcmp(aux->opt, t->aopt + r, sizeof(gap_opt_t)) &&
+            same_widths(aux->width_back, row_of(t, r, tail ? 2 + s : s), 13))
+            call = 6 + s;
     }
-    for (; i < n; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
-    h ^= h >> 32;
-    return h | 1;                          /* 0 marks an empty slot */
+    if (call < 0) return NULL;
+    const size_t c = 8 * (size_t)r + (size_t)call;
+    const int na = t->pf.call_n[c];
+    bwt_aln1_t *out = (bwt_aln1_t *)calloc((size_t)aln_capacity(na), sizeof(bwt_aln1_t));
+    if (na > 0) memcpy(out, t->pf.hits + 9 * t->pf.call_hit[c], sizeof(bwt_aln1_t) * (size_t)na);
+    memcpy(aux->width_back, t->pf.wafter + 2 * c * (size_t)t->pf.cw_stride, sizeof(bwt_width_t) * ((size_t)n + 1));
+    *n_out = na;
+    return out;
+}
+
+/* bwt_cal_width (bwtaln.c:73-116) from the calling thread's read's rows: type 1 of any
+ * prefix of either strand, or of its last 12 bases; type 0 of the whole strand.  Returns
+ * 1 with width and *ret written, 0 when the table does not hold it. */
+int hsa_splice_table_width(const Idx2BWT *bi, int len, const ubyte_t *str, bwt_width_t *width, int type, int *ret)
+{
+    int r;
+    const pf_tab_t *t = tab_of(bi, &r);
+    if (!t || len < 0) return 0;
+    const int L = t->len[r];
+    for (int s = 0; s < 2; ++s) {
+        const ubyte_t *ss = strand_seq(t, r, s);
+        if (type == 1 && len <= L && !memcmp(str, ss, (size_t)len)) {
+            const int32_t *row = row_of(t, r, s);
+            for (int i = 0; i < len; ++i) { width[i].w = (bwtint_t)row[2 * i]; width[i].bid = row[2 * i + 1]; }
+            width[len].w = 0;
+            width[len].bid = (len ? row[2 * (len - 1) + 1] : 0) + 1;
+            *ret = width[len].bid;
+            __atomic_fetch_add(&g_w_hits, 1, __ATOMIC_RELAXED);
+            return 1;
+        }
+        if ((type == 1 && len == 12 && L >= 12 && !memcmp(str, ss + L - 12, 12)) ||
+            (type != 1 && len == L && !memcmp(str, ss, (size_t)len))) {
+            const int32_t *row = row_of(t, r, type == 1 ? 2 + s : 4 + s);
+            for (int i = type == 1 ? 0 : 1; i <= len; ++i) { width[i].w = (bwtint_t)row[2 * i]; width[i].bid = row[2 * i + 1]; }
+            *ret = width[len].bid;
+            __atomic_fetch_add(&g_w_hits, 1, __ATOMIC_RELAXED);
+            return 1;
+        }
+    }
+    __atomic_fetch_add(&g_w_misses, 1, __ATOMIC_RELAXED);
+    return 0;
+}
+
+/* SA index -> (occ, seq id, 1-based position) for the calling thread's read: the lookups
+ * bwt_aln_corelate_check makes on its seed and anchor hits (bwtgap.c:698, :711).
+ * Returns 1 with o[0..2] = occ, sid, ori, else 0. */
+int hsa_splice_table_sa(const Idx2BWT *bi, uint32_t idx, uint32_t o[3])
+{
+    int r;
+    const pf_tab_t *t = tab_of(bi, &r);
+    if (!t || !t->pf.call_sa) return 0;
+    for (int c = 0; c < 8; ++c) {
+        const size_t cc = 8 * (size_t)r + (size_t)c;
+        const int na = t->pf.call_n[cc];
+        if (na <= 0) continue;
+        const uint32_t *h = t->pf.hits + 9 * t->pf.call_hit[cc];
+        uint64_t cur = t->pf.call_sa[cc];
+        for (int x = 0; x < na; ++x) {
+            const uint32_t k = h[9 * x + 1], l = h[9 * x + 2], lim = k + 50u;
+            const uint32_t span = (k > l || lim < k) ? 0u : (l < lim - 1u ? l : lim - 1u) - k + 1u;
+            if (idx >= k && idx - k < span) {
+                const uint32_t *v = t->pf.sa + 4 * (cur + (idx - k));
+                o[0] = v[0]; o[1] = v[1]; o[2] = v[2];
+                __atomic_fetch_add(&g_sa_hits, 1, __ATOMIC_RELAXED);
+                return 1;
+            }
+            cur += span;
+        }
+    }
+    __atomic_fetch_add(&g_sa_misses, 1, __ATOMIC_RELAXED);
+    return 0;
 }
 
 void hsa_splice_memo_clear(void)
 {
-    pthread_rwlock_wrlock(&g_memo_mu);
-    hsa_arena_free(&g_memo_arena);
-    free(g_memo);
-    g_memo = NULL;
-    g_memo_cap = g_memo_n = 0;
-    pthread_rwlock_unlock(&g_memo_mu);
+    g_pf_live = 0;
+    free(g_pf.seq); free(g_pf.rc); free(g_pf.len); free(g_pf.aopt);
+    memset(&g_pf, 0, sizeof g_pf);
 }
 
-static void memo_put(const bwt_aux_t *in, const bwt_width_t *wout, const bwt_aln1_t *hits, int n_aln)
-{
-    if (2 * (g_memo_n + 1) > g_memo_cap) {     /* grow: open addressing at <= 1/2 load */
-        size_t cap = g_memo_cap ? g_memo_cap * 2 : 1024;
-        memo_ent_t *t = (memo_ent_t *)calloc(cap, sizeof(memo_ent_t));
-        for (size_t i = 0; i < g_memo_cap; ++i) {
-            if (!g_memo[i].h) continue;
-            size_t j = g_memo[i].h & (cap - 1);
-            while (t[j].h) j = (j + 1) & (cap - 1);
-            t[j] = g_memo[i];
-        }
-        free(g_memo);
-        g_memo = t;
-        g_memo_cap = cap;
-    }
-    const size_t kl = key_of(in, NULL);
-    uint8_t *key = (uint8_t *)hsa_arena_alloc(&g_memo_arena, kl);
-    key_of(in, key);
-    const uint64_t h = key_hash(key, kl);
-    size_t j = h & (g_memo_cap - 1);
-    while (g_memo[j].h) {
-        if (g_memo[j].h == h && g_memo[j].key_len == kl && !memcmp(g_memo[j].key, key, kl)) return;
-        j = (j + 1) & (g_memo_cap - 1);
-    }
-    memo_ent_t *e = g_memo + j;
-    e->h = h; e->key = key; e->key_len = kl; e->n_aln = n_aln; e->len = in->len;
-    e->hits = (bwt_aln1_t *)hsa_arena_alloc(&g_memo_arena, sizeof(bwt_aln1_t) * (size_t)(n_aln > 0 ? n_aln : 1));
-    if (n_aln > 0) memcpy(e->hits, hits, sizeof(bwt_aln1_t) * (size_t)n_aln);
-    e->wout = (bwt_width_t *)hsa_arena_alloc(&g_memo_arena, sizeof(bwt_width_t) * ((size_t)in->len + 1));
-    memcpy(e->wout, wout, sizeof(bwt_width_t) * ((size_t)in->len + 1));
-    ++g_memo_n;
-}
-
-static const memo_ent_t *memo_get(const bwt_aux_t *a)
-{
-    if (!g_memo_n) return NULL;
-    const size_t kl = key_of(a, NULL);
-    uint8_t stackbuf[4096];
-    uint8_t *key = kl <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc(kl);
-    key_of(a, key);
-    const uint64_t h = key_hash(key, kl);
-    const memo_ent_t *hit = NULL;
-    for (size_t j = h & (g_memo_cap - 1); g_memo[j].h; j = (j + 1) & (g_memo_cap - 1))
-        if (g_memo[j].h == h && g_memo[j].key_len == kl && !memcmp(g_memo[j].key, key, kl)) { hit = g_memo + j; break; }
-    if (key != stackbuf) free(key);
-    return hit;
-}
-
-/* The SA indices the splice path's correlation can look up for the prefetched hits
- * (bwt_aln_corelate_check, bwtgap.c:698 and :711: k .. min(l, k + 49) of each hit),
- * collected for the SA -> position prefetch (hsa_splice_take_sa_list). */
-static uint32_t *g_sa_list;
-static size_t g_sa_n, g_sa_cap;
-
-static void sa_list_add(const bwt_aln1_t *h, int n)     /* caller holds g_memo_mu */
-{
-    for (int x = 0; x < n; ++x)
-        for (uint64_t j = h[x].k; j <= h[x].l && j < (uint64_t)h[x].k + 50; ++j) {
-            if (g_sa_n == g_sa_cap) {
-                g_sa_cap = g_sa_cap ? 2 * g_sa_cap : 4096;
-                g_sa_list = (uint32_t *)realloc(g_sa_list, sizeof(uint32_t) * g_sa_cap);
-            }
-            g_sa_list[g_sa_n++] = (uint32_t)j;
-        }
-}
-
-/* The collected SA indices (ownership passes to the caller, who frees them). */
-size_t hsa_splice_take_sa_list(uint32_t **idx)
-{
-    pthread_rwlock_wrlock(&g_memo_mu);
-    *idx = g_sa_list;
-    const size_t n = g_sa_n;
-    g_sa_list = NULL;
-    g_sa_n = g_sa_cap = 0;
-    pthread_rwlock_unlock(&g_memo_mu);
-    return n;
-}
-
-/* Search calls[0..c) in one batch (bwt_match_gap_batch) and put every answer in the
- * table, keyed by the call's inputs: win[i] holds its width_back as it was before the
- * search (calls[i].width_back is a scratch copy the search rewrites; a width_seed
- * aliased to it is re-aliased to win[i]).  n_out[i] receives the hit counts. */
-static double g_t_search, g_t_put;   /* prefetch timing (HSA_VERBOSE) */
-
-static void batch_into_memo(bwt_aux_t *calls, int c, bwt_width_t **win, int *n_out)
-{
-    if (c <= 0) return;
-    bwt_aux_t **cp = (bwt_aux_t **)calloc((size_t)c, sizeof(bwt_aux_t *));
-    bwt_aln1_t **out = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)c);
-    for (int i = 0; i < c; ++i) cp[i] = calls + i;
-    const double t0 = hsa_now();
-    bwt_match_gap_batch(cp, c, out, n_out);
-    const double t1 = hsa_now();
-    g_t_search += t1 - t0;
-    pthread_rwlock_wrlock(&g_memo_mu);
-    for (int i = 0; i < c; ++i) {
-        bwt_width_t *after = calls[i].width_back;
-        const int alias = calls[i].width_seed == after;
-        calls[i].width_back = win[i];
-        if (alias) calls[i].width_seed = win[i];
-        memo_put(calls + i, after, out[i], n_out[i]);
-        sa_list_add(out[i], n_out[i]);
-        free(after); free(out[i]);
-    }
-    pthread_rwlock_unlock(&g_memo_mu);
-    g_t_put += hsa_now() - t1;
-    free(cp); free(out);
-}
-
-/* One call of the batch: aux[r] copied as bwt_splice_match copies it (bwtgap.c:756-759),
- * with its own option block, strand, length, and a scratch width_back initialised from
- * w (n + 1 pairs, kept in win). */
-static bwt_aux_t *add_call(bwt_aux_t *calls, gap_opt_t *opts, bwt_width_t **win, int c, const bwt_aux_t *a,
-                           const gap_opt_t *o, int strand, int len, const uint32_t *w)
-{
-    bwt_aux_t *x = calls + c;
-    *x = *a;
-    opts[c] = *o;
-    x->opt = opts + c;
-    x->len = len;
-    x->strand = strand;
-    win[c] = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)len + 1));
-    memcpy(win[c], w, sizeof(bwt_width_t) * ((size_t)len + 1));
-    x->width_back = (bwt_width_t *)malloc(sizeof(bwt_width_t) * ((size_t)len + 1));
-    memcpy(x->width_back, win[c], sizeof(bwt_width_t) * ((size_t)len + 1));
-    x->width_seed = NULL;
-    return x;
-}
-
-#define ANCHOR 12   /* the anchor length of bwtgap.c:911 and :1187 */
-
-/* The splice path's searches of each read bwt_splice_match will be called on, run on the
- * GPU as two batches before the host asks for them; aux[r] as bwt_splice_match receives
- * it (seq, rc_seq, len, opt = local_opt of that read, stack).
- *  1. The six seed searches (bwtgap.c:762-812): widths of the strand prefixes
- *     (bwt_cal_width type 1, as :807 computes them), width_seed aliased to width_back.
- *  2. The 12-mer anchor searches made after an extension succeeds (options of aux_ext:
- *     max_gape 3, :782; width_seed NULL):
- *       - seeds 0 and 1 of a strand map and seed 2 does not (seg_mtype 3): the strand's
- *         last 12 bases with their own widths (:911-919);
- *       - seeds 1 and 2 map and seed 0 does not (seg_mtype 6): its first 12 bases with
- *         the whole read's widths (:867/:871, :1187-1192), i.e. the first 13 width
- *         entries of the prefix of length 13.
- *     Whether the host reaches them depends on the seed correlation and the
- *     backtracking, so the anchor of every strand whose seed pattern leads there is
- *     searched: one small search per such strand, where the host would otherwise make a
- *     GPU round trip per call. */
+/* The prefetch for reads aux[0..n) as bwt_splice_match receives them (seq, rc_seq, len,
+ * opt = local_opt of that read, stack with the batch's n_stacks), in the order the splice
+ * path will run them (hsa_splice_set_read's numbering). */
 int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
 {
+    hsa_splice_memo_clear();
     if (n <= 0) return 0;
     const double t_start = hsa_now();
-    g_t_search = g_t_put = 0.0;
     hsa_index_t *ix = hsa_gpu_index_of(bi);
-    /* widths: per read, strand s, the prefix of seed_len and of seed_len + len % 3 */
-    int nw = 0;
-    size_t wcodes = 0;
+    const gap_opt_t *o0 = aux[0]->opt;
+    const int n_stacks = aux[0]->stack ? aux[0]->stack->n_stacks
+                                       : hsa_aln_score(o0, o0->max_diff + 1, o0->max_gapo + 1, o0->max_gape + 1);
+    int max_len = 0, ok = 1;
+    size_t tot = 0;
     for (int r = 0; r < n; ++r) {
-        const int L = aux[r]->len, sl = L / 3;
-        if (sl < 1) continue;
-        nw += 4;
-        wcodes += 4 * (size_t)sl + 2 * (size_t)(L % 3);
+        const gap_opt_t *o = aux[r]->opt;
+        /* one seed and one anchor regime: every read's options but max_diff / seed_len equal */
+        gap_opt_t a = *o, b = *o0;
+        a.max_diff = b.max_diff = 0; a.seed_len = b.seed_len = 0;
+        if (memcmp(&a, &b, sizeof a) || aux[r]->len < 3 || aux[r]->len > 3 * 1021 ||
+            (aux[r]->stack && aux[r]->stack->n_stacks != n_stacks))
+            ok = 0;
+        if (aux[r]->len > max_len) max_len = aux[r]->len;
+        tot += (size_t)aux[r]->len;
     }
-    if (nw == 0) return 0;
-    uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)nw);
-    uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)nw);
-    size_t *woff = (size_t *)malloc(sizeof(size_t) * (size_t)nw);
-    uint8_t *codes = (uint8_t *)malloc(wcodes + 1);
-    size_t co = 0, wo = 0;
-    int q = 0;
-    for (int r = 0; r < n; ++r) {
-        const int L = aux[r]->len, sl = L / 3;
-        if (sl < 1) continue;
-        for (int s = 0; s < 2; ++s)
-            for (int k = 0; k < 2; ++k) {
-                const int la = sl + (k ? L % 3 : 0);
-                offs[q] = co; lens[q] = (uint32_t)la; woff[q] = wo;
-                memcpy(codes + co, s ? aux[r]->rc_seq : aux[r]->seq, (size_t)la);
-                co += (size_t)la;
-                wo += 2 * ((size_t)la + 1);
-                ++q;
-            }
-    }
-    uint32_t *wout = (uint32_t *)malloc(sizeof(uint32_t) * (wo + 2));
-    int rc = hsa_width_batch(ix, (size_t)nw, offs, lens, codes, co, wout);
-    if (rc) hsa_gpu_fatal("GPU bwt_cal_width", rc);
-    /* the seed calls, set up as bwtgap.c:797-810 sets up aux_seed */
-    const int nc = 6 * (nw / 4);
-    bwt_aux_t *calls = (bwt_aux_t *)calloc((size_t)nc, sizeof(bwt_aux_t));
-    gap_opt_t *opts = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nc);
-    bwt_width_t **win = (bwt_width_t **)malloc(sizeof(bwt_width_t *) * (size_t)nc);
-    int *n_out = (int *)malloc(sizeof(int) * (size_t)nc);
-    int c = 0, w = 0;
+    if (!ok) return 0;                     /* no table: every call of the splice path runs on its own */
+    pf_tab_t *t = &g_pf;
+    t->n = n; t->n_stacks = n_stacks; t->bi = bi;
+    t->seq = (const ubyte_t **)malloc(sizeof(ubyte_t *) * (size_t)n);
+    t->rc = (ubyte_t *)malloc((size_t)2 * (size_t)max_len * (size_t)n + 16);
+    t->len = (int *)malloc(sizeof(int) * (size_t)n);
+    t->aopt = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)n);
+    uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)n);
+    uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)n);
+    int32_t *amd = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+    uint8_t *codes = (uint8_t *)malloc(tot + 1);
+    size_t co = 0;
+    int amd_max = 0;
     for (int r = 0; r < n; ++r) {
         const bwt_aux_t *a = aux[r];
-        const int L = a->len, sl = L / 3;
-        if (sl < 1) continue;
-        gap_opt_t so = *a->opt;                                 /* :769-774 */
-        so.mode &= ~BWA_MODE_GAPE;
-        so.max_gapo = 0;
-        so.max_gape = 0;
-        so.max_diff = a->opt->max_seed_diff;
-        for (int i = 0; i < 6; ++i) {
-            const int s = i / 3, la = sl + (i % 3 == 2 ? L % 3 : 0);
-            so.seed_len = la;                                   /* :802 */
-            const uint32_t *wk = wout + woff[w + 2 * s + (i % 3 == 2 && L % 3 ? 1 : 0)];
-            bwt_aux_t *x = add_call(calls, opts, win, c, a, &so, s, la, wk);
-            if (s) x->rc_seq = a->rc_seq + (i % 3) * sl;       /* :805-806 */
-            else x->seq = a->seq + (i % 3) * sl;
-            x->width_seed = x->width_back;                      /* :804-809 */
-            ++c;
-        }
-        w += 4;
+        const int L = a->len;
+        t->seq[r] = a->seq; t->len[r] = L;
+        ubyte_t *rc = t->rc + (size_t)2 * (size_t)max_len * (size_t)r;
+        for (int j = 0; j < L; ++j) { const ubyte_t c = a->seq[L - 1 - j]; rc[j] = c < 4 ? (ubyte_t)(3 - c) : c; }
+        t->aopt[r] = *a->opt;
+        t->aopt[r].max_gape = 3;                                /* aux_ext (bwtgap.c:777-782) */
+        lens[r] = (uint32_t)L; offs[r] = co; amd[r] = a->opt->max_diff;
+        amd_max = amd[r] > amd_max ? amd[r] : amd_max;
+        memcpy(codes + co, a->seq, (size_t)L);
+        co += (size_t)L;
     }
-    batch_into_memo(calls, c, win, n_out);
-
-    /* the anchors of the strands whose seed pattern is 3 or 6 */
-    int na = 0;
-    size_t acodes = 0;
-    for (int r = 0, rr = 0; r < n; ++r) {
-        const int L = aux[r]->len;
-        if (L / 3 < 1) continue;
-        for (int s = 0; s < 2 && L > ANCHOR; ++s) {
-            const int *no = n_out + 6 * rr + 3 * s;
-            const int mask = (no[0] > 0) | (no[1] > 0) << 1 | (no[2] > 0) << 2;
-            if (mask == 3) { ++na; acodes += ANCHOR; }
-            if (mask == 6) { ++na; acodes += ANCHOR + 1; }
-        }
-        ++rr;
+    t->pf.max_len = max_len;
+    t->sopt = *o0;                                              /* aux_seed (bwtgap.c:769-774) */
+    t->sopt.mode &= ~BWA_MODE_GAPE;
+    t->sopt.max_gapo = 0;
+    t->sopt.max_gape = 0;
+    t->sopt.max_diff = o0->max_seed_diff;
+    gap_opt_t ao = t->aopt[0];
+    const hsa_regime_t srg = hsa_regime_of(&t->sopt, n_stacks, t->sopt.max_diff);
+    const hsa_regime_t arg = hsa_regime_of(&ao, n_stacks, amd_max);
+    hsa_gpu_lock();
+    const int rc = hsa_splice_prefetch_batch(ix, &srg, &arg, n, lens, offs, codes, co, amd, &t->pf);
+    hsa_gpu_unlock();
+    free(lens); free(offs); free(amd); free(codes);
+    if (rc == HSA_E_ARG) {             /* options or reads outside the device pass: no table */
+        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] splice prefetch skipped: %s\n", hsa_last_error());
+        hsa_splice_memo_clear();
+        return 0;
     }
-    if (na > 0) {
-        uint64_t *ao = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)na);
-        uint32_t *al = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)na);
-        uint8_t *ac = (uint8_t *)malloc(acodes + 1);
-        int *ar = (int *)malloc(sizeof(int) * (size_t)na);     /* read, strand, kind */
-        size_t aco = 0, awo = 0;
-        int k = 0;
-        for (int r = 0, rr = 0; r < n; ++r) {
-            const bwt_aux_t *a = aux[r];
-            const int L = a->len;
-            if (L / 3 < 1) continue;
-            for (int s = 0; s < 2 && L > ANCHOR; ++s) {
-                const int *no = n_out + 6 * rr + 3 * s;
-                const int mask = (no[0] > 0) | (no[1] > 0) << 1 | (no[2] > 0) << 2;
-                if (mask != 3 && mask != 6) continue;
-                const ubyte_t *sq = s ? a->rc_seq : a->seq;
-                const int tail = mask == 3;
-                al[k] = tail ? ANCHOR : ANCHOR + 1;
-                ao[k] = aco;
-                memcpy(ac + aco, tail ? sq + L - ANCHOR : sq, al[k]);
-                aco += al[k];
-                awo += 2 * ((size_t)al[k] + 1);
-                ar[k] = r << 2 | s << 1 | tail;
-                ++k;
-            }
-            ++rr;
-        }
-        uint32_t *aw = (uint32_t *)malloc(sizeof(uint32_t) * (awo + 2));
-        rc = hsa_width_batch(ix, (size_t)na, ao, al, ac, aco, aw);
-        if (rc) hsa_gpu_fatal("GPU bwt_cal_width", rc);
-        bwt_aux_t *acalls = (bwt_aux_t *)calloc((size_t)na, sizeof(bwt_aux_t));
-        gap_opt_t *aopts = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)na);
-        bwt_width_t **awin = (bwt_width_t **)malloc(sizeof(bwt_width_t *) * (size_t)na);
-        int *an = (int *)malloc(sizeof(int) * (size_t)na);
-        size_t wp = 0;
-        for (int j = 0; j < na; ++j) {
-            const bwt_aux_t *a = aux[ar[j] >> 2];
-            const int s = (ar[j] >> 1) & 1, tail = ar[j] & 1, L = a->len;
-            gap_opt_t eo = *a->opt;
-            eo.max_gape = 3;                                    /* aux_ext (:777-782) */
-            bwt_aux_t *x = add_call(acalls, aopts, awin, j, a, &eo, s, ANCHOR, aw + wp);
-            if (tail) {                                         /* :912 */
-                if (s) x->rc_seq = a->rc_seq + L - ANCHOR;
-                else x->seq = a->seq + L - ANCHOR;
-            }
-            wp += 2 * ((size_t)al[j] + 1);
-        }
-        batch_into_memo(acalls, na, awin, an);
-        for (int j = 0; j < na; ++j) free(awin[j]);
-        free(ao); free(al); free(ac); free(ar); free(aw); free(acalls); free(aopts); free(awin); free(an);
-    }
-    for (int i = 0; i < c; ++i) free(win[i]);
-    free(offs); free(lens); free(woff); free(codes); free(wout);
-    free(calls); free(opts); free(win); free(n_out);
+    if (rc) hsa_gpu_fatal("GPU splice prefetch", rc);
+    g_pf_live = 1;
     if (getenv("HSA_VERBOSE"))
-        fprintf(stderr, "[hsa] seed/anchor prefetch: %.3f s (GPU searches %.3f s, table %.3f s, the rest: set-up and "
-                        "widths)\n", hsa_now() - t_start, g_t_search, g_t_put);
+        fprintf(stderr, "[hsa] splice prefetch: %d reads, %.3f s (device pass %.1f ms of kernels)\n", n,
+                hsa_now() - t_start, t->pf.kernel_ms);
     return 0;
 }
 
-/* Table statistics since the last call (hits, misses), for logs. */
+/* Table statistics since the last call (hits, misses), for logs: bwt_match_gap, then
+ * bwt_cal_width and SA -> position (hsa_splice_table_stats). */
 void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses)
 {
-    pthread_rwlock_wrlock(&g_memo_mu);
-    *hits = g_memo_hits; *misses = g_memo_misses;
-    g_memo_hits = g_memo_misses = 0;
-    pthread_rwlock_unlock(&g_memo_mu);
+    *hits = __atomic_exchange_n(&g_memo_hits, 0, __ATOMIC_RELAXED);
+    *misses = __atomic_exchange_n(&g_memo_misses, 0, __ATOMIC_RELAXED);
+}
+
+void hsa_splice_table_stats(uint64_t *w_hits, uint64_t *w_misses, uint64_t *sa_hits, uint64_t *sa_misses)
+{
+    *w_hits = __atomic_exchange_n(&g_w_hits, 0, __ATOMIC_RELAXED);
+    *w_misses = __atomic_exchange_n(&g_w_misses, 0, __ATOMIC_RELAXED);
+    *sa_hits = __atomic_exchange_n(&g_sa_hits, 0, __ATOMIC_RELAXED);
+    *sa_misses = __atomic_exchange_n(&g_sa_misses, 0, __ATOMIC_RELAXED);
 }
 
 /* bwt_match_gap (bwtgap.c:118, declared bwtgap.h:26): the reference's entry point,
@@ -504,20 +399,12 @@ void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses)
  * Same return contract: a calloc'd array, never NULL, freed by the caller. */
 bwt_aln1_t *bwt_match_gap(bwt_aux_t *aux, int *_n_aln)
 {
-    pthread_rwlock_rdlock(&g_memo_mu);
-    const memo_ent_t *e = memo_get(aux);
-    if (e) {
+    bwt_aln1_t *out = table_match_gap(aux, _n_aln);
+    if (out) {
         __atomic_fetch_add(&g_memo_hits, 1, __ATOMIC_RELAXED);
-        bwt_aln1_t *out = (bwt_aln1_t *)calloc((size_t)aln_capacity(e->n_aln), sizeof(bwt_aln1_t));
-        if (e->n_aln > 0) memcpy(out, e->hits, sizeof(bwt_aln1_t) * (size_t)e->n_aln);
-        memcpy(aux->width_back, e->wout, sizeof(bwt_width_t) * ((size_t)e->len + 1));
-        *_n_aln = e->n_aln;
-        pthread_rwlock_unlock(&g_memo_mu);
         return out;
     }
-    if (g_memo_n) __atomic_fetch_add(&g_memo_misses, 1, __ATOMIC_RELAXED);
-    pthread_rwlock_unlock(&g_memo_mu);
-    bwt_aln1_t *out = NULL;
+    if (g_pf_live) __atomic_fetch_add(&g_memo_misses, 1, __ATOMIC_RELAXED);
     bwt_match_gap_batch(&aux, 1, &out, _n_aln);
     return out;
 }

@@ -66,7 +66,10 @@ void bwa_cal_pac_pos(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seq, int max_
         for (int j = 0; j < p->n_multi; ++j) idx[q++] = p->multi[j].sa;
     }
     if (n > 0) {
-        const int rc = hsa_sa_position_batch(hsa_gpu_index_of(bi_bwt), n, idx, res);
+        hsa_index_t *ix = hsa_gpu_index_of(bi_bwt);
+        hsa_gpu_lock();
+        const int rc = hsa_sa_position_batch(ix, n, idx, res);
+        hsa_gpu_unlock();
         if (rc) hsa_gpu_fatal("GPU SA -> position", rc);
     }
     q = 0;

@@ -258,10 +258,17 @@ static int build_tries_t(hsa_index *ix, RD fwd, RD rev, IT T, const IT *C)
     if (D == 0) return 0;
     const size_t es = sizeof(IT) == 4 ? 16 : 32, ws = sizeof(IT) == 4 ? 8 : 16;
     const size_t nw = trie_base(D + 1), ns = Ds ? trie_base(Ds + 1) : 0;
-    HSA_HIP(hipMalloc(&ix->d_trie_w, nw * ws));
-    if (Ds) {
-        HSA_HIP(hipMalloc(&ix->d_trie_s, ns * es));
-        HSA_HIP(hipMalloc(&ix->d_trie_m, trie_mbase(Ds) + 16));
+    // the tries only save rank steps: without the memory for them the index still serves
+    // every search (rank steps only), so an allocation failure is not an error here
+    const bool got = hipMalloc(&ix->d_trie_w, nw * ws) == hipSuccess &&
+                     (!Ds || (hipMalloc(&ix->d_trie_s, ns * es) == hipSuccess &&
+                              hipMalloc(&ix->d_trie_m, trie_mbase(Ds) + 16) == hipSuccess));
+    if (!got) {
+        (void)hipGetLastError();
+        (void)hipFree(ix->d_trie_w); (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m);
+        ix->d_trie_w = nullptr; ix->d_trie_s = nullptr; ix->d_trie_m = nullptr;
+        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] root tries: no device memory for them, rank steps only\n");
+        return 0;
     }
     TrieC<IT> Cv;
     for (int c = 0; c < 4; ++c) Cv.v[c] = C[c];
@@ -445,9 +452,16 @@ int hsa_need_unshared(const hsa_index *ix, const char *what)
 extern "C" void hsa_index_free(hsa_index_t *ix)
 {
     if (!ix) return;
+    if (!ix->parent && ix->n_clones > 0) {
+        // live clones still read the shared arrays: the free is deferred to the last
+        // clone's (the handle stays valid for them, not for the caller)
+        ix->free_pending = true;
+        return;
+    }
     (void)hipSetDevice(ix->device);
+    hsa_index *orphan = nullptr;
     if (ix->parent) {           // the shared arrays stay with the parent
-        --ix->parent->n_clones;
+        if (--ix->parent->n_clones == 0 && ix->parent->free_pending) orphan = ix->parent;
         ix->blk_base[0] = ix->blk_base[1] = nullptr;
         ix->d_sa = ix->d_blocks = nullptr;
         ix->d_wsa = ix->d_wisa = ix->d_wtext = nullptr;
@@ -460,6 +474,9 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (ix->d_any_aux) (void)hipFree(ix->d_any_aux);
     if (ix->d_split) (void)hipFree(ix->d_split);
     if (ix->d_fwd) (void)hipFree(ix->d_fwd);
+    if (ix->d_pf) (void)hipFree(ix->d_pf);
+    if (ix->d_pf2) (void)hipFree(ix->d_pf2);
+    if (ix->h_pf) (void)hipHostFree(ix->h_pf);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
     (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
     (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m); (void)hipFree(ix->d_trie_w);
@@ -472,6 +489,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
             if (ix->pev[i][j]) (void)hipEventDestroy(ix->pev[i][j]);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
     delete ix;
+    if (orphan) hsa_index_free(orphan);     // a parent freed before its last clone
 }
 
 extern "C" size_t hsa_index_bytes(const hsa_index_t *ix)

@@ -62,6 +62,11 @@ struct hsa_index {
     void *d_any_aux = nullptr; size_t d_any_aux_cap = 0;
     void *d_split = nullptr; size_t d_split_cap = 0;   // strand-split items' results (k_split_finalize)
     void *d_fwd = nullptr; size_t d_fwd_cap = 0;       // lazy forward rows: count + reads for the forward pass
+    // hsa_splice_prefetch_batch: inputs, calls and outputs; its SA lookups; the pinned
+    // host copy of the outputs the caller's tables point into
+    void *d_pf = nullptr; size_t d_pf_cap = 0;
+    void *d_pf2 = nullptr; size_t d_pf2_cap = 0;
+    void *h_pf = nullptr; size_t h_pf_cap = 0;
     // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;
@@ -93,6 +98,7 @@ struct hsa_index {
     // and wrap tables, tries, SA, walk arrays) and owns its stream, events and scratch
     hsa_index *parent = nullptr;
     int n_clones = 0;                   // live clones of this index
+    bool free_pending = false;          // hsa_index_free called while clones were live
 };
 // HSA_E_ARG when an index's shared arrays may not be replaced (a clone, or an index with
 // live clones)

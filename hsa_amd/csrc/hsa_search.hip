@@ -162,6 +162,7 @@ static long search_any_host(hsa_index_t *ix, const hsa_regime_t *regimes, int n_
                             const uint8_t *codes, size_t codes_len, int32_t *n_aln, uint32_t *flags, uint64_t *hit_off,
                             uint32_t **hits_out, hsa_stats_t *stats, const MgHost *mh)
 {
+    HSA_HIP(hipSetDevice(ix->device));
     hipStream_t st = ix->stream;
     uint32_t max_len = 1, max_seed = 0;
     for (int j = 0; j < n; ++j) {
@@ -220,8 +221,9 @@ static long search_any_host(hsa_index_t *ix, const hsa_regime_t *regimes, int n_
     if (ctr[11]) { hsa_set_error("%llu reads exceed the large-pass capacity", ctr[11]); return HSA_E_ARG; }
     float ms = 0;
     HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
-    const uint64_t total = ctr[1];
+    const uint64_t total = ctr[1] < hit_cap ? ctr[1] : hit_cap;
     uint32_t *h = (uint32_t *)malloc((total + 1) * 36);
+    if (!h) { hsa_set_error("host allocation of %llu hits failed", (unsigned long long)total); return HSA_E_MEM; }
     if (total) HSA_HIP(hipMemcpy(h, d_hits, total * 36, hipMemcpyDeviceToHost));
     if (mh) {
         int32_t *cw = (int32_t *)malloc(cw_bytes + 8);
@@ -305,6 +307,7 @@ static long search_batch_impl(hsa_index_t *ix, const hsa_regime_t *regimes, int 
     if ((rc = jobs_limits(jobs, n_jobs, max_len, max_seed))) return rc;
     if (mh && (rc = mg_limits(jobs, mh->mg, n_jobs, *mh, max_seed))) return rc;
     if (codes_len >= 0xFFFFFFFFull) { hsa_set_error("read codes of one call must be < 4 GiB"); return HSA_E_ARG; }
+    HSA_HIP(hipSetDevice(ix->device));      // before any split: both halves allocate on ix's device
     for (int j = 0; j < n_jobs; ++j)        // the kernels read codes[off, off + len) of every job
         if (jobs[j].off > codes_len || jobs[j].len > codes_len - jobs[j].off) {
             hsa_set_error("job %d: codes [%llu, +%u) past codes_len %zu", j, (unsigned long long)jobs[j].off,
@@ -560,6 +563,388 @@ extern "C" int hsa_splice_seeds_device(hsa_index_t *ix, const hsa_regime_t *seed
                           &mgp)))
         return rc;
     HSA_HIP(hipEventRecord(ix->ev1, st));
+    return 0;
+}
+
+// ---------------------------------------------------------------- splice prefetch
+// hsa_splice_prefetch_batch (include/hsa_gpu.h): every width, seed search, anchor search
+// and SA -> position lookup bwt_splice_match (bwtgap.c:748-1332) can make before its
+// first extension, for a batch of fallback reads, in one device pass.
+struct PfArgs {
+    RankDir fwd, rev;
+    uint32_t T;
+    uint32_t C[5];
+    uint32_t n, max_len, sc, rs, cws;       // reads, longest, strand-code stride (bytes), row stride, cw stride (pairs)
+    const uint32_t *lens;
+    const uint64_t *offs;
+    const uint8_t *codes;                   // the reads as bwa_seq_t.seq holds them
+    const int32_t *amd;                     // per read: the anchors' max_diff
+    int32_t seed_max_diff;
+    uint8_t *scodes;                        // strand s of read r at (2 r + s) * sc
+    int32_t *rows;                          // 6 rows per read, rs pairs each (W1 s0/s1, W12 s0/s1, W0 s0/s1)
+    hsa_job_t *jobs;                        // 8 calls per read
+    hsa_mg_job_t *mg;
+    int32_t *cw;                            // per call cws pairs
+    int32_t *list;                          // seed calls, then anchor calls
+    int32_t *call_n;                        // 8 n
+    uint32_t *call_fl;
+    unsigned long long *acount;             // anchor calls listed
+};
+
+__device__ __forceinline__ uint32_t pf_base(const PfArgs &a, uint32_t r, uint32_t s, uint32_t p)
+{
+    const uint32_t L = a.lens[r];
+    const uint32_t c = a.codes[a.offs[r] + (s ? L - 1u - p : p)];
+    return s && c < 4 ? 3u - c : c;         // the reverse complement (bwtaln.c:326-333)
+}
+
+// thread (r, s, kind): kind 0 bwt_cal_width type 1 of the whole strand (and the strand's
+// codes), 1 type 1 of its last 12 bases, 2 type 0 of the whole strand (bwtaln.c:73-116;
+// the same chains as k_width / k_width0)
+__global__ void __launch_bounds__(BLOCK) k_pf_rows(PfArgs a)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t r = t / 6u, s = (t % 6u) & 1u, kind = (t % 6u) >> 1;
+    if (r >= a.n) return;
+    const uint32_t L = a.lens[r];
+    int32_t *const o = a.rows + 2 * ((size_t)r * 6u + kind * 2u + s) * a.rs;
+    uint32_t k = 0, l = a.T, bid = 0;
+    if (kind == 0 || kind == 1) {
+        if (kind == 1 && L < 12u) return;
+        const uint32_t p0 = kind == 1 ? L - 12u : 0u, n = kind == 1 ? 12u : L;
+        uint8_t *const sc = a.scodes + (size_t)(2u * r + s) * a.sc;
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t c = pf_base(a, r, s, p0 + i);
+            if (kind == 0) sc[i] = (uint8_t)c;
+            if (c < 4) {
+                uint32_t ok, ol;
+                hsa_occ1_pair(a.rev, k, l + 1u, c, ok, ol);
+                const uint32_t cc = c == 0 ? a.C[0] : c == 1 ? a.C[1] : c == 2 ? a.C[2] : a.C[3];
+                k = cc + ok + 1u;
+                l = cc + ol;
+            }
+            if (k > l || c > 3) { k = 0; l = a.T; ++bid; }
+            o[2 * i] = (int32_t)(l - k + 1u);
+            o[2 * i + 1] = (int32_t)bid;
+        }
+        o[2 * n] = 0;
+        o[2 * n + 1] = (int32_t)(bid + 1u);
+        return;
+    }
+    o[0] = 0; o[1] = 0;                      // entry 0: never written by the reference
+    for (uint32_t i = L - 1u; i > 0 && L > 0; --i) {
+        const uint32_t c = pf_base(a, r, s, i);
+        if (c < 4) {
+            uint32_t ok, ol;
+            hsa_occ1_pair(a.fwd, k, l + 1u, c, ok, ol);
+            const uint32_t cc = c == 0 ? a.C[0] : c == 1 ? a.C[1] : c == 2 ? a.C[2] : a.C[3];
+            k = cc + ok + 1u;
+            l = cc + ol;
+        }
+        if (k > l || c > 3) { k = 0; l = a.T; ++bid; }
+        o[2 * i] = (int32_t)(l - k + 1u);
+        o[2 * i + 1] = (int32_t)bid;
+    }
+    o[2 * L] = 0;
+    o[2 * L + 1] = (int32_t)(bid + 1u);
+}
+
+// thread (r, call 0..5): seed t of strand s (bwtgap.c:797-812): the strand [t sl, t sl + la)
+// with width_back = width_seed = the strand prefix's widths (bwt_cal_width of la bases,
+// :807): the first la entries of W1 and the terminal {0, bid + 1}
+__global__ void __launch_bounds__(BLOCK) k_pf_seeds(PfArgs a)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t r = t / 6u, i = t % 6u, s = i / 3u, tt = i % 3u;
+    if (r >= a.n) return;
+    const uint32_t L = a.lens[r], sl = L / 3u, la = sl + (tt == 2u ? L % 3u : 0u);
+    const uint32_t call = 8u * r + i;
+    a.list[6u * r + i] = (int32_t)call;
+    const int32_t *const w1 = a.rows + 2 * ((size_t)r * 6u + s) * a.rs;
+    int32_t *const cw = a.cw + 2 * (size_t)call * a.cws;
+    for (uint32_t p = 0; p < la; ++p) { cw[2 * p] = w1[2 * p]; cw[2 * p + 1] = w1[2 * p + 1]; }
+    cw[2 * la] = 0;
+    cw[2 * la + 1] = (la ? w1[2 * (la - 1u) + 1] : 0) + 1;
+    hsa_job_t J;
+    J.off = (uint64_t)(2u * r + s) * a.sc + tt * sl;
+    J.len = la;
+    J.max_diff = a.seed_max_diff;
+    J.seed_len = (int32_t)la;
+    J.regime = 0;
+    a.jobs[call] = J;
+    hsa_mg_job_t M;
+    M.wb_off = (uint64_t)call * a.cws;
+    M.ws_off = 0;
+    M.strand = (int32_t)s;
+    M.seed = HSA_SEED_ALIAS;
+    a.mg[call] = M;
+}
+
+// thread (r, s): the 12-mer anchor bwt_splice_match searches after an extension when the
+// strand's seed pattern is 3 (seeds 0 and 1 hit: its last 12 bases with their own widths,
+// bwtgap.c:911-919) or 6 (seeds 1 and 2: its first 12 with the whole strand's widths,
+// :1187-1192); width_seed NULL, the anchor regime, the read's max_diff
+__global__ void __launch_bounds__(BLOCK) k_pf_anchors(PfArgs a)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t r = t >> 1, s = t & 1u;
+    if (r >= a.n) return;
+    const uint32_t L = a.lens[r], call = 8u * r + 6u + s;
+    const int32_t *const cn = a.call_n + 8u * r + 3u * s;
+    const uint32_t *const cf = a.call_fl + 8u * r + 3u * s;
+    const bool done = !(cf[0] & HSA_F_OVERFLOW) && !(cf[1] & HSA_F_OVERFLOW) && !(cf[2] & HSA_F_OVERFLOW);
+    const uint32_t mask = (cn[0] > 0) | (cn[1] > 0) << 1 | (cn[2] > 0) << 2;
+    if (L <= 12u || !done || (mask != 3u && mask != 6u)) { a.call_n[call] = -1; return; }
+    const bool tail = mask == 3u;
+    const int32_t *const src = a.rows + 2 * ((size_t)r * 6u + (tail ? 2u : 0u) + s) * a.rs;
+    int32_t *const cw = a.cw + 2 * (size_t)call * a.cws;
+    for (uint32_t p = 0; p < 13u; ++p) { cw[2 * p] = src[2 * p]; cw[2 * p + 1] = src[2 * p + 1]; }
+    hsa_job_t J;
+    J.off = (uint64_t)(2u * r + s) * a.sc + (tail ? L - 12u : 0u);
+    J.len = 12u;
+    J.max_diff = a.amd[r];
+    J.seed_len = 0;
+    J.regime = 1;
+    a.jobs[call] = J;
+    hsa_mg_job_t M;
+    M.wb_off = (uint64_t)call * a.cws;
+    M.ws_off = 0;
+    M.strand = (int32_t)s;
+    M.seed = HSA_SEED_NONE;
+    a.mg[call] = M;
+    a.list[6u * a.n + atomicAdd(a.acount, 1ull)] = (int32_t)call;
+}
+
+// The SA indices bwt_aln_corelate_check can look up for a call's hits: k .. min(l, k + 49)
+// (bwtgap.c:698 reads at most 10 per hit, :711 at most 50; the loop bounds in bwtint_t)
+__device__ __forceinline__ uint32_t pf_sa_span(uint32_t k, uint32_t l)
+{
+    const uint32_t lim = k + 50u;                     // wraps as the reference's bound does
+    if (k > l || lim < k) return 0;
+    const uint32_t hi = l < lim - 1u ? l : lim - 1u;
+    return hi - k + 1u;
+}
+
+struct PfSaArgs {
+    uint32_t n_calls;
+    const int32_t *call_n;
+    const uint64_t *call_hit;                // relative to the call's hit region
+    const uint32_t *hits_s, *hits_a;         // seed calls' and anchor calls' hit regions
+    unsigned long long *call_sa;             // out: first SA result of the call
+    unsigned long long *total;
+    uint32_t *idx;                           // pass 2: the indices
+};
+
+__global__ void __launch_bounds__(BLOCK) k_pf_sa(PfSaArgs a, int fill)
+{
+    const uint32_t c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c >= a.n_calls) return;
+    const int32_t n = a.call_n[c];
+    if (n <= 0) { if (!fill) a.call_sa[c] = 0; return; }
+    const uint32_t *h = ((c & 7u) >= 6u ? a.hits_a : a.hits_s) + a.call_hit[c] * 9u;
+    if (!fill) {
+        unsigned long long cnt = 0;
+        for (int x = 0; x < n; ++x) cnt += pf_sa_span(h[9 * x + 1], h[9 * x + 2]);
+        a.call_sa[c] = atomicAdd(a.total, cnt);
+        return;
+    }
+    unsigned long long o = a.call_sa[c];
+    for (int x = 0; x < n; ++x) {
+        const uint32_t k = h[9 * x + 1], m = pf_sa_span(k, h[9 * x + 2]);
+        for (uint32_t j = 0; j < m; ++j) a.idx[o++] = k + j;
+    }
+}
+
+// The three capacity passes of caller-width searches over a device job list (as
+// hsa_splice_seeds_device runs them); counters ctr[16] zeroed here.
+static int mg_passes(hsa_index *ix, const hsa_regime_t *d_reg, const uint8_t *d_bmap, int nb, const hsa_job_t *jobs,
+                     const int32_t *list, const unsigned long long *n_dev, int n_upper, int max_len, bool gaps, bool wide,
+                     int max_entries, const uint8_t *codes, const MgPass &mgp, int32_t *d_n, uint32_t *d_fl,
+                     uint64_t *d_ho, uint32_t *d_hits, uint64_t hit_cap, unsigned long long *ctr, hipStream_t st)
+{
+    int rc;
+    LaunchPlan P, B, H;
+    if ((rc = plan_launch(ix, n_upper, max_len, 0, nb, gaps, wide, PASS_MAIN, P)) ||
+        (rc = plan_launch(ix, n_upper, max_len, 0, nb, gaps, wide, PASS_BIG, B)) ||
+        (rc = plan_launch(ix, n_upper, max_len, 0, nb, gaps, wide, PASS_HUGE, H, max_entries)))
+        return rc;
+    if ((rc = hsa_grow(&ix->d_ovf, &ix->d_ovf_cap, (size_t)n_upper * 4 + 64)) ||
+        (rc = hsa_grow(&ix->d_ovf2, &ix->d_ovf2_cap, (size_t)n_upper * 4 + 64)))
+        return rc;
+    HSA_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(unsigned long long), st));
+    if ((rc = launch_pass(ix, P, ix->main, d_reg, d_bmap, jobs, list, n_upper, max_len, 0, codes, d_n, d_fl, d_ho, d_hits,
+                          hit_cap, ctr, st, (int32_t *)ix->d_ovf, n_dev, 10, &mgp)) ||
+        (rc = launch_pass(ix, B, ix->big, d_reg, d_bmap, jobs, (const int32_t *)ix->d_ovf, n_upper, max_len, 0, codes, d_n,
+                          d_fl, d_ho, d_hits, hit_cap, ctr, st, (int32_t *)ix->d_ovf2, ctr + 8, 9, &mgp, 12)) ||
+        (rc = launch_pass(ix, H, ix->huge, d_reg, d_bmap, jobs, (const int32_t *)ix->d_ovf2, n_upper, max_len, 0, codes,
+                          d_n, d_fl, d_ho, d_hits, hit_cap, ctr, st, nullptr, ctr + 12, 15, &mgp)))
+        return rc;
+    return 0;
+}
+
+extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
+                                         int n, const uint32_t *lens, const uint64_t *offs, const uint8_t *codes,
+                                         size_t codes_len, const int32_t *anchor_max_diff, hsa_splice_pf_t *out)
+{
+    memset(out, 0, sizeof *out);
+    if (n <= 0) return 0;
+    if (int rc0 = hsa_need32(ix)) return rc0;
+    if (!seed_rg || !anchor_rg || !lens || !offs || !codes || !anchor_max_diff || !out) {
+        hsa_set_error("hsa_splice_prefetch_batch: null argument");
+        return HSA_E_ARG;
+    }
+    const hsa_regime_t rg2[2] = {*seed_rg, *anchor_rg};
+    int rc = check_regimes(rg2, 2);
+    if (rc) return rc;
+    if (seed_rg->max_gapo != 0) { hsa_set_error("seed searches have no gap opens (bwtgap.c:772)"); return HSA_E_ARG; }
+    if (!fast_regimes(rg2, 2)) { hsa_set_error("splice prefetch: options outside k_search's layouts"); return HSA_E_ARG; }
+    uint32_t M = 0;
+    for (int r = 0; r < n; ++r) {
+        if (lens[r] < 3 || lens[r] > 3 * (FAST_MAX_LEN - 2)) {    // seeds of at most FAST_MAX_LEN bases
+            hsa_set_error("splice prefetch: read %d of %u bases", r, lens[r]);
+            return HSA_E_ARG;
+        }
+        if (offs[r] > codes_len || lens[r] > codes_len - offs[r]) { hsa_set_error("read %d past codes_len", r); return HSA_E_ARG; }
+        if (anchor_max_diff[r] > anchor_rg->max_diff) { hsa_set_error("read %d: max_diff above the regime's", r); return HSA_E_ARG; }
+        M = lens[r] > M ? lens[r] : M;
+    }
+    HSA_HIP(hipSetDevice(ix->device));
+    hipStream_t st = ix->stream;
+    const double t0 = [] { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t.tv_sec + 1e-9 * t.tv_nsec; }();
+    const size_t N = (size_t)n, calls = 8 * N;
+    const uint32_t sc = (M + 15u) / 16u * 16u + 16u, rs = M + 1u, cws = M / 3u + 3u > 13u ? M / 3u + 3u : 13u;
+    const uint64_t cap_s = 6 * N * 16 + 65536, cap_a = 2 * N * 16 + 16384;
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    // device layout
+    size_t o = 0;
+    const size_t o_lens = o; o += al(N * 4);
+    const size_t o_offs = o; o += al(N * 8);
+    const size_t o_amd = o; o += al(N * 4);
+    const size_t o_codes = o; o += al(codes_len + 64);
+    const size_t o_sc = o; o += al(2 * N * sc + 64);
+    const size_t o_jobs = o; o += al(calls * sizeof(hsa_job_t));
+    const size_t o_mg = o; o += al(calls * sizeof(hsa_mg_job_t));
+    const size_t o_list = o; o += al(8 * N * 4);
+    const size_t o_ctr = o; o += 1024;                    // seed ctr[16], anchor ctr[16], anchor count, SA total
+    // outputs, one contiguous block: [call_n | call_fl | call_hit | call_sa | rows | cw | hits_s | hits_a]
+    const size_t o_out = o;
+    const size_t q_n = 0, q_fl = q_n + al(calls * 4), q_ho = q_fl + al(calls * 4), q_sa = q_ho + al(calls * 8);
+    const size_t q_rows = q_sa + al(calls * 8), q_cw = q_rows + al(N * 6 * rs * 8), q_hs = q_cw + al(calls * cws * 8);
+    const size_t q_ha = q_hs + al(cap_s * 36), q_end = q_ha + al(cap_a * 36);
+    o += q_end;
+    if ((rc = hsa_grow(&ix->d_pf, &ix->d_pf_cap, o + 256))) return rc;
+    char *d = (char *)ix->d_pf;
+    HSA_HIP(hipMemcpyAsync(d + o_lens, lens, N * 4, hipMemcpyHostToDevice, st));
+    HSA_HIP(hipMemcpyAsync(d + o_offs, offs, N * 8, hipMemcpyHostToDevice, st));
+    HSA_HIP(hipMemcpyAsync(d + o_amd, anchor_max_diff, N * 4, hipMemcpyHostToDevice, st));
+    HSA_HIP(hipMemcpyAsync(d + o_codes, codes, codes_len, hipMemcpyHostToDevice, st));
+    unsigned long long *ctr_s = (unsigned long long *)(d + o_ctr), *ctr_a = ctr_s + 16, *acnt = ctr_s + 32,
+                       *satot = ctr_s + 33, *scnt = ctr_s + 34;
+    HSA_HIP(hipMemsetAsync(ctr_s, 0, 1024, st));
+    char *dq = d + o_out;
+    PfArgs A;
+    A.fwd = RankDir{ix->blk[0], ix->isa0};
+    A.rev = RankDir{ix->blk[1], ix->risa0};
+    A.T = ix->T;
+    memcpy(A.C, ix->C, sizeof A.C);
+    A.n = (uint32_t)n; A.max_len = M; A.sc = sc; A.rs = rs; A.cws = cws;
+    A.lens = (const uint32_t *)(d + o_lens); A.offs = (const uint64_t *)(d + o_offs);
+    A.codes = (const uint8_t *)(d + o_codes); A.amd = (const int32_t *)(d + o_amd);
+    A.seed_max_diff = seed_rg->max_diff;
+    A.scodes = (uint8_t *)(d + o_sc);
+    A.rows = (int32_t *)(dq + q_rows);
+    A.jobs = (hsa_job_t *)(d + o_jobs); A.mg = (hsa_mg_job_t *)(d + o_mg);
+    A.cw = (int32_t *)(dq + q_cw); A.list = (int32_t *)(d + o_list);
+    A.call_n = (int32_t *)(dq + q_n); A.call_fl = (uint32_t *)(dq + q_fl);
+    A.acount = acnt;
+    HSA_HIP(hipMemsetAsync(d + o_sc, 4, 2 * N * sc + 64, st));         // padding reads as N
+    hipLaunchKernelGGL(k_pf_rows, dim3((unsigned)((6 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
+    hipLaunchKernelGGL(k_pf_seeds, dim3((unsigned)((6 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
+    HSA_HIP(hipGetLastError());
+    // both regimes staged once: seeds use regime 0, anchors regime 1
+    void *before = ix->d_in;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1536))) return rc;
+    int nb = 0;
+    if ((rc = stage_regimes(ix, rg2, 2, (char *)ix->d_in, nb, st, before != ix->d_in))) return rc;
+    const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
+    const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
+    const bool wide = need_wide(rg2, 2);
+    const MgPass mgp{A.mg, A.cw};
+    const unsigned long long n_seed = 6 * N;
+    HSA_HIP(hipMemcpyAsync(scnt, &n_seed, 8, hipMemcpyHostToDevice, st));
+    HSA_HIP(hipEventRecord(ix->ev0, st));
+    if ((rc = mg_passes(ix, d_reg, d_bmap, nb, A.jobs, A.list, scnt, (int)(6 * N), (int)(M / 3u + 2u), false, wide,
+                        seed_rg->max_entries, A.scodes, mgp, A.call_n, A.call_fl, (uint64_t *)(dq + q_ho),
+                        (uint32_t *)(dq + q_hs), cap_s, ctr_s, st)))
+        return rc;
+    hipLaunchKernelGGL(k_pf_anchors, dim3((unsigned)((2 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
+    HSA_HIP(hipGetLastError());
+    if ((rc = mg_passes(ix, d_reg, d_bmap, nb, A.jobs, A.list + 6 * N, acnt, (int)(2 * N), 12,
+                        anchor_rg->max_gapo > 0, wide, anchor_rg->max_entries, A.scodes, mgp, A.call_n, A.call_fl,
+                        (uint64_t *)(dq + q_ho), (uint32_t *)(dq + q_ha), cap_a, ctr_a, st)))
+        return rc;
+    // unfinished calls (hits past the caps, stacks past the HUGE pass) are not answered
+    PfSaArgs S;
+    S.n_calls = (uint32_t)calls;
+    S.call_n = A.call_n; S.call_hit = (const uint64_t *)(dq + q_ho);
+    S.hits_s = (const uint32_t *)(dq + q_hs); S.hits_a = (const uint32_t *)(dq + q_ha);
+    S.call_sa = (unsigned long long *)(dq + q_sa); S.total = satot; S.idx = nullptr;
+    const bool with_sa = ix->d_sa != nullptr;
+    if (with_sa) hipLaunchKernelGGL(k_pf_sa, dim3((unsigned)((calls + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, S, 0);
+    HSA_HIP(hipGetLastError());
+    unsigned long long hc[40];
+    HSA_HIP(hipMemcpyAsync(hc, ctr_s, sizeof hc, hipMemcpyDeviceToHost, st));
+    HSA_HIP(hipStreamSynchronize(st));
+    const uint64_t n_sa = with_sa ? hc[33] : 0;
+    if (n_sa && (rc = hsa_grow(&ix->d_pf2, &ix->d_pf2_cap, al(n_sa * 4) + n_sa * 16 + 256))) return rc;
+    uint32_t *d_idx = (uint32_t *)ix->d_pf2, *d_sao = (uint32_t *)((char *)ix->d_pf2 + al(n_sa * 4));
+    if (n_sa) {
+        S.idx = d_idx;
+        hipLaunchKernelGGL(k_pf_sa, dim3((unsigned)((calls + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, S, 1);
+        HSA_HIP(hipGetLastError());
+        if ((rc = hsa_sa_position_device(ix, n_sa, d_idx, d_sao, st))) return rc;
+    }
+    HSA_HIP(hipEventRecord(ix->ev1, st));
+    // one copy of the output block (hits up to their counts) into pinned host memory
+    const uint64_t nh_s = hc[1] < cap_s ? hc[1] : cap_s, nh_a = hc[16 + 1] < cap_a ? hc[16 + 1] : cap_a;
+    const size_t h_need = q_hs + (nh_s + nh_a) * 36 + al(n_sa * 16) + 256;
+    if (h_need > ix->h_pf_cap) {
+        if (ix->h_pf) (void)hipHostFree(ix->h_pf);
+        ix->h_pf = nullptr; ix->h_pf_cap = 0;
+        HSA_HIP(hipHostMalloc(&ix->h_pf, h_need + h_need / 4, hipHostMallocDefault));
+        ix->h_pf_cap = h_need + h_need / 4;
+    }
+    char *h = (char *)ix->h_pf;
+    HSA_HIP(hipMemcpyAsync(h, dq, q_hs + nh_s * 36, hipMemcpyDeviceToHost, st));
+    if (nh_a) HSA_HIP(hipMemcpyAsync(h + q_hs + nh_s * 36, dq + q_ha, nh_a * 36, hipMemcpyDeviceToHost, st));
+    const size_t h_sa = al(q_hs + (nh_s + nh_a) * 36);
+    if (n_sa) HSA_HIP(hipMemcpyAsync(h + h_sa, d_sao, n_sa * 16, hipMemcpyDeviceToHost, st));
+    HSA_HIP(hipStreamSynchronize(st));
+    float ms = 0;
+    HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+    // anchor calls' hit offsets into the one hits array; unfinished calls -2
+    int32_t *cn = (int32_t *)(h + q_n);
+    const uint32_t *cf = (const uint32_t *)(h + q_fl);
+    uint64_t *ch = (uint64_t *)(h + q_ho);
+    for (size_t c = 0; c < calls; ++c) {
+        if ((c & 7u) >= 6u && cn[c] >= 0) ch[c] += nh_s;
+        if (cn[c] >= 0 && (cf[c] & HSA_F_OVERFLOW)) cn[c] = -2;
+    }
+    out->n = n; out->max_len = (int)M; out->row_stride = (int)rs; out->cw_stride = (int)cws;
+    out->call_n = cn; out->call_hit = ch;
+    out->call_sa = with_sa ? (const uint64_t *)(h + q_sa) : nullptr;
+    out->rows = (const int32_t *)(h + q_rows);
+    out->wafter = (const int32_t *)(h + q_cw);
+    out->hits = (const uint32_t *)(h + q_hs);
+    out->sa = n_sa ? (const uint32_t *)(h + h_sa) : nullptr;
+    out->n_hits = nh_s + nh_a; out->n_sa = n_sa;
+    out->kernel_ms = ms;
+    if (getenv("HSA_VERBOSE")) {
+        struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t);
+        fprintf(stderr, "[hsa] splice prefetch on the device: %d reads, %llu seed + %llu anchor calls, %llu hits, %llu SA "
+                        "lookups, %.1f ms (kernels %.1f ms)\n", n, (unsigned long long)n_seed, (unsigned long long)hc[32],
+                (unsigned long long)(nh_s + nh_a), (unsigned long long)n_sa, 1e3 * (t.tv_sec + 1e-9 * t.tv_nsec - t0), ms);
+    }
     return 0;
 }
 

@@ -1972,6 +1972,42 @@ static bool use_split(const LaunchPlan &P, int n, const unsigned long long *n_de
     return 2 * (size_t)n <= P.resident;
 }
 
+// The pass's search scratch (per-lane pools, links, staged hits), sized to what the
+// device can give: the pool per lane is the plan's capacity unless that would not fit in
+// the free HBM (less a 2 GiB margin) or in HSA_SCRATCH_MB, in which case it is halved
+// until it does (down to 512 entries), and again if the allocation itself fails.  A
+// smaller pool changes no result: a read that outgrows its lane is re-run in the BIG and
+// HUGE passes as before, so the cost is speed, never an error (the reference's capacity
+// bound is max_entries, bwtgap.c:150-151, which the HUGE pass keeps).
+static int scratch_fit(hsa_index *ix, SearchScratch &S, LaunchPlan &P, size_t EW)
+{
+    const size_t lb = P.huge ? 4 : 2, floor_cap = 512;
+    auto pe_of = [&](uint32_t pc) { return (size_t)((pc + 31u) & ~31u) * EW; };
+    auto bytes = [&](uint32_t pc) { return P.lanes * (pe_of(pc) * (16 + lb) + (size_t)P.hcap * EW * 36); };
+    const bool held = S.pool && lb == S.link_bytes && P.lanes * pe_of(P.pcap) <= S.pool_entries &&
+                      P.lanes * (size_t)P.hcap * EW <= S.hit_entries;
+    if (!held && !P.huge) {
+        const char *cm = getenv("HSA_SCRATCH_MB");      // read per pass: tests set it mid-process
+        const size_t cap_mb = cm ? strtoull(cm, nullptr, 10) : 0;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); fr = (size_t)-1 / 2; }
+        fr += S.pool_entries * (16 + S.link_bytes) + S.hit_entries * 36;     // what the reservation frees first
+        size_t avail = fr > ((size_t)2 << 30) ? fr - ((size_t)2 << 30) : 0;
+        if (cap_mb && avail > (cap_mb << 20)) avail = cap_mb << 20;
+        const uint32_t want = P.pcap;
+        while (bytes(P.pcap) > avail && P.pcap > floor_cap) P.pcap = P.pcap / 2 > floor_cap ? P.pcap / 2 : floor_cap;
+        if (P.pcap != want && getenv("HSA_VERBOSE"))
+            fprintf(stderr, "[hsa] search scratch: pool %u -> %u entries per lane (%.1f GB for %zu lanes; %.1f GB "
+                            "available)\n", want, P.pcap, bytes(P.pcap) / 1e9, P.lanes, avail / 1e9);
+    }
+    for (;;) {
+        const int rc = hsa_scratch_reserve(S, P.lanes, pe_of(P.pcap), (size_t)P.hcap * EW, lb);
+        if (rc != HSA_E_MEM || P.huge || P.pcap <= floor_cap) return rc;
+        P.pcap = P.pcap / 2 > floor_cap ? P.pcap / 2 : floor_cap;
+        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] search scratch: allocation failed, pool -> %u per lane\n", P.pcap);
+    }
+}
+
 template <typename IT = uint32_t>
 static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, const hsa_regime_t *d_regimes,
                        const uint8_t *d_bmap, const hsa_job_t *d_jobs, const int32_t *d_list, int n, int max_len,
@@ -1989,7 +2025,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
     }
     // 64-bit intervals: two uint4 per pool entry, 10 staged words per hit (HitW)
     constexpr size_t EW = sizeof(IT) / 4;
-    int rc = hsa_scratch_reserve(S, P.lanes, (size_t)((P.pcap + 31u) & ~31u) * EW, P.hcap * EW, P.huge ? 4 : 2);
+    int rc = scratch_fit(ix, S, P, EW);
     if (rc) return rc;
     const uint32_t esz = P.wide ? 2u : 1u;
     const uint32_t rb = (((uint32_t)max_len + 1u) * esz + 3u) & ~3u, rs = (((uint32_t)max_seed + 1u) * esz + 3u) & ~3u;

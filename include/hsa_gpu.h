@@ -107,8 +107,10 @@ int  hsa_index_build_walk(hsa_index_t *ix, const uint32_t *d_sa_full, const uint
  * clone shares src's read-only device arrays (rank blocks, wrap tables, tries, SA, walk
  * arrays) and has its own stream, events and search scratch, so hsa_search_device on
  * the two handles may overlap (the next batch's k_widths fills the last waves of this
- * one's k_search).  Free every clone before src; hsa_index_set_sa and
- * hsa_index_build_walk refuse a clone and an index with live clones.  No reference
+ * one's k_search).  hsa_index_free(src) while clones are live defers the free of the
+ * shared arrays to the last clone's hsa_index_free (src must not be used after it);
+ * hsa_index_set_sa and hsa_index_build_walk refuse a clone and an index with live
+ * clones.  No reference
  * counterpart: the reference searches one batch at a time (bwtaln.c:477, :506). */
 int  hsa_index_clone(hsa_index_t *src, hsa_index_t **out);
 
@@ -295,6 +297,55 @@ typedef struct {
     int32_t max_len;                      /* longest read */
 } hsa_seed_batch_t;
 int hsa_splice_seeds_device(hsa_index_t *ix, const hsa_regime_t *seed_regime, const hsa_seed_batch_t *b, void *stream);
+
+/* ---- the splice path's prefetch of one read batch ----
+ * bwt_splice_match (bwtgap.c:748-1332) runs on the host for every read the main search
+ * leaves without a hit; before its first seed extension, the searches it can make are
+ * determined by the read alone.  This call runs all of them for n such reads in one
+ * device pass (replacing, for the host's splice tables, one GPU call per bwt_match_gap /
+ * bwt_cal_width / BWTRetrievePositionFromSAIndex the reference makes there):
+ *   per read r (codes as bwa_seq_t.seq: 0-3, 4 = N; 3 <= lens[r] <= 3 063) and strand s
+ *   (0: the read, 1: its reverse complement, bwtaln.c:326-333),
+ *   rows (bwt_width_t pairs, int32 w then bid; row_stride pairs apart, row j of read r
+ *     at rows + 2 * (6 r + j) * row_stride):
+ *     j = s      bwt_cal_width type 1 of the whole strand (L + 1 pairs, bwtaln.c:84-97);
+ *                the width of the strand's prefix of length la is its first la entries
+ *                and {0, bid of entry la - 1, + 1};
+ *     j = 2 + s  type 1 of the strand's last 12 bases (13 pairs; L >= 12 only);
+ *     j = 4 + s  type 0 of the whole strand (L + 1 pairs, entry 0 = 0; bwtaln.c:98-115);
+ *   calls (8 per read, call 8 r + c):
+ *     c = 3 s + t, t = 0..2: seed t of strand s (bwtgap.c:797-812): the strand's bases
+ *       [t sl, t sl + la) (sl = L / 3, la = sl + (t == 2 ? L % 3 : 0)), width_back =
+ *       width_seed = the strand prefix's widths of length la, regime seed_rg, max_diff
+ *       seed_rg->max_diff, seed_len la;
+ *     c = 6 + s: the strand's 12-mer anchor when its seeds' hit pattern is 3 (seeds 0 and
+ *       1 hit: its last 12 bases with row 2 + s, bwtgap.c:911-919) or 6 (seeds 1 and 2:
+ *       its first 12 with the first 13 entries of row s, :1187-1192), width_seed NULL,
+ *       regime anchor_rg, max_diff anchor_max_diff[r];
+ *     call_n: hits (bwt_aln1_t records at hits + 9 * call_hit, start = end = 0 as
+ *       bwt_match_gap returns them), -1 not searched, -2 not finished (hits past the
+ *       buffer, or a stack past the reference's bound): the caller searches it itself;
+ *     wafter: the call's width_back after the search (gap_shadow, bwtgap.c:217),
+ *       cw_stride pairs per call;
+ *   SA (with hsa_index_set_sa): BWTRetrievePositionFromSAIndex of k .. min(l, k + 49) of
+ *     every hit of every call, in order (bwt_aln_corelate_check, bwtgap.c:698, :711):
+ *     4 u32 each as hsa_sa_position_batch, the call's first at sa + 4 * call_sa.
+ * The arrays point into pinned host memory the index owns until its next call. */
+typedef struct {
+    int n, max_len, row_stride, cw_stride;
+    const int32_t *rows;
+    const int32_t *call_n;
+    const uint64_t *call_hit;
+    const uint32_t *hits;
+    const int32_t *wafter;
+    const uint64_t *call_sa;      /* NULL without an SA */
+    const uint32_t *sa;
+    uint64_t n_hits, n_sa;
+    double kernel_ms;
+} hsa_splice_pf_t;
+int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg, int n,
+                              const uint32_t *lens, const uint64_t *offs, const uint8_t *codes, size_t codes_len,
+                              const int32_t *anchor_max_diff, hsa_splice_pf_t *out);
 
 /* SA index -> text position (BWTSaValue BWT.c:1195 + BWTRetrievePositionFromSAIndex
  * 2BWT-Interface.c:329), batched.  hsa_index_set_sa uploads the sampled suffix array

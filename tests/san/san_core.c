@@ -252,3 +252,102 @@ int hsa_extend_sliced(hsa_index_t *ix, const hsa_regime_t *regimes, int n_regime
     (void)slots; (void)resume; (void)n_slots; (void)budget;
     return hsa_extend_batch(ix, regimes, n_regimes, jobs, n, codes, bids, win_len, ret, max_pos, aln_out);
 }
+
+/* hsa_splice_prefetch_batch (include/hsa_gpu.h) on the restatement: the rows, the six
+ * seed calls and the anchors of every read, and the SA lookups of their hits. */
+static int32_t *g_pf_rows, *g_pf_n, *g_pf_wa;
+static uint64_t *g_pf_hit, *g_pf_sa;
+static hv_t g_pf_hits;
+static uint32_t *g_pf_sav;
+static size_t g_pf_nsa, g_pf_sacap;
+
+int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg, int n,
+                              const uint32_t *lens, const uint64_t *offs, const uint8_t *codes, size_t codes_len,
+                              const int32_t *anchor_max_diff, hsa_splice_pf_t *out)
+{
+    (void)codes_len;
+    const or_index_t *ox = (const or_index_t *)ix;
+    memset(out, 0, sizeof *out);
+    free(g_pf_rows); free(g_pf_n); free(g_pf_wa); free(g_pf_hit); free(g_pf_sa); free(g_pf_hits.h); free(g_pf_sav);
+    g_pf_hits.h = NULL; g_pf_hits.n = g_pf_hits.cap = 0; g_pf_sav = NULL; g_pf_nsa = g_pf_sacap = 0;
+    int M = 0;
+    for (int r = 0; r < n; ++r) M = (int)lens[r] > M ? (int)lens[r] : M;
+    const size_t rs = (size_t)M + 1, cws = (size_t)(M / 3 + 3 > 13 ? M / 3 + 3 : 13);
+    g_pf_rows = (int32_t *)calloc((size_t)n * 6 * rs * 2 + 2, 4);
+    g_pf_n = (int32_t *)calloc((size_t)n * 8 + 1, 4);
+    g_pf_hit = (uint64_t *)calloc((size_t)n * 8 + 1, 8);
+    g_pf_sa = (uint64_t *)calloc((size_t)n * 8 + 1, 8);
+    g_pf_wa = (int32_t *)calloc((size_t)n * 8 * cws * 2 + 2, 4);
+    uint8_t *ss[2];
+    ss[0] = (uint8_t *)malloc((size_t)M + 1);
+    ss[1] = (uint8_t *)malloc((size_t)M + 1);
+    for (int r = 0; r < n; ++r) {
+        const int L = (int)lens[r], sl = L / 3;
+        const uint8_t *q = codes + offs[r];
+        for (int j = 0; j < L; ++j) { ss[0][j] = q[j]; ss[1][j] = q[L - 1 - j] < 4 ? (uint8_t)(3 - q[L - 1 - j]) : q[L - 1 - j]; }
+        int32_t *row[6];
+        for (int j = 0; j < 6; ++j) row[j] = g_pf_rows + 2 * ((size_t)r * 6 + (size_t)j) * rs;
+        for (int s = 0; s < 2; ++s) {
+            or_cal_width(ox, L, ss[s], (uint32_t *)row[s]);
+            if (L >= 12) or_cal_width(ox, 12, ss[s] + L - 12, (uint32_t *)row[2 + s]);
+            or_cal_width0(ox, L, ss[s], (uint32_t *)row[4 + s]);
+        }
+        for (int c = 0; c < 8; ++c) {
+            const int s = c < 6 ? c / 3 : c - 6, t = c % 3;
+            const size_t cc = 8 * (size_t)r + (size_t)c;
+            int32_t *cw = g_pf_wa + 2 * cc * cws;
+            hsa_job_t J;
+            memset(&J, 0, sizeof J);
+            const uint8_t *sq;
+            int len, kind;
+            const hsa_regime_t *R;
+            if (c < 6) {
+                const int la = sl + (t == 2 ? L % 3 : 0);
+                for (int p = 0; p < la; ++p) { cw[2 * p] = row[s][2 * p]; cw[2 * p + 1] = row[s][2 * p + 1]; }
+                cw[2 * la] = 0;
+                cw[2 * la + 1] = (la ? row[s][2 * (la - 1) + 1] : 0) + 1;
+                J.max_diff = seed_rg->max_diff; J.seed_len = la;
+                sq = ss[s] + t * sl; len = la; kind = 2; R = seed_rg;
+            } else {
+                const int32_t *cn = g_pf_n + 8 * (size_t)r + 3 * s;
+                const int mask = (cn[0] > 0) | (cn[1] > 0) << 1 | (cn[2] > 0) << 2;
+                if (L <= 12 || (mask != 3 && mask != 6)) { g_pf_n[cc] = -1; continue; }
+                const int tail = mask == 3;
+                const int32_t *src = tail ? row[2 + s] : row[s];
+                for (int p = 0; p < 13; ++p) { cw[2 * p] = src[2 * p]; cw[2 * p + 1] = src[2 * p + 1]; }
+                J.max_diff = anchor_max_diff[r];
+                sq = ss[s] + (tail ? L - 12 : 0); len = 12; kind = 0; R = anchor_rg;
+            }
+            or_opt_t o = opt_of(R, &J);
+            uint32_t *h = NULL;
+            const int na = or_match_gap(ox, &o, R->n_stacks, sq, len, s, (uint32_t *)cw, kind, NULL, &h);
+            g_pf_n[cc] = na;
+            g_pf_hit[cc] = g_pf_hits.n;
+            if (na > 0) hv_add(&g_pf_hits, h, na);
+            or_free(h);
+        }
+        if (!g_sa_vals) continue;
+        for (int c = 0; c < 8; ++c) {                   /* k .. min(l, k + 49) of every hit */
+            const size_t cc = 8 * (size_t)r + (size_t)c;
+            g_pf_sa[cc] = g_pf_nsa;
+            for (int x = 0; x < g_pf_n[cc]; ++x) {
+                const uint32_t *hh = g_pf_hits.h + 9 * (g_pf_hit[cc] + (size_t)x);
+                for (uint32_t j = hh[1]; j <= hh[2] && j < hh[1] + 50u; ++j) {
+                    if (g_pf_nsa == g_pf_sacap) {
+                        g_pf_sacap = g_pf_sacap ? 2 * g_pf_sacap : 1024;
+                        g_pf_sav = (uint32_t *)realloc(g_pf_sav, g_pf_sacap * 16);
+                    }
+                    if (hsa_sa_position_batch(ix, 1, &j, g_pf_sav + 4 * g_pf_nsa)) return HSA_E_ARG;
+                    ++g_pf_nsa;
+                }
+            }
+        }
+    }
+    free(ss[0]); free(ss[1]);
+    out->n = n; out->max_len = M; out->row_stride = (int)rs; out->cw_stride = (int)cws;
+    out->rows = g_pf_rows; out->call_n = g_pf_n; out->call_hit = g_pf_hit;
+    out->hits = g_pf_hits.h ? g_pf_hits.h : (g_pf_hits.h = (uint32_t *)calloc(9, 4));
+    out->wafter = g_pf_wa; out->call_sa = g_sa_vals ? g_pf_sa : NULL; out->sa = g_pf_sav;
+    out->n_hits = g_pf_hits.n; out->n_sa = g_pf_nsa;
+    return 0;
+}

@@ -8,12 +8,18 @@ import numpy as np
 from golden_io import INDEX, load_case, parse_opts
 
 
-def _worker(rank, world, port, name, batch, short_reads, q, use_gpu=False):
+def _worker(rank, world, port, name, batch, short_reads, q, use_gpu=False, backend="gloo"):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":      # RCCL: the collectives on the rank's GPU, as bench.py does
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        comm = torch.device("cuda", 0)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        comm = torch.device("cpu")
     try:
         from hsa_amd import index_io, shard
         from oracle_ctypes import Opt, OracleIndex, default_opt
@@ -40,14 +46,15 @@ def _worker(rank, world, port, name, batch, short_reads, q, use_gpu=False):
                 return n_aln, flags, hoff, hits
 
         def allreduce_max(a):
-            t = torch.from_numpy(a.astype(np.int64))
+            t = torch.from_numpy(a.astype(np.int64)).to(comm)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            return t.numpy().astype(np.int32)
+            return t.cpu().numpy().astype(np.int32)
 
         info = {}
         res = shard.search_sharded(search, make_opt, opt0, lens, codes, batch, world, rank, allreduce_max, info)
-        out = shard.gather_to_root(res, dist, "cpu")
+        out = shard.gather_to_root(res, dist, comm)
         if rank == 0:
+            info["backend"] = dist.get_backend()
             q.put((out, info))
     finally:
         dist.destroy_process_group()

@@ -73,18 +73,25 @@ HSA_GPU_ALL = os.path.join(ROOT, "oracle", "_ref", "HSA_gpu_all")
 
 @pytest.mark.skipif(not os.path.exists(HSA_GPU_ALL), reason="oracle/_ref/HSA_gpu_all not built (make -C oracle)")
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,reads", [("default", "reads"), ("n4o0", "reads"), ("splice_default", "splice_reads"),
-                                        ("splice_n4o1", "splice_reads"), ("splice_n4o1O120", "splice_reads")])
-def test_dropin_all_entry_points_sam_identical(name, reads):
+@pytest.mark.parametrize("name,reads,env", [("default", "reads", {}), ("n4o0", "reads", {}),
+                                            ("splice_default", "splice_reads", {}), ("splice_n4o1", "splice_reads", {}),
+                                            ("splice_n4o1O120", "splice_reads", {}),
+                                            ("splice_n4o1", "splice_reads",
+                                             {"HSA_SPLICE_PREFETCH": "0", "HSA_SPLICE_THREADS": "4"})])
+def test_dropin_all_entry_points_sam_identical(name, reads, env):
     """Every drop-in entry point replaced at once (oracle/ref.mk HSA_gpu_all):
     bwa_cal_sa_reg_gap, bwt_match_gap, and the SAM stage's bwa_cal_pac_pos, whose SA ->
     position lookups (seq_id, position and the duplicate filter of the extra hits in
     every SAM line) run as one GPU batch per read batch (hsa_amd/csrc/bwtse_gpu.c).
     splice_n4o1O120 (-O 120): n_stacks 283, more score LIFOs than an extension slice slot
-    holds, so the splice path's extensions run through hsa_extend_batch."""
+    holds, so the splice path's extensions run through hsa_extend_batch.
+    HSA_SPLICE_PREFETCH=0 with 4 runner threads: no splice tables, so every seed and
+    anchor search and every width of the splice path is a direct GPU call, made from
+    four host threads at once (the calls serialise on slot 0's index)."""
     idx = os.path.join(GOLD, "index", "tiny.fa")
     fq = os.path.join(GOLD, MAN[reads])
-    r = subprocess.run([HSA_GPU_ALL, "aln", *MAN[name]["args"], idx, fq], capture_output=True, timeout=120)
+    r = subprocess.run([HSA_GPU_ALL, "aln", *MAN[name]["args"], idx, fq], capture_output=True, timeout=120,
+                       env=dict(os.environ, **env))
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     if hashlib.sha256(r.stdout).hexdigest() != MAN[name]["sam_sha256"]:
         ref = gzip.open(os.path.join(GOLD, f"dropin_ref_{name}.sam.gz")).read().splitlines()

@@ -242,6 +242,46 @@ def test_device_path_rerun_is_exact():
     assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
 
 
+@pytest.mark.parametrize("case", ["tiny_gap100_n4o1", "rep_gap60_default"])
+def test_scratch_cap_shrinks_pool_and_stays_exact(case, monkeypatch, capfd):
+    """HSA_SCRATCH_MB caps the search scratch a handle may take (as a co-resident
+    process or a third handle would, by leaving little HBM free): the main pass's
+    per-lane pool shrinks to fit instead of the call failing, reads that outgrow the
+    smaller pool finish in the BIG/HUGE re-runs, and every hit equals the oracle's."""
+    from hsa_amd._lib import GpuIndex
+    monkeypatch.setenv("HSA_SCRATCH_MB", "4")
+    monkeypatch.setenv("HSA_VERBOSE", "1")
+    g = load_case(case)
+    fresh = GpuIndex(*index_io.read_index(INDEX[g["index"]]))     # no scratch held yet
+    try:
+        got, (e_n, e_f, e_h, _) = _device_run(case, ix=fresh)
+    finally:
+        fresh.close()
+    assert "search scratch: pool" in capfd.readouterr().err, "the pool was not capped"
+    assert got["c"][11] == 0, "reads left unfinished"
+    assert np.array_equal(got["f"] & 1, e_f & 1)
+    assert np.array_equal(got["n"], e_n)
+    exp = split_hits(e_n, e_h)
+    bad = [i for i in range(len(exp)) if not np.array_equal(got["h"][got["o"][i]:got["o"][i] + max(got["n"][i], 0)],
+                                                             exp[i])]
+    assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
+
+
+def test_parent_freed_before_its_clone():
+    """hsa_index_free on an index whose clone is still live defers the free of the shared
+    rank blocks to the clone's own hsa_index_free: the clone still searches exactly."""
+    from hsa_amd._lib import GpuIndex, lib
+    parent = GpuIndex(*index_io.read_index(INDEX["tiny"]))
+    c = parent.clone()
+    lib().hsa_index_free(parent.h)            # the C API directly (the wrapper closes clones first)
+    parent.h, parent._clones = None, []
+    try:
+        got, (e_n, e_f, e_h, _) = _device_run("tiny_mm100_n4o0", ix=c)
+    finally:
+        c.close()                              # frees the clone, then the deferred parent
+    assert np.array_equal(got["n"], e_n) and np.array_equal(got["f"] & 1, e_f & 1)
+
+
 @pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("case", ["tiny_mm100_n4o0", "tiny_gap100_n4o1", "rep_mm100_n4o1"])
 def test_rank_queries_match_oracle(case, split, monkeypatch):

@@ -54,12 +54,23 @@ def test_two_ranks_gpu_search_equal_sequential(name, short_reads):
     _two_ranks(name, short_reads, use_gpu=True)
 
 
-def _two_ranks(name, short_reads, use_gpu):
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,short_reads", [("tiny_gap100_n4o1_b400", False), ("tiny_exact36_n0", True)])
+def test_one_rank_rccl_gather_equal_sequential(name, short_reads):
+    """The bench's RCCL path (the `nccl` backend: bench.py's all-reduce of the
+    option-state flags and its hit-list gather, hsa_amd/shard.py) executed on the box's
+    GPU at world size 1, with the HIP search: the gathered lists equal the sequential
+    reference's."""
+    _two_ranks(name, short_reads, use_gpu=True, world=1, backend="nccl")
+
+
+def _two_ranks(name, short_reads, use_gpu, world=2, backend="gloo"):
     batch = CASES[name]["batch"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, batch, short_reads, q, use_gpu)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, batch, short_reads, q, use_gpu, backend))
+             for r in range(world)]
     for p in procs:
         p.start()
     out = None
@@ -74,10 +85,12 @@ def _two_ranks(name, short_reads, use_gpu):
         p.join(timeout=120)
         assert p.exitcode == 0
     (n_aln, flags, hits), info = out
-    # rank 0 holds batches 0, 2, 4, ...: with the short reads in batch 0, its later
-    # batches must have been searched again with the sticky seed_len
-    assert info["first_sticky"] == (0 if short_reads else None)
-    assert bool(info["rerun"]) == short_reads
+    assert info["backend"] == backend
+    if world > 1:
+        # rank 0 holds batches 0, 2, 4, ...: with the short reads in batch 0, its later
+        # batches must have been searched again with the sticky seed_len
+        assert info["first_sticky"] == (0 if short_reads else None)
+        assert bool(info["rerun"]) == short_reads
     e_n, e_f, e_h = _sequential(name, batch, short_reads)
     assert np.array_equal(n_aln, e_n)
     assert np.array_equal(flags, e_f)
