@@ -547,8 +547,8 @@ def main():
                          "search scratch does not fit are dropped")
     ap.add_argument("--ref-sample", type=int, default=-1,
                     help="reads the REFERENCE's own CPU path (oracle/_ref/ref_probe) searches, over --ref-procs "
-                         "processes (-1: 8 000 per process for config 2, 2 000 for config 3; 0: skip the reference "
-                         "legs)")
+                         "processes (-1: 8 000 per process for config 2, 2 000 for config 3, 1 000 for config 4; 0: "
+                         "skip the reference legs)")
     ap.add_argument("--ref-procs", type=int, default=0,
                     help="reference processes (0: the CPU threads of the job's share, 16 per GPU rank)")
     ap.add_argument("--e2e-reads", type=int, default=1_000_000,
@@ -593,8 +593,8 @@ def main():
     # the job's CPU share (16 per GPU rank: the whole share of the node at N = 8)
     ref_procs = a.ref_procs or cpu_info()["threads"] * world
     if a.ref_sample < 0:
-        a.ref_sample = {2: 8_000, 3: 2_000}.get(a.config, 0) * ref_procs
-    ref_legs = rank == 0 and a.config in (2, 3) and not wide and a.ref_sample > 0 and T < (1 << 32)
+        a.ref_sample = {2: 8_000, 3: 2_000, 4: 1_000}.get(a.config, 0) * ref_procs
+    ref_legs = rank == 0 and a.config in (2, 3, 4) and not wide and a.ref_sample > 0 and T < (1 << 32)
     t0 = time.time()
     if wide:
         gi, res, extra = build_index64(T, GENOME_SEED, device)
@@ -1070,7 +1070,8 @@ def main():
                                       "sample": f"{n} reads of the same workload: bwa_cal_sa_reg_gap restatement + "
                                                 f"the 6 seed searches of its {int((fl & 1).sum())} fallback reads, "
                                                 f"1 thread, in {dt1:.1f} s"}
-    # the reference's own CPU path, and the drop-in end to end (rank 0, N=1, configs 2, 3)
+    # the reference's own CPU path, and the drop-in end to end (rank 0, configs 2-4; config
+    # 4's end to end runs the whole splice path of its fallback reads)
     # With N ranks it runs after the gather on rank 0, over the CPU share of all N ranks
     # (the other ranks wait on the rendezvous store meanwhile, without spinning a core);
     # the drop-in end to end needs a GPU of its own and runs at N = 1 only.
@@ -1088,9 +1089,9 @@ def main():
             port = result.get("cpu_baseline")
             result["cpu_baseline"] = dict(legs["reference"])
             if port:
-                result["cpu_baseline"].update(cpu_model=port["cpu_model"],
-                                              physical_cores_visible=port["physical_cores_visible"],
-                                              port={k: port[k] for k in ("value", "cores", "value_1core", "sample")})
+                result["cpu_baseline"].update(cpu_model=port.get("cpu_model"),
+                                              physical_cores_visible=port.get("physical_cores_visible"),
+                                              port={k: port.get(k) for k in ("value", "cores", "value_1core", "sample")})
             if legs.get("dropin_e2e"):
                 result["dropin_e2e"] = legs["dropin_e2e"]
         else:

@@ -17,6 +17,7 @@
  * search the rest in regime B.  When the two regimes cannot differ for any read
  * (same effective options, equal read lengths) the whole call is one launch.
  */
+#include <malloc.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdio.h>
@@ -35,6 +36,8 @@
 #pragma weak hsa_splice_run
 #pragma weak hsa_splice_table_stats
 #pragma weak hsa_splice_set_read
+#pragma weak hsa_splice_warm
+#pragma weak hsa_splice_prefetch_warm
 #pragma weak hsa_splice_sa_clear
 #pragma weak hsa_splice_sa_stats
 
@@ -186,12 +189,15 @@ static void write_outputs(bwa_seq_t *seqs, int n, const int32_t *n_aln, const ui
 /* write_outputs on a thread of its own (while the splice prefetch runs on the device) */
 typedef struct {
     bwa_seq_t *seqs; int n; const int32_t *n_aln; const uint32_t *flags; const uint64_t *hoff; const uint32_t *hits;
+    double secs;
 } out_job_t;
 
 static void *out_job_run(void *arg)
 {
-    const out_job_t *j = (const out_job_t *)arg;
+    out_job_t *j = (out_job_t *)arg;
+    const double t0 = hsa_now();
     write_outputs(j->seqs, j->n, j->n_aln, j->flags, j->hoff, j->hits);
+    j->secs = hsa_now() - t0;
     return NULL;
 }
 
@@ -551,6 +557,25 @@ int hsa_gpu_attach(const Idx2BWT *bi)
     }
     if (g_att[e].n == 0) g_att[e].key = NULL;
     pthread_mutex_unlock(&g_att_mu);
+    /* the splice path's host and device resources, made before the first batch needs them */
+    if (rc == 0) {
+        /* Every batch hands the host ~100 000 calloc'd hit arrays (bwt_match_gap's contract,
+         * bwtgap.c:137-138) that the host frees before the next batch (bwaseqio.c:244).
+         * glibc returns the freed pages to the kernel by default, so each batch re-faults
+         * them (~20 ms per 100 000 reads); keeping them in the heap makes the next batch's
+         * arrays reuse them.  Results do not depend on it; HSA_MALLOC_TUNE=0 leaves the
+         * host's malloc as it is. */
+        const char *mt = getenv("HSA_MALLOC_TUNE");
+        static int tuned = 0;
+        if (!tuned && (!mt || atoi(mt) != 0)) {
+            mallopt(M_TRIM_THRESHOLD, 1 << 30);
+            mallopt(M_MMAP_THRESHOLD, 64 << 20);
+            tuned = 1;
+        }
+        if (hsa_splice_warm && hsa_splice_extend_active && hsa_splice_extend_active()) hsa_splice_warm(4096);
+        if (hsa_splice_prefetch_warm && hsa_splice_prefetch_active && hsa_splice_prefetch_active())
+            hsa_splice_prefetch_warm(bi);
+    }
     return rc;
 }
 
@@ -696,7 +721,7 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     int nf = 0;
     for (int i = 0; i < n_seqs; ++i)
         nf += !(flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) && n_aln[i] == 0 && (flags[i] & HSA_F_FALLBACK);
-    out_job_t oj = {seqs, n_seqs, n_aln, flags, hoff, hits};
+    out_job_t oj = {seqs, n_seqs, n_aln, flags, hoff, hits, 0.0};
     pthread_t oth;
     int out_async = 0;
     if (want_pf && nf > 0 && have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active()) {
@@ -742,8 +767,10 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
         sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)n_seqs + 1));
         sr_idx = (int *)malloc(sizeof(int) * ((size_t)n_seqs + 1));
     }
+    const double tj = hsa_now();
     if (out_async) pthread_join(oth, NULL);
-    else write_outputs(seqs, n_seqs, n_aln, flags, hoff, hits);
+    else out_job_run(&oj);
+    const double t_join = hsa_now() - tj;
     int q_fb = 0;                                               /* the read's prefetch-table number */
     for (int i = 0; i < n_seqs; ++i) {                          /* the splice path's reads, in order */
         bwa_seq_t *p = seqs + i;
@@ -803,7 +830,9 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     free(sr); free(sr_idx);
     if (getenv("HSA_VERBOSE"))
         fprintf(stderr, "[hsa] batch of %d reads: search %.3f s, splice prefetch %.3f s, splice path %.3f s "
-                        "(%d fallback reads)\n", n_seqs, t1 - t0, t_pf, hsa_now() - t2 + (t2 - t1 - t_pf), n_sr);
+                        "(%d fallback reads; per-read outputs %.1f ms%s, %.1f ms waited for)\n", n_seqs, t1 - t0, t_pf,
+                hsa_now() - t2 + (t2 - t1 - t_pf), n_sr, 1e3 * oj.secs, out_async ? " beside the prefetch" : "",
+                1e3 * t_join);
     if (aux.stack) {
         free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);
         ref_stack_free(aux.stack);

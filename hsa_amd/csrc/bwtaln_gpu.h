@@ -60,6 +60,8 @@ void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses);
 void hsa_splice_table_stats(uint64_t *w_hits, uint64_t *w_misses, uint64_t *sa_hits, uint64_t *sa_misses);
 /* the prefetch table's answers for the read the calling thread works on */
 void hsa_splice_set_read(int r);
+void hsa_splice_prefetch_warm(const Idx2BWT *bi);
+void hsa_splice_warm(int n_coroutines);
 int hsa_splice_table_width(const Idx2BWT *bi, int len, const ubyte_t *str, bwt_width_t *width, int type, int *ret);
 int hsa_splice_table_sa(const Idx2BWT *bi, uint32_t idx, uint32_t o[3]);
 

@@ -544,6 +544,19 @@ static co_t *co_pool(int W, int max_len, int n_stacks)
     return g_co;
 }
 
+/* The coroutine pool made ahead of the first batch (hsa_gpu_attach): n coroutines, their
+ * stacks mapped and the top pages of each touched, so that the first batch's splice
+ * path does not pay the mappings and first-touch faults. */
+void hsa_splice_warm(int n)
+{
+    if (n > CO_MAX) n = CO_MAX;
+    pthread_mutex_lock(&g_co_mu);
+    co_t *co = co_pool(n, 128, 1);
+    for (int k = 0; k < n; ++k)
+        memset((char *)co[k].stack + CO_STACK - (32u << 10), 0, 32u << 10);
+    pthread_mutex_unlock(&g_co_mu);
+}
+
 /* One host thread of the runner: its coroutines, the reads they take from the shared
  * queue, and its own scheduling point (tl_sched). */
 typedef struct runner_s runner_t;

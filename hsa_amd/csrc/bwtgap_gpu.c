@@ -378,6 +378,35 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
     return 0;
 }
 
+/* One small device pass at attach time: the prefetch's kernels loaded and its buffers
+ * made before the first batch (its answers are discarded). */
+void hsa_splice_prefetch_warm(const Idx2BWT *bi)
+{
+    gap_opt_t o;
+    memset(&o, 0, sizeof o);
+    o.s_mm = 3; o.s_gapo = 11; o.s_gape = 4; o.max_diff = 4; o.max_gapo = 1; o.max_gape = 6;   /* gap_init_opt */
+    o.max_seed_diff = 2; o.seed_len = 32; o.max_entries = 2000000; o.max_top2 = 30; o.indel_end_skip = 5;
+    o.max_del_occ = 10; o.fnr = -1.0f;
+    ubyte_t seq[2][100], rc[2][100];
+    for (int r = 0; r < 2; ++r)
+        for (int j = 0; j < 100; ++j) {
+            seq[r][j] = (ubyte_t)((j * 7 + r * 3 + (j >> 3)) & 3);
+            rc[r][99 - j] = (ubyte_t)(3 - seq[r][j]);
+        }
+    gap_stack_t st;
+    memset(&st, 0, sizeof st);
+    st.n_stacks = hsa_aln_score(&o, o.max_diff + 1, o.max_gapo + 1, o.max_gape + 1);
+    bwt_aux_t a[2], *ap[2];
+    memset(a, 0, sizeof a);
+    for (int r = 0; r < 2; ++r) {
+        a[r].bi_bwt = (Idx2BWT *)bi; a[r].seq = seq[r]; a[r].rc_seq = rc[r]; a[r].len = 100; a[r].opt = &o;
+        a[r].stack = &st; a[r].max_len = 100;
+        ap[r] = a + r;
+    }
+    hsa_splice_prefetch(bi, 2, ap);
+    hsa_splice_memo_clear();
+}
+
 /* Table statistics since the last call (hits, misses), for logs: bwt_match_gap, then
  * bwt_cal_width and SA -> position (hsa_splice_table_stats). */
 void hsa_splice_memo_stats(uint64_t *hits, uint64_t *misses)

@@ -911,8 +911,9 @@ extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *se
     if (h_need > ix->h_pf_cap) {
         if (ix->h_pf) (void)hipHostFree(ix->h_pf);
         ix->h_pf = nullptr; ix->h_pf_cap = 0;
-        HSA_HIP(hipHostMalloc(&ix->h_pf, h_need + h_need / 4, hipHostMallocDefault));
-        ix->h_pf_cap = h_need + h_need / 4;
+        const size_t want = h_need + h_need / 4 > ((size_t)64 << 20) ? h_need + h_need / 4 : ((size_t)64 << 20);
+        HSA_HIP(hipHostMalloc(&ix->h_pf, want, hipHostMallocDefault));
+        ix->h_pf_cap = want;
     }
     char *h = (char *)ix->h_pf;
     HSA_HIP(hipMemcpyAsync(h, dq, q_hs + nh_s * 36, hipMemcpyDeviceToHost, st));

@@ -242,7 +242,7 @@ def test_device_path_rerun_is_exact():
     assert not bad, f"{len(bad)} reads differ; first {bad[0]}"
 
 
-@pytest.mark.parametrize("case", ["tiny_gap100_n4o1", "rep_gap60_default"])
+@pytest.mark.parametrize("case", ["tiny_gap100_n4o1", "rep_mm100_n4o1"])
 def test_scratch_cap_shrinks_pool_and_stays_exact(case, monkeypatch, capfd):
     """HSA_SCRATCH_MB caps the search scratch a handle may take (as a co-resident
     process or a third handle would, by leaving little HBM free): the main pass's
