@@ -168,35 +168,32 @@ static void *out_run(void *arg)
     return NULL;
 }
 
-/* out_run over every read, on up to 8 host threads for large calls */
+/* out_run over every read, on the calling thread: the arrays then come from its heap
+ * arena, where the host frees them and the next batch reuses them (on several threads
+ * they were slower: allocations from several arenas, freed from the host's) */
 static void write_outputs(bwa_seq_t *seqs, int n, const int32_t *n_aln, const uint32_t *flags, const uint64_t *hoff,
                           const uint32_t *hits)
 {
-    enum { MAXT = 8 };
-    const int nt = n >= (1 << 14) ? MAXT : 1;
-    out_part_t part[MAXT];
-    pthread_t th[MAXT];
-    int started[MAXT] = {0};
-    for (int k = 0; k < nt; ++k) {
-        part[k] = (out_part_t){seqs, n_aln, flags, hoff, hits, (int)((long)n * k / nt), (int)((long)n * (k + 1) / nt)};
-        if (k > 0) started[k] = pthread_create(&th[k], NULL, out_run, &part[k]) == 0;
-        if (k > 0 && !started[k]) out_run(&part[k]);
-    }
-    out_run(&part[0]);
-    for (int k = 1; k < nt; ++k) if (started[k]) pthread_join(th[k], NULL);
+    out_part_t part = {seqs, n_aln, flags, hoff, hits, 0, n};
+    out_run(&part);
 }
 
-/* write_outputs on a thread of its own (while the splice prefetch runs on the device) */
+/* The splice prefetch of one batch on a thread of its own (bwa_cal_sa_reg_gap). */
 typedef struct {
-    bwa_seq_t *seqs; int n; const int32_t *n_aln; const uint32_t *flags; const uint64_t *hoff; const uint32_t *hits;
+    const Idx2BWT *bi;
+    int n;
+    bwt_aux_t *fa, **fp;
+    gap_opt_t *fo;
+    ubyte_t *rc;
+    gap_stack_t st_shape;
     double secs;
-} out_job_t;
+} pf_job_t;
 
-static void *out_job_run(void *arg)
+static void *pf_job_run(void *arg)
 {
-    out_job_t *j = (out_job_t *)arg;
+    pf_job_t *j = (pf_job_t *)arg;
     const double t0 = hsa_now();
-    write_outputs(j->seqs, j->n, j->n_aln, j->flags, j->hoff, j->hits);
+    hsa_splice_prefetch(j->bi, j->n, j->fp);
     j->secs = hsa_now() - t0;
     return NULL;
 }
@@ -222,6 +219,7 @@ typedef struct {
 
 static int hb_append(hitbuf_t *b, const uint32_t *src, size_t n)
 {
+    if (n == 0) return 0;
     if (b->n + n > b->cap) {
         size_t c = (b->n + n) * 2 + 64;
         uint32_t *p = (uint32_t *)realloc(b->h, c * 36);
@@ -536,6 +534,31 @@ static int attach_slot(const Idx2BWT *bi, int slot, hsa_index_t *const *have, hs
     return rc;
 }
 
+/* Two small searches on every slot at attach time, one without and one with gap opens:
+ * the search kernels the first batches use are loaded before them (answers discarded). */
+static void search_warm(const Idx2BWT *bi)
+{
+    int n_slots = 0;
+    hsa_index_t *const *slots = hsa_gpu_slots_of(bi, &n_slots);
+    uint8_t codes[2 * 100];
+    for (int j = 0; j < 200; ++j) codes[j] = (uint8_t)((j * 5 + (j >> 4)) & 3);
+    const uint32_t lens[2] = {100, 100};
+    const uint64_t offs[2] = {0, 100};
+    for (int gapo = 0; gapo < 2; ++gapo) {
+        gap_opt_t o;
+        memset(&o, 0, sizeof o);
+        o.s_mm = 3; o.s_gapo = 11; o.s_gape = 4; o.max_diff = 4; o.max_gapo = gapo; o.max_gape = 6;   /* gap_init_opt */
+        o.max_seed_diff = 2; o.seed_len = 32; o.max_entries = 2000000; o.max_top2 = 30; o.indel_end_skip = 5;
+        o.max_del_occ = 10; o.fnr = -1.0f;
+        int32_t n_aln[2], sp[4];
+        uint32_t fl[2], *hits = NULL;
+        uint64_t ho[2];
+        if (hsa_cal_sa_reg_gap_multi(slots, n_slots, &o, 2, lens, offs, codes, sizeof codes, n_aln, fl, ho, &hits, sp,
+                                     NULL) >= 0)
+            hsa_free(hits);
+    }
+}
+
 /* Upload the bidirectional BWT of a loaded Idx2BWT once per slot in use (hook after
  * BWTLoad2BWT); slots added later by hsa_gpu_set_devices are attached on first use. */
 int hsa_gpu_attach(const Idx2BWT *bi)
@@ -571,7 +594,17 @@ int hsa_gpu_attach(const Idx2BWT *bi)
             mallopt(M_TRIM_THRESHOLD, 1 << 30);
             mallopt(M_MMAP_THRESHOLD, 64 << 20);
             tuned = 1;
+            /* and the heap those arrays take for a 100 000-read batch, made now: its pages
+             * faulted in once, here, and kept */
+            enum { N_WARM = 120000 };
+            void **w = (void **)malloc(sizeof(void *) * N_WARM);
+            if (w) {
+                for (int i = 0; i < N_WARM; ++i) w[i] = calloc(10, sizeof(bwt_aln1_t));
+                for (int i = N_WARM - 1; i >= 0; --i) free(w[i]);
+                free(w);
+            }
         }
+        search_warm(bi);
         if (hsa_splice_warm && hsa_splice_extend_active && hsa_splice_extend_active()) hsa_splice_warm(4096);
         if (hsa_splice_prefetch_warm && hsa_splice_prefetch_active && hsa_splice_prefetch_active())
             hsa_splice_prefetch_warm(bi);
@@ -709,9 +742,9 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     const int n_stacks = hsa_aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
     /* the splice path's widths, seed and anchor searches and SA lookups of every fallback
      * read in one device pass (hsa_splice_prefetch, bwtgap_gpu.c), when the host's
-     * bwt_splice_match calls our bwt_match_gap; the per-read output arrays are written on
-     * host threads meanwhile */
-    int prefetched = 0;
+     * bwt_splice_match calls our bwt_match_gap: on a thread of its own, while this thread
+     * writes the per-read output arrays (so that they come from the host thread's own heap
+     * arena, where the host frees them) */
     double t_pf = 0.0;
     const double t1 = hsa_now();
     /* HSA_SPLICE_PREFETCH=0: no table, every splice-path call goes to the GPU on its own
@@ -721,41 +754,50 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     int nf = 0;
     for (int i = 0; i < n_seqs; ++i)
         nf += !(flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) && n_aln[i] == 0 && (flags[i] & HSA_F_FALLBACK);
-    out_job_t oj = {seqs, n_seqs, n_aln, flags, hoff, hits, 0.0};
-    pthread_t oth;
-    int out_async = 0;
-    if (want_pf && nf > 0 && have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active()) {
-        out_async = pthread_create(&oth, NULL, out_job_run, &oj) == 0;
-        bwt_aux_t *fa = (bwt_aux_t *)calloc((size_t)nf, sizeof(bwt_aux_t));
-        bwt_aux_t **fp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)nf);
-        gap_opt_t *fo = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nf);
-        ubyte_t *rc = (ubyte_t *)malloc(tot + 1);
-        gap_stack_t st_shape;                       /* only n_stacks is read */
-        memset(&st_shape, 0, sizeof st_shape);
-        st_shape.n_stacks = n_stacks;
+    pf_job_t pj;
+    memset(&pj, 0, sizeof pj);
+    pthread_t pth;
+    int pf_async = 0;
+    const int prefetched = want_pf && nf > 0 && have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active();
+    if (prefetched) {
+        pj.bi = bi_bwt;
+        pj.n = nf;
+        pj.fa = (bwt_aux_t *)calloc((size_t)nf, sizeof(bwt_aux_t));
+        pj.fp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)nf);
+        pj.fo = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nf);
+        pj.rc = (ubyte_t *)malloc(tot + 1);
+        memset(&pj.st_shape, 0, sizeof pj.st_shape);   /* only n_stacks is read */
+        pj.st_shape.n_stacks = n_stacks;
         int q = 0;
         for (int i = 0; i < n_seqs; ++i) {
             if ((flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) || n_aln[i] != 0 || !(flags[i] & HSA_F_FALLBACK)) continue;
             const bwa_seq_t *p = seqs + i;
-            ubyte_t *r = rc + offs[i];
+            ubyte_t *r = pj.rc + offs[i];
             for (int j = 0; j < (int)p->len; ++j) {
                 ubyte_t c = p->seq[p->len - 1 - j];
                 r[j] = c < 4 ? (ubyte_t)(3 - c) : c;
             }
-            fo[q] = local;
-            fo[q].max_diff = sp[2 * i];
-            fo[q].seed_len = sp[2 * i + 1];
-            fa[q].bi_bwt = (Idx2BWT *)bi_bwt; fa[q].arr = arr; fa[q].max_len = max_len;
-            fa[q].seq = p->seq; fa[q].rc_seq = r; fa[q].len = (int)p->len; fa[q].opt = fo + q;
-            fa[q].stack = &st_shape;
-            fp[q] = fa + q;
+            pj.fo[q] = local;
+            pj.fo[q].max_diff = sp[2 * i];
+            pj.fo[q].seed_len = sp[2 * i + 1];
+            bwt_aux_t *x = pj.fa + q;
+            x->bi_bwt = (Idx2BWT *)bi_bwt; x->arr = arr; x->max_len = max_len;
+            x->seq = p->seq; x->rc_seq = r; x->len = (int)p->len; x->opt = pj.fo + q;
+            x->stack = &pj.st_shape;
+            pj.fp[q] = x;
             ++q;
         }
-        t_pf = hsa_now();
-        hsa_splice_prefetch(bi_bwt, nf, fp);
-        t_pf = hsa_now() - t_pf;
-        prefetched = 1;
-        free(fa); free(fp); free(fo); free(rc);
+        pf_async = pthread_create(&pth, NULL, pf_job_run, &pj) == 0;
+        if (!pf_async) pf_job_run(&pj);
+    }
+    const double to = hsa_now();
+    write_outputs(seqs, n_seqs, n_aln, flags, hoff, hits);
+    const double t_out = hsa_now() - to;
+    if (pf_async) pthread_join(pth, NULL);
+    const double t_join = hsa_now() - to - t_out;
+    if (prefetched) {
+        t_pf = pj.secs;
+        free(pj.fa); free(pj.fp); free(pj.fo); free(pj.rc);
     }
     /* the host's splice path for the fallback reads: all of them at once as coroutines
      * whose seed extensions run batched on the GPU, when the host calls our
@@ -767,10 +809,6 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
         sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)n_seqs + 1));
         sr_idx = (int *)malloc(sizeof(int) * ((size_t)n_seqs + 1));
     }
-    const double tj = hsa_now();
-    if (out_async) pthread_join(oth, NULL);
-    else out_job_run(&oj);
-    const double t_join = hsa_now() - tj;
     int q_fb = 0;                                               /* the read's prefetch-table number */
     for (int i = 0; i < n_seqs; ++i) {                          /* the splice path's reads, in order */
         bwa_seq_t *p = seqs + i;
@@ -831,7 +869,7 @@ void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *s
     if (getenv("HSA_VERBOSE"))
         fprintf(stderr, "[hsa] batch of %d reads: search %.3f s, splice prefetch %.3f s, splice path %.3f s "
                         "(%d fallback reads; per-read outputs %.1f ms%s, %.1f ms waited for)\n", n_seqs, t1 - t0, t_pf,
-                hsa_now() - t2 + (t2 - t1 - t_pf), n_sr, 1e3 * oj.secs, out_async ? " beside the prefetch" : "",
+                hsa_now() - t2 + (t2 - t1 - t_pf), n_sr, 1e3 * t_out, prefetched ? " beside the prefetch" : "",
                 1e3 * t_join);
     if (aux.stack) {
         free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);

@@ -382,9 +382,10 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
  * made before the first batch (its answers are discarded). */
 void hsa_splice_prefetch_warm(const Idx2BWT *bi)
 {
+    for (int gapo = 0; gapo < 2; ++gapo) {       /* anchors without and with gap opens */
     gap_opt_t o;
     memset(&o, 0, sizeof o);
-    o.s_mm = 3; o.s_gapo = 11; o.s_gape = 4; o.max_diff = 4; o.max_gapo = 1; o.max_gape = 6;   /* gap_init_opt */
+    o.s_mm = 3; o.s_gapo = 11; o.s_gape = 4; o.max_diff = 4; o.max_gapo = gapo; o.max_gape = 6;   /* gap_init_opt */
     o.max_seed_diff = 2; o.seed_len = 32; o.max_entries = 2000000; o.max_top2 = 30; o.indel_end_skip = 5;
     o.max_del_occ = 10; o.fnr = -1.0f;
     ubyte_t seq[2][100], rc[2][100];
@@ -405,6 +406,7 @@ void hsa_splice_prefetch_warm(const Idx2BWT *bi)
     }
     hsa_splice_prefetch(bi, 2, ap);
     hsa_splice_memo_clear();
+    }
 }
 
 /* Table statistics since the last call (hits, misses), for logs: bwt_match_gap, then
