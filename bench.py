@@ -70,7 +70,7 @@ def log(*a):
 def build_index(T, seed, device, with_files=False):
     """The hg19-sized index on the device.  with_files: also keep the text (packed) and
     the forward direction's every-8th SA values (hsa_build_bwt_index_device, the same
-    sort), for the reference's index files (reference_files)."""
+    sort: the .sa of `HSA index`), for the reference's index files (reference_files)."""
     import torch
     from hsa_amd import _lib
     L = _lib.lib()
@@ -86,17 +86,18 @@ def build_index(T, seed, device, with_files=False):
         Cc = np.zeros(5, np.uint32)
         t0 = time.time()
         if rev == 0:
-            # the forward BWT with its whole suffix array (the same sort): the walk's SA,
-            # and every SA_INTERVAL-th value for the reference's .sa
+            # the forward BWT and (with_files) every SA_INTERVAL-th suffix-array value of
+            # the same sort, for the reference's .sa
             i64 = C.c_uint64()
             C64 = np.zeros(5, np.uint64)
-            sa = torch.zeros(T + 1, dtype=torch.int32, device="cuda")
+            sa = torch.zeros(T // SA_INTERVAL + 2 if with_files else 1, dtype=torch.int32, device="cuda")
             _lib.check(L.hsa_build_bwt_index_device(device, T, text.data_ptr(), bw.data_ptr(), C.byref(i64), C64,
-                                                    1, sa.data_ptr()))
+                                                    SA_INTERVAL if with_files else 0,
+                                                    sa.data_ptr() if with_files else None))
             isa0.value = int(i64.value)
             Cc[:] = C64.astype(np.uint32)
             if with_files:
-                extra["sa"] = sa[::SA_INTERVAL].cpu().numpy().view(np.uint32)
+                extra["sa"] = sa[:T // SA_INTERVAL + 1].cpu().numpy().view(np.uint32)
         else:
             _lib.check(L.hsa_build_bwt_device(device, T, text.data_ptr(), rev, bw.data_ptr(), C.byref(isa0), Cc))
         log(f"[bench] BWT{' (reverse)' if rev else ''} of {T} bp built on the device in {time.time() - t0:.1f} s")
@@ -105,11 +106,6 @@ def build_index(T, seed, device, with_files=False):
         extra["text"] = text[:nw].cpu().numpy().view(np.uint32)
     gi = _lib.GpuIndex.from_device_codes(T, res[0][1], res[0][2], res[0][0].data_ptr(), T, res[1][1], res[1][2],
                                          res[1][0].data_ptr(), device=device)
-    if os.environ.get("HSA_WALK") == "1":                   # experiment builds only
-        t0 = time.time()
-        gi.build_walk(sa.data_ptr(), text.data_ptr())      # the unique-interval walk's SA, ISA, text
-        log(f"[bench] unique-interval walk arrays (SA, ISA, text: {(8 * (T + 1) + T // 4) / 2**30:.1f} GiB) "
-            f"in {time.time() - t0:.1f} s")
     del text, sa
     torch.cuda.empty_cache()
     return gi, res, extra

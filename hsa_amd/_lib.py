@@ -31,7 +31,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_cal_sa_reg_gap_multi", "hsa_index_create_device64", "hsa_index_is64", "hsa_occ4_batch64",
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
-    "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced", "hsa_index_trie", "hsa_index_build_walk",
+    "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced", "hsa_index_trie",
     "hsa_index_clone", "hsa_splice_prefetch_batch",
 ]
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
@@ -178,7 +178,6 @@ def lib():
     L.hsa_index_bytes.restype = C.c_size_t
     L.hsa_index_bytes.argtypes = [vp]
     L.hsa_index_trie.argtypes = [vp, C.c_void_p, C.c_void_p, C.c_void_p]
-    L.hsa_index_build_walk.argtypes = [vp, C.c_void_p, C.c_void_p]
     L.hsa_index_clone.argtypes = [vp, C.POINTER(vp)]
     L.hsa_index_stream.restype = vp
     L.hsa_index_stream.argtypes = [vp]
@@ -410,11 +409,6 @@ class GpuIndex:
 
     def nbytes(self) -> int:
         return int(lib().hsa_index_bytes(self.h))
-
-    def build_walk(self, d_sa_full=None, d_text=None):
-        """The unique-interval walk's arrays (hsa_index_build_walk): device pointers of
-        the full SA and the packed text, or None to derive them from the sampled SA."""
-        check(lib().hsa_index_build_walk(self.h, d_sa_full, d_text))
 
     def trie(self):
         """(width-trie depth, search-trie depth, bytes) of the index's root tries."""

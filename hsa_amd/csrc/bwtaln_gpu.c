@@ -524,11 +524,6 @@ static int attach_slot(const Idx2BWT *bi, int slot, hsa_index_t *const *have, hs
     if (rc == 0 && f->saValue && bi->hsp)
         rc = hsa_index_set_sa(ix, f->saValue, f->saValueSizeInWord, f->saInterval,
                               (const uint32_t *)bi->hsp->blockList, bi->hsp->numOfBlock);
-    /* the unique-interval walk's arrays, derived from that SA on the device, for an
-     * experiment build that walks (HSA_WALK=1); without the memory for them the searches
-     * just take rank steps */
-    const char *we = getenv("HSA_WALK");
-    if (rc == 0 && f->saValue && we && atoi(we) == 1) (void)hsa_index_build_walk(ix, NULL, NULL);
     if (rc != 0 && ix) { hsa_index_free(ix); ix = NULL; }
     *out = ix;
     return rc;

@@ -233,13 +233,11 @@ RankDir64 hsa_rank_dir64(const hsa_index *ix, int dir)
     return RankDir64{ix->blk[dir], dir ? ix->risa0_64 : ix->isa0_64, ix->any_wrap[dir] ? 1u : 0u};
 }
 
-// The root tries of hsa_trie.h, level by level on the index's stream.  The width trie
-// (k_widths) has HSA_TRIE_DEPTH levels (0 = none; by default 12, less for a text shorter
-// than 4^(D-1) characters, whose deeper levels would hold mostly empty strings).  The
-// search trie (k_search) is built only when HSA_TRIE_MODE >= 1 at index creation, with
-// min(D, HSA_TRIE_SDEPTH or 11) levels: k_search measured slower with it.
+// The root width trie of hsa_trie.h, level by level on the index's stream: HSA_TRIE_DEPTH
+// levels (0 = none; by default 12, less for a text shorter than 4^(D-1) characters, whose
+// deeper levels would hold mostly empty strings).
 template <typename IT, typename RD>
-static int build_tries_t(hsa_index *ix, RD fwd, RD rev, IT T, const IT *C)
+static int build_tries_t(hsa_index *ix, RD rev, IT T, const IT *C)
 {
     uint32_t D = HSA_TRIE_DEFAULT_DEPTH;
     if (const char *e = getenv("HSA_TRIE_DEPTH")) {        // as asked (tests: tries deeper than the text)
@@ -248,26 +246,16 @@ static int build_tries_t(hsa_index *ix, RD fwd, RD rev, IT T, const IT *C)
     } else {
         while (D > 0 && (1ull << (2 * D)) > 4ull * (uint64_t)T) --D;
     }
-    uint32_t Ds = 0;
-    if (const char *m = getenv("HSA_TRIE_MODE"); m && atoi(m) >= 1) {
-        Ds = 11;
-        if (const char *sd = getenv("HSA_TRIE_SDEPTH")) Ds = (uint32_t)atoi(sd);
-        Ds = Ds < D ? Ds : D;
-    }
-    ix->trie_depth = ix->trie_sdepth = 0;
+    ix->trie_depth = 0;
     if (D == 0) return 0;
-    const size_t es = sizeof(IT) == 4 ? 16 : 32, ws = sizeof(IT) == 4 ? 8 : 16;
-    const size_t nw = trie_base(D + 1), ns = Ds ? trie_base(Ds + 1) : 0;
-    // the tries only save rank steps: without the memory for them the index still serves
+    const size_t ws = sizeof(IT) == 4 ? 8 : 16;
+    const size_t nw = trie_base(D + 1);
+    // the trie only saves rank steps: without the memory for it the index still serves
     // every search (rank steps only), so an allocation failure is not an error here
-    const bool got = hipMalloc(&ix->d_trie_w, nw * ws) == hipSuccess &&
-                     (!Ds || (hipMalloc(&ix->d_trie_s, ns * es) == hipSuccess &&
-                              hipMalloc(&ix->d_trie_m, trie_mbase(Ds) + 16) == hipSuccess));
-    if (!got) {
+    if (hipMalloc(&ix->d_trie_w, nw * ws) != hipSuccess) {
         (void)hipGetLastError();
-        (void)hipFree(ix->d_trie_w); (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m);
-        ix->d_trie_w = nullptr; ix->d_trie_s = nullptr; ix->d_trie_m = nullptr;
-        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] root tries: no device memory for them, rank steps only\n");
+        ix->d_trie_w = nullptr;
+        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] root trie: no device memory for it, rank steps only\n");
         return 0;
     }
     TrieC<IT> Cv;
@@ -277,9 +265,6 @@ static int build_tries_t(hsa_index *ix, RD fwd, RD rev, IT T, const IT *C)
     HSA_HIP(hipMemsetAsync(d_bad, 0, 4, ix->stream));
     for (uint32_t d = 0; d < D; ++d) {
         const unsigned nb = (unsigned)(((1ull << (2 * d)) + 255) / 256);
-        if (d < Ds)
-            hipLaunchKernelGGL((k_trie_search_level<IT, RD>), dim3(nb), dim3(256), 0, ix->stream, fwd, T, Cv, d,
-                               ix->d_trie_s, ix->d_trie_m, d_bad);
         hipLaunchKernelGGL((k_trie_width_level<IT, RD>), dim3(nb), dim3(256), 0, ix->stream, rev, T, Cv, d, ix->d_trie_w,
                            d_bad);
         HSA_HIP(hipGetLastError());
@@ -288,24 +273,21 @@ static int build_tries_t(hsa_index *ix, RD fwd, RD rev, IT T, const IT *C)
     HSA_HIP(hipStreamSynchronize(ix->stream));
     (void)hipFree(d_bad);
     if (bad) {                      // the two BWTs disagree: no trie (rank steps only)
-        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] root tries: intervals past the text, not kept\n");
-        (void)hipFree(ix->d_trie_w); (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m);
-        ix->d_trie_w = nullptr; ix->d_trie_s = nullptr; ix->d_trie_m = nullptr;
+        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] root trie: intervals past the text, not kept\n");
+        (void)hipFree(ix->d_trie_w);
+        ix->d_trie_w = nullptr;
         return 0;
     }
     ix->trie_depth = D;
-    ix->trie_sdepth = Ds;
     ix->trie_wide = sizeof(IT) == 8;
-    ix->trie_bytes = nw * ws + ns * es + (Ds ? trie_mbase(Ds) : 0);
+    ix->trie_bytes = nw * ws;
     return 0;
 }
 
 static int build_tries(hsa_index *ix)
 {
-    if (ix->wide)
-        return build_tries_t<uint64_t, RankDir64>(ix, hsa_rank_dir64(ix, 0), hsa_rank_dir64(ix, 1), ix->T64, ix->C64);
-    return build_tries_t<uint32_t, RankDir>(ix, RankDir{ix->blk[0], ix->isa0}, RankDir{ix->blk[1], ix->risa0}, ix->T,
-                                            ix->C);
+    if (ix->wide) return build_tries_t<uint64_t, RankDir64>(ix, hsa_rank_dir64(ix, 1), ix->T64, ix->C64);
+    return build_tries_t<uint32_t, RankDir>(ix, RankDir{ix->blk[1], ix->risa0}, ix->T, ix->C);
 }
 
 int hsa_need32(const hsa_index *ix)
@@ -431,9 +413,8 @@ extern "C" int hsa_index_clone(hsa_index_t *src, hsa_index_t **out)
     ix->rT64 = root->rT64; ix->risa0_64 = root->risa0_64; memcpy(ix->rC64, root->rC64, sizeof ix->rC64);
     ix->d_sa = root->d_sa; ix->d_blocks = root->d_blocks;
     ix->sa_interval = root->sa_interval; ix->n_blocks = root->n_blocks;
-    ix->d_wsa = root->d_wsa; ix->d_wisa = root->d_wisa; ix->d_wtext = root->d_wtext;
-    ix->d_trie_s = root->d_trie_s; ix->d_trie_m = root->d_trie_m; ix->d_trie_w = root->d_trie_w;
-    ix->trie_depth = root->trie_depth; ix->trie_sdepth = root->trie_sdepth;
+    ix->d_trie_w = root->d_trie_w;
+    ix->trie_depth = root->trie_depth;
     ix->trie_wide = root->trie_wide; ix->trie_bytes = root->trie_bytes;
     ix->parent = root;
     ++root->n_clones;
@@ -464,8 +445,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
         if (--ix->parent->n_clones == 0 && ix->parent->free_pending) orphan = ix->parent;
         ix->blk_base[0] = ix->blk_base[1] = nullptr;
         ix->d_sa = ix->d_blocks = nullptr;
-        ix->d_wsa = ix->d_wisa = ix->d_wtext = nullptr;
-        ix->d_trie_s = nullptr; ix->d_trie_m = nullptr; ix->d_trie_w = nullptr;
+        ix->d_trie_w = nullptr;
     }
     (void)hipFree(ix->blk_base[0]); (void)hipFree(ix->blk_base[1]);
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big); hsa_scratch_free(ix->huge);
@@ -479,8 +459,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (ix->h_pf) (void)hipHostFree(ix->h_pf);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
     (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
-    (void)hipFree(ix->d_trie_s); (void)hipFree(ix->d_trie_m); (void)hipFree(ix->d_trie_w);
-    (void)hipFree(ix->d_wsa); (void)hipFree(ix->d_wisa); (void)hipFree(ix->d_wtext);
+    (void)hipFree(ix->d_trie_w);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
     if (ix->evm) (void)hipEventDestroy(ix->evm);
@@ -500,7 +479,7 @@ extern "C" int hsa_index_is64(const hsa_index_t *ix) { return ix->is64 ? 1 : 0; 
 extern "C" int hsa_index_trie(const hsa_index_t *ix, uint32_t *depth, uint32_t *sdepth, size_t *bytes)
 {
     if (depth) *depth = ix->trie_depth;
-    if (sdepth) *sdepth = ix->trie_sdepth;
+    if (sdepth) *sdepth = 0;                   // no search trie (hsa_trie.h)
     if (bytes) *bytes = ix->trie_bytes;
     return 0;
 }

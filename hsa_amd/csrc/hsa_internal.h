@@ -70,16 +70,11 @@ struct hsa_index {
     // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;
-    // the unique-interval walk (hsa_index_build_walk): full SA, its inverse, packed text
-    uint32_t *d_wsa = nullptr, *d_wisa = nullptr, *d_wtext = nullptr;
     uint64_t *d_ctr = nullptr;
-    // root tries (hsa_trie.h): every string of up to trie_depth characters; built with
-    // the index's interval width (trie_wide: 64-bit entries), 0 = none
-    uint4 *d_trie_s = nullptr;          // search trie entries (levels 1..D)
-    uint8_t *d_trie_m = nullptr;        // search trie child masks (levels 0..D-1)
-    void *d_trie_w = nullptr;           // width trie entries (levels 1..D)
-    uint32_t trie_depth = 0;            // width trie levels
-    uint32_t trie_sdepth = 0;           // search trie levels (0: not built)
+    // the root width trie (hsa_trie.h): every string of up to trie_depth characters;
+    // built with the index's interval width (trie_wide: 64-bit entries), 0 = none
+    void *d_trie_w = nullptr;           // entries of levels 1..D
+    uint32_t trie_depth = 0;
     bool trie_wide = false;
     size_t trie_bytes = 0;
     unsigned char staged[1280];         // last regime block copied to d_in (skip identical re-copies)
@@ -95,7 +90,7 @@ struct hsa_index {
     uint64_t pev_n = 0;
     hipEvent_t ev_split = nullptr;      // recorded by launch_pass between k_widths and k_search
     // hsa_index_clone: a clone shares the parent's read-only device arrays (rank blocks
-    // and wrap tables, tries, SA, walk arrays) and owns its stream, events and scratch
+    // and wrap tables, tries, SA) and owns its stream, events and scratch
     hsa_index *parent = nullptr;
     int n_clones = 0;                   // live clones of this index
     bool free_pending = false;          // hsa_index_free called while clones were live

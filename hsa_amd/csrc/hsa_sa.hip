@@ -129,93 +129,3 @@ extern "C" int hsa_sa_position_batch(hsa_index_t *ix, size_t n, const uint32_t *
     return 0;
 }
 
-// ---------------------------------------------------------------- unique-interval walk
-// k_search walks an interval that holds one suffix (k = l) against the text: the
-// suffix's position p = SA[k], the read's next bases against text[p - 1], text[p - 2],
-// ..., and the row of the last matched suffix ISA[p - t] -- three loads for a run of t
-// steps the reference makes one rank pair at a time (the run's rev_k is unchanged: one
-// suffix's reverse interval does not move).  Those arrays are built here.
-
-// SA[r] of every row from the sampled SA by LF walks (BWTSaValue, BWT.c:1195-1220), with
-// the rows the reference cannot answer exactly made exact: row 0 (the '$' suffix) is T,
-// and a walk reaching the row of suffix 0 (inverseSa0) stops there (the sampled
-// sa[0] is -1 as BWTLoad leaves it, BWT.c:222).
-__global__ void __launch_bounds__(256) k_walk_sa(SaArgs a, uint32_t T, uint32_t *sa_full)
-{
-    const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r > T) return;
-    uint32_t v = T;
-    if (r > 0) {
-        uint32_t idx = (uint32_t)r, s = 0;
-        for (;;) {
-            if (idx == a.isa0) { v = s; break; }
-            if (idx % a.interval == 0) { v = a.sa[idx / a.interval] + s; break; }
-            idx = psi_minus(a, idx);
-            ++s;
-        }
-    }
-    sa_full[r] = v;
-}
-
-__global__ void __launch_bounds__(256) k_walk_isa(const uint32_t *sa_full, uint32_t T, uint32_t *isa)
-{
-    const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r <= T) isa[sa_full[r]] = (uint32_t)r;
-}
-
-// text[p - 1] = the BWT character of the row whose suffix starts at p (LSB-first 2-bit)
-__global__ void __launch_bounds__(256) k_walk_text(const uint32_t *sa_full, const uint4 *blk, uint32_t isa0, uint32_t T,
-                                                   uint32_t *text)
-{
-    const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r > T || r == isa0) return;
-    const uint32_t p = sa_full[r];
-    if (p == 0) return;
-    const uint32_t b = (uint32_t)r - ((uint32_t)r > isa0);       // the $-less BWT position of row r
-    const uint32_t c = (blk[b >> 4].w >> (2u * (b & 15u))) & 3u;
-    if (c) atomicOr(&text[(p - 1u) >> 4], c << (2u * ((p - 1u) & 15u)));
-}
-
-extern "C" int hsa_index_build_walk(hsa_index_t *ix, const uint32_t *d_sa_full, const uint32_t *d_text_lsb)
-{
-    if (int rc0 = hsa_need32(ix)) return rc0;
-    if (ix->wide) { hsa_set_error("hsa_index_build_walk: 32-bit indexes only"); return HSA_E_ARG; }
-    if (int rc0 = hsa_need_unshared(ix, "hsa_index_build_walk")) return rc0;
-    if (!d_sa_full && !ix->d_sa) { hsa_set_error("hsa_index_build_walk: no suffix array (hsa_index_set_sa)"); return HSA_E_ARG; }
-    HSA_HIP(hipSetDevice(ix->device));
-    (void)hipFree(ix->d_wsa); (void)hipFree(ix->d_wisa); (void)hipFree(ix->d_wtext);
-    ix->d_wsa = ix->d_wisa = ix->d_wtext = nullptr;
-    const uint32_t T = ix->T;
-    const size_t n = (size_t)T + 1, nw = ((size_t)T + 15) / 16 + 4;
-    if (hipMalloc(&ix->d_wsa, n * 4) != hipSuccess || hipMalloc(&ix->d_wisa, n * 4) != hipSuccess ||
-        hipMalloc(&ix->d_wtext, nw * 4) != hipSuccess) {
-        (void)hipFree(ix->d_wsa); (void)hipFree(ix->d_wisa); (void)hipFree(ix->d_wtext);
-        ix->d_wsa = ix->d_wisa = ix->d_wtext = nullptr;
-        hsa_set_error("hsa_index_build_walk: %zu bytes of device memory", n * 8 + nw * 4);
-        return HSA_E_MEM;
-    }
-    hipStream_t st = ix->stream;
-    const unsigned g = (unsigned)((n + 255) / 256);
-    if (d_sa_full) {
-        HSA_HIP(hipMemcpyAsync(ix->d_wsa, d_sa_full, n * 4, hipMemcpyDeviceToDevice, st));
-        HSA_HIP(hipMemcpyAsync(ix->d_wsa, &T, 4, hipMemcpyHostToDevice, st));   // row 0: the '$' suffix
-    } else {
-        SaArgs A;
-        A.blk = ix->blk[0]; A.isa0 = ix->isa0;
-        memcpy(A.C, ix->C, sizeof A.C);
-        A.sa = ix->d_sa; A.interval = ix->sa_interval; A.blocks = nullptr; A.n_blocks = 0;
-        A.idx = nullptr; A.out = nullptr; A.n = 0;
-        hipLaunchKernelGGL(k_walk_sa, dim3(g), dim3(256), 0, st, A, T, ix->d_wsa);
-    }
-    hipLaunchKernelGGL(k_walk_isa, dim3(g), dim3(256), 0, st, ix->d_wsa, T, ix->d_wisa);
-    if (d_text_lsb) {
-        HSA_HIP(hipMemsetAsync(ix->d_wtext, 0, nw * 4, st));
-        HSA_HIP(hipMemcpyAsync(ix->d_wtext, d_text_lsb, ((size_t)T + 15) / 16 * 4, hipMemcpyDeviceToDevice, st));
-    } else {
-        HSA_HIP(hipMemsetAsync(ix->d_wtext, 0, nw * 4, st));
-        hipLaunchKernelGGL(k_walk_text, dim3(g), dim3(256), 0, st, ix->d_wsa, ix->blk[0], ix->isa0, T, ix->d_wtext);
-    }
-    HSA_HIP(hipGetLastError());
-    HSA_HIP(hipStreamSynchronize(st));
-    return 0;
-}

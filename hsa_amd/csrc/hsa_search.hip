@@ -879,7 +879,13 @@ extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *se
         return rc;
     hipLaunchKernelGGL(k_pf_anchors, dim3((unsigned)((2 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
     HSA_HIP(hipGetLastError());
-    if ((rc = mg_passes(ix, d_reg, d_bmap, nb, A.jobs, A.list + 6 * N, acnt, (int)(2 * N), 12,
+    // the anchors' pass is planned for the anchors there are (a gapped regime's pool per
+    // lane is large: planning for all 2 n strands would size the scratch for them)
+    unsigned long long n_anchor = 0;
+    HSA_HIP(hipMemcpyAsync(&n_anchor, acnt, 8, hipMemcpyDeviceToHost, st));
+    HSA_HIP(hipStreamSynchronize(st));
+    if (n_anchor &&
+        (rc = mg_passes(ix, d_reg, d_bmap, nb, A.jobs, A.list + 6 * N, acnt, (int)n_anchor, 12,
                         anchor_rg->max_gapo > 0, wide, anchor_rg->max_entries, A.scodes, mgp, A.call_n, A.call_fl,
                         (uint64_t *)(dq + q_ho), (uint32_t *)(dq + q_ha), cap_a, ctr_a, st)))
         return rc;

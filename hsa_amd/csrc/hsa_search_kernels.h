@@ -55,11 +55,8 @@
 #define BLOCK 256
 #define MAXB 128          // dense buckets per regime (BMask<2>)
 #define MAXS 512          // score table length per regime (n_stacks <= MAXS)
-#ifndef HSA_CTL_LOOP
-#define HSA_CTL_LOOP 0    // 1: loop the control code until every lane needs a rank step
-#endif
 
-enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END, PH_WALK, PH_WEXP };
+enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END };
 
 struct SearchArgs {
     RankDir fwd, rev;
@@ -118,15 +115,11 @@ struct SearchArgs {
     int32_t *sp_n;                 // per item: hits, or -1 for a capacity overflow
     uint64_t *sp_off;
     uint32_t *sp_q, *sp_p;         //   its rank queries and pops (counted by the finalize)
-    // root tries (hsa_trie.h) of the index, ktd levels (0: none, or not of this
-    // instantiation's interval width): k_search (ungapped regimes) answers the steps of
-    // strings up to ktd characters from kts / ktm, k_widths from ktw
-    const uint4 *kts;
-    const uint8_t *ktm;
+    // the root width trie (hsa_trie.h) of the index, ktd levels (0: none, or not of this
+    // instantiation's interval width): k_widths answers the steps of strings up to ktd
+    // characters from ktw
     const void *ktw;
-    uint32_t ktd;                  // width trie levels
-    uint32_t ksd;                  // search trie levels k_search uses (0: none)
-    uint32_t kjm;                  // characters an exact tail jumps per trie load
+    uint32_t ktd;
     // cost order (main pass of a batch larger than the chip): k_widths writes each row's
     // final bid (wkey), k_order_* sort the list positions by it, most differences first,
     // and k_search takes its reads in that order (perm), so the costly searches do not
@@ -144,12 +137,6 @@ struct SearchArgs {
     // forward row (when computed) at row rmap[q], so every width lane stores coalesced;
     // null: row q * 2 + strand
     int32_t *rmap;
-    // unique-interval walk (ungapped 32-bit searches, hsa_index_build_walk): the full
-    // suffix array, its inverse and the packed text; a node whose interval holds one
-    // suffix (k = l) and at least wmin positions still to match
-    const uint32_t *wsa, *wisa, *wtext;
-    uint32_t wmin;
-    uint32_t wstreak;              // ... reached by at least this many one-suffix match steps in a row
 };
 
 // The kernel's arguments re-read from the kernarg segment where a rare path uses them
@@ -219,20 +206,8 @@ template <typename IT> struct Ent {
     IT x, y, z;
     uint32_t w;
 };
-// The search trie in k_search (hsa_trie.h; ungapped regimes): measured slower than the
-// rank steps it replaces, so compiled only into experiment builds
-// (tools/build_variant.sh strie -DHSA_SEARCH_TRIE=1); k_widths' width trie is always in.
-#ifndef HSA_SEARCH_TRIE
-#define HSA_SEARCH_TRIE 0
-#endif
 #ifndef HSA_WAVES_SIMD
 #define HSA_WAVES_SIMD 4      // k_search's launch bound: waves per SIMD its VGPRs must allow
-#endif
-// The unique-interval walk (PH_WALK; hsa_index_build_walk): bit-exact, measured slower
-// than the rank steps it replaces, so compiled only into experiment builds
-// (tools/build_variant.sh walk -DHSA_UNIQUE_WALK=1).
-#ifndef HSA_UNIQUE_WALK
-#define HSA_UNIQUE_WALK 0
 #endif
 #ifndef HSA_POOL_CHUNK
 #define HSA_POOL_CHUNK 1
@@ -826,7 +801,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     E e{0, 0, 0, 0};
     // per-lane statistics (a lane's counts of one launch stay far below 2^32); kept in
     // VGPRs: wave-uniform accumulators pushed the kernel's SGPRs into spills
-    uint32_t st_p = 0, st_wq = 0, st_q = 0, st_b = 0, st_t = 0;
+    uint32_t st_p = 0, st_wq = 0, st_q = 0, st_b = 0;
     uint32_t sq0 = 0, sp0 = 0;            // split mode: the counters when the item started
     const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
 #ifdef HSA_DIAG
@@ -866,12 +841,6 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     // step needs, loaded in the control phase so that its latency overlaps the rank load
     const uint8_t *rowp = nullptr;
     uint32_t cur_c = 0;
-    // the walk of a unique interval (PH_WALK): stage 0 the suffix's text position SA[k],
-    // 1 text chunks compared with the read, 2 the row ISA[p] of the last matched suffix;
-    // ik = the current suffix's text position, il = positions matched
-    constexpr bool WALK = HSA_UNIQUE_WALK && !GAPS && sizeof(IT) == 4 && !F::NIB;
-    uint32_t wstage = 0;
-    uint32_t wstreak = 0;          // one-suffix match steps in a row (virtual tops): the walk's trigger
     // base of the current strand's sequence at p (from the LDS element, or the HBM row)
     auto getc = [&](int p) -> uint32_t {
         if constexpr (F::NIB) return WFmt<uint8_t>::code(rowp[((uint32_t)p >> 2) * 256u + ((uint32_t)p & 3u)]);
@@ -898,12 +867,6 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         ent_store<IT>(a.pool, pbase, slot, v);
         const uint32_t old = mask.test(b) ? (uint32_t)HEAD(b) : NIL;
         NXT(slot) = (LT)old;
-#ifdef HSA_X_LINKSTORE2      // sensitivity experiment only: one more link store per push (into
-        if (!HUGE && pool_top < a.pcap) NXT(pool_top) = (LT)old;   // the next free slot: harmless)
-#endif
-#ifdef HSA_X_ENTSTORE2       // sensitivity experiment only: one more entry store per push
-        if (!HUGE && pool_top < a.pcap) ent_store<IT>(a.pool, pbase, pool_top, v);
-#endif
         HEAD(b) = (LT)slot;
         mask.set(b);
     };
@@ -961,18 +924,6 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 __builtin_amdgcn_global_load_lds(ss + q * 64, ds + q * NT, 4, 0, 0);
         }
         }
-#ifdef HSA_EXTRA_LOADS
-        // experiment only: HSA_EXTRA_LOADS random 16-byte rank-table loads per strand
-        // start, to test whether k_search's time follows its memory request count
-        {
-            uint32_t acc = 0, h = qpos * 2654435761u + C_STRAND(ctl);
-            for (int x = 0; x < HSA_EXTRA_LOADS; ++x) {
-                h = h * 1664525u + 1013904223u;
-                acc += a.fwd.blk[h % (a.T >> 4)].w;
-            }
-            if (acc == 0x9e3779b9u) a.ctr[15] = acc;
-        }
-#endif
         __builtin_amdgcn_s_waitcnt(0);                 // the DMA writes are visible to LDS reads
         DC(15);
         start_search();
@@ -1213,24 +1164,16 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         TMARK(0);
 #endif
         // ---------------- (B) control until a rank step is needed
-        // req: 1 rank pair at rp1, rp2; from the root trie (ungapped regimes, nodes of
-        // fewer than ktd characters, which hold their trie node in e.x): 2 an exact tail's
-        // jump (entry rp1; tq = characters | N-stop << 8 | depth << 9), 3 an expansion's
-        // child mask (byte rp1), 4 an expansion's four children at the last level (rp1..+3)
+        // req: 1 a rank pair at rp1, rp2
         int req = 0;
         IT rp1 = 0, rp2 = 0;
-        uint32_t tq = 0;
 #ifdef HSA_DIAG
         if (lane == 0) DC(5);
 #endif
-        // One control pass per iteration (HSA_CTL_LOOP=0): a lane whose pop needs no
-        // rank step (pruned, hit, strand change) just skips this iteration's step
-        // instead of making the whole wave run the control code again.
-#if HSA_CTL_LOOP
-        while (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END && !req) {
-#else
+        // One control pass per iteration: a lane whose pop needs no rank step (pruned,
+        // hit, strand change) just skips this iteration's step instead of making the whole
+        // wave run the control code again.
         if (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END) do {
-#endif
 #ifdef HSA_DIAG
             { const uint64_t em = __ballot(1); if (lane == __ffsll((unsigned long long)em) - 1) DC(7); }
 #endif
@@ -1240,25 +1183,6 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 break;
             }
             const uint32_t ph = C_PH(ctl);
-            if constexpr (WALK) {
-                if (ph == PH_WALK) {
-                    req = 5 + (int)wstage;                                // SA[k], a text chunk, ISA[p]
-                    rp1 = wstage == 0 ? e.x : ik;
-                    break;
-                }
-                if (ph == PH_WEXP) {
-                    // the walk's last matched node (popped as the run's last virtual top): a
-                    // hit at position 0 (bwtgap.c:176), else its expansion's rank step
-                    if (M_I(e.w) == 0) {
-                        SET_PH(ctl, PH_POP);
-                        if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
-                        continue;
-                    }
-                    req = 1; rp1 = e.x; rp2 = e.y + 1u;
-                    SET_PH(ctl, PH_EXPAND);
-                    break;
-                }
-            }
             if (ph == PH_EXACT) {
                 if constexpr (F::NIB) {
                     // the rank step goes out with the base load; an N (c > 3) drops it in (D)
@@ -1278,15 +1202,11 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 ctl &= ~(1u << 6);                                        // e already holds it
             } else {
                 DC(4);
-                wstreak = 0;
                 // pop the head of the lowest non-empty bucket
                 const int b = mask.lowest();
                 const uint32_t slot = HEAD(b);
                 e = ent_load<IT>(a.pool, pbase, slot);
                 const uint32_t nx = NXT(slot);
-#ifdef HSA_X_POPLOAD2        // sensitivity experiment only: one more link load per pool pop
-                if (*(volatile LT *)&NXT(slot) == (LT)0xFFFE && nx == 0x12345u) e.w ^= 1u;
-#endif
                 if (nx == NIL) mask.reset(b);
                 else HEAD(b) = (LT)nx;
                 if (HUGE) { NXT(slot) = (LT)free_head; free_head = slot; }
@@ -1306,57 +1226,15 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
                 continue;
             }
-            // a trie node: ungapped, the strand longer than the trie (so no trie node is
-            // ever a hit), fewer than ktd characters matched
-            const uint32_t dep = (uint32_t)(C_LEN(ctl) - ei);
-            const bool tn = HSA_SEARCH_TRIE && !GAPS && (uint32_t)C_LEN(ctl) > a.ksd && dep < a.ksd;
             if (em == 0 && (M_ST(m) == ST_M || (R_MODE & MODE_GAPE) || M_GE(m) == R_MAXGE)) {
-                if (tn) {
-                    // bwt_match_exact from a trie node: the read's next bases down to the
-                    // trie's last level (or to an N) in one load
-                    const uint32_t jm = a.ksd - dep < a.kjm ? a.ksd - dep : a.kjm;
-                    uint32_t idx = e.x, j = 0;
-                    bool nstop = false;
-#pragma unroll
-                    for (uint32_t t = 0; t < HSA_TRIE_MAX_DEPTH; ++t) {
-                        if (t < jm && !nstop) {
-                            const uint32_t c = getc(ei - 1 - (int)t);
-                            if (c > 3) nstop = true;
-                            else { idx = idx * 4u + c; ++j; }
-                        }
-                    }
-                    if (j == 0) continue;                                 // an N first (2BWT-Interface.c:377)
-                    req = 2; rp1 = (IT)(trie_base(dep + j) + idx);
-                    tq = j | (nstop ? 256u : 0u) | dep << 9;
-                    SET_PH(ctl, PH_EXACT);
-                    break;
-                }
                 ik = e.x; il = e.y; aux = e.z + (e.y - e.x); pos = (uint32_t)(ei - 1);   // bwt_match_exact
                 SET_PH(ctl, PH_EXACT);
                 continue;
             }
-            if constexpr (WALK) {
-                // a unique interval (one suffix) with enough read left: walk it against the
-                // text instead of one rank step per matched position
-                if (e.x == e.y && cold_args()->wsa && wstreak >= cold_args()->wstreak && (uint32_t)ei >= cold_args()->wmin) {
-                    wstage = 0;
-                    req = 5; rp1 = e.x;
-                    SET_PH(ctl, PH_WALK);
-                    break;
-                }
-            }
-            if (tn) {
-                req = dep + 1u < a.ksd ? 3 : 4;
-                rp1 = (IT)(req == 3 ? trie_mbase(dep) + e.x : trie_base(a.ksd) + 4ull * e.x);
-            } else {
-                req = 1; rp1 = e.x; rp2 = e.y + 1u;
-            }
+            req = 1; rp1 = e.x; rp2 = e.y + 1u;
             if constexpr (F::NIB) cur_c = getc(ei - 1);                  // the expansion's base (D)
             SET_PH(ctl, PH_EXPAND);
-        }
-#if !HSA_CTL_LOOP
-        while (0);
-#endif
+        } while (0);
 
 #ifdef HSA_DIAG
         TMARK(1);
@@ -1373,35 +1251,9 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         }
 #endif
         uint32_t two = 0;
-        IT rkt[4];
-        uint32_t tL = 0, tm = 0;
         if (req == 1) {
             two = occ_pair(Ix<IT>::fwd(a), rp1, rp2, oa, ob) - 1u;
             st_q += 2u; st_b += 1u + two;
-        } else if (req == 2) {
-            trie_s_load<IT>(a.kts, (uint64_t)rp1, oa[0], ob[0], rkt[0], tL);
-            ++st_t;
-        } else if (req == 3) {
-            tm = a.ktm[(uint64_t)rp1];
-            st_q += 2u; ++st_t;
-        } else if (req == 4) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) trie_s_load<IT>(a.kts, (uint64_t)rp1 + c, oa[c], ob[c], rkt[c], tL);
-            st_q += 2u; ++st_t;
-        }
-        uint32_t wv = 0, wt0 = 0, wt1 = 0, wt2 = 0;
-        if constexpr (WALK) {
-            if (req == 5 || req == 7) {
-                const ColdArgs r = cold_args();
-                wv = (req == 5 ? r->wsa : r->wisa)[(uint32_t)rp1];
-            } else if (req == 6) {
-                // the text words of positions [ik - 48, ik): the next 32 characters before ik
-                const uint32_t *tx = cold_args()->wtext;
-                const uint32_t wb = ((uint32_t)rp1 - 1u) >> 4;
-                wt2 = tx[wb];
-                wt1 = wb >= 1 ? tx[wb - 1] : 0u;
-                wt0 = wb >= 2 ? tx[wb - 2] : 0u;
-            }
         }
 
 #ifdef HSA_DIAG
@@ -1410,65 +1262,9 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
 #endif
         // ---------------- (D) apply
         const uint32_t ph = C_PH(ctl);
-        if (WALK && req == 5) {
-            ik = wv; il = 0;                                             // the suffix's text position
-            if (ik == 0) SET_PH(ctl, PH_WEXP);                           // nothing before it ('$')
-            else wstage = 1;
-        } else if (WALK && req == 6) {
-            // compare the read's next bases with the text before the suffix, up to 32
-            const uint32_t np = (uint32_t)M_I(e.w) - il, q = ik;
-            uint32_t m = np < q ? np : q;
-            m = m < 32u ? m : 32u;
-            const uint32_t wb = (q - 1u) >> 4;
-            const int em = m_of(e.w);
-            uint32_t tm = 0;
-            bool pruned = false;
-            for (; tm < m; ++tm) {
-                const uint32_t tp = q - 1u - tm, d = wb - (tp >> 4);
-                const uint32_t tw = d == 0 ? wt2 : d == 1 ? wt1 : wt0;
-                const uint32_t tc = (tw >> (2u * (tp & 15u))) & 3u;
-                if (getc((int)(np - 1u - tm)) != tc) break;              // an N (> 3) never matches
-                // the matched child is the next pop: pruned when gap_shadow has raised a
-                // bid it reads (bwtgap.c:170), and the run ends with it
-                const int cp = (int)(np - 1u - tm);
-                if (cp > 0 && em < (int)(wbg(cp - 1) & F::BIDM)) { pruned = true; ++tm; break; }
-            }
-            il += tm; ik -= tm;
-            if (pruned) {
-                st_q += 2u * il; st_b += il; st_p += il;                 // its expansions and pops, the last pruned
-                SET_PH(ctl, PH_POP);
-            } else if (tm == 32u && np > 32u && q > 32u) {
-                // every one matched: the next chunk
-            } else if (il == 0) {
-                SET_PH(ctl, PH_WEXP);                                    // no match: the node's own expansion
-            } else {
-                wstage = 2;                                              // the row of the last matched suffix
-            }
-        } else if (WALK && req == 7) {
-            // il matched positions: il expansions (two rank queries each) and il virtual-top
-            // pops the reference makes; the node il positions on, one suffix at row ISA[p]
-            st_q += 2u * il; st_b += il; st_p += il;
-            e = E{(IT)wv, (IT)wv, e.z, meta_pack((uint32_t)M_I(e.w) - il, ST_M, 0u, (uint32_t)M_MM(e.w), 0u, 0u)};
-            SET_PH(ctl, PH_WEXP);
-        } else if (F::NIB && req == 1 && ph == PH_EXACT && cur_c > 3) {
+        if (F::NIB && req == 1 && ph == PH_EXACT && cur_c > 3) {
             st_q -= 2u; st_b -= 1u + two;                                // not a step (2BWT-Interface.c:377)
             SET_PH(ctl, PH_POP);
-        } else if (req == 2) {
-            // the trie's exact jump: the steps bwt_match_exact takes until its interval
-            // empties (L) or it meets an N or the trie's last level; from there on, rank
-            // steps (PH_EXACT)
-            const uint32_t j = tq & 255u, dep = tq >> 9;
-            st_q += 2u * (tL ? tL - dep : j);
-            if (tL || (tq & 256u)) {
-                SET_PH(ctl, PH_POP);
-            } else {
-                ik = oa[0]; il = ob[0]; aux = rkt[0] + (ob[0] - oa[0]);
-                pos = (uint32_t)M_I(e.w) - 1u - j;
-                // the write-back guard (2BWT-Interface.c:383-386) reads the start entry's
-                // k, l, rev_k, rev_l: of a node, only the root's k and rev_k are zero
-                if (dep == 0) { e.x = 0; e.y = TT; e.z = 0; }
-                else { e.x = 1; e.y = 1; e.z = 1; }
-            }
         } else if (req && ph == PH_EXACT) {
             // BWTSARangeBackward_Bidirection (2BWT-Interface.c:135-170), one character
             const uint32_t c = F::NIB ? cur_c : getc((int)pos);
@@ -1499,7 +1295,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             const int len = C_LEN(ctl);
             IT srk[4];
             uint32_t ne = 0;                                             // children that occur
-            if (req == 1) {
+            {
                 IT oc = 0;
 #pragma unroll
                 for (int c = 3; c >= 0; --c) {
@@ -1509,19 +1305,9 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                     srk[c] = (erl - oc) - (ob[c] - oa[c]);
                     oc += d;
                 }
-            } else if (req == 3) {
-                // children of fewer than ktd characters: trie nodes 4 idx + c
-#pragma unroll
-                for (int c = 0; c < 4; ++c) { oa[c] = ek * 4u + (IT)c; ob[c] = 0; srk[c] = 0; }
-                ne = tm;
-            } else {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) srk[c] = rkt[c];
             }
-            if (req != 3) {
 #pragma unroll
-                for (int c = 0; c < 4; ++c) ne |= (oa[c] <= ob[c] ? 1u : 0u) << c;
-            }
+            for (int c = 0; c < 4; ++c) ne |= (oa[c] <= ob[c] ? 1u : 0u) << c;
             int allow_diff = 1, allow_M = 1;
             if (i > 0) {
                 // width[i-1].bid, width[i].bid and w[i-1] == w[i] (bwtgap.c:256-258)
@@ -1599,8 +1385,6 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 if (bk <= mask.lowest()) { e = v; ctl |= 1u << 6; }
                 else flush(v, bk);
             }
-            if constexpr (WALK)     // a one-suffix node whose match child is the next pop
-                wstreak = (ek == el && C_VT(ctl) && !M_ISD(e.w)) ? wstreak + 1u : 0u;
             SET_PH(ctl, PH_POP);
         }
 #ifdef HSA_DIAG
@@ -1623,7 +1407,6 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     atomicAdd(&a.ctr[2], (unsigned long long)st_q);
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);
-    if (st_t) atomicAdd(&a.ctr[10], (unsigned long long)st_t);
     if (st_wq) {
         atomicAdd(&a.ctr[2], (unsigned long long)st_wq);
         atomicAdd(&a.ctr[7], (unsigned long long)st_wq);
@@ -1936,23 +1719,10 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.split = 0; A.sp_n = nullptr; A.sp_off = nullptr; A.sp_q = nullptr; A.sp_p = nullptr;
     const char *te = getenv("HSA_TRIE");           // HSA_TRIE=0: rank steps only (A/B runs)
     const bool tr = ix->trie_depth > 0 && ix->trie_wide == (sizeof(IT) == 8) && !(te && atoi(te) == 0);
-    A.kts = tr ? ix->d_trie_s : nullptr;
-    A.ktm = tr ? ix->d_trie_m : nullptr;
     A.ktw = tr ? ix->d_trie_w : nullptr;
     A.ktd = tr ? ix->trie_depth : 0u;
-    // the search trie (built only on request, HSA_TRIE_MODE >= 1 at index creation;
-    // HSA_TRIE_MODE=0 at search time turns it off again, 2 = one level per exact step)
-    const char *tm = getenv("HSA_TRIE_MODE");
-    const int mode = tm ? atoi(tm) : 1;
-    A.ksd = tr && mode ? ix->trie_sdepth : 0u;
-    A.kjm = mode == 2 ? 1u : HSA_TRIE_MAX_DEPTH;
     A.wkey = nullptr; A.perm = nullptr; A.okey = 0;
     A.fwd_list = nullptr; A.fwd_n = nullptr; A.fwd_only = 0; A.rmap = nullptr;
-    const char *we = getenv("HSA_WALK");          // HSA_WALK=0: rank steps only (A/B runs)
-    const bool walk = sizeof(IT) == 4 && ix->d_wsa && !(we && atoi(we) == 0);
-    A.wsa = walk ? ix->d_wsa : nullptr; A.wisa = walk ? ix->d_wisa : nullptr; A.wtext = walk ? ix->d_wtext : nullptr;
-    A.wmin = getenv("HSA_WALK_MIN") ? (uint32_t)atoi(getenv("HSA_WALK_MIN")) : 8u;
-    A.wstreak = getenv("HSA_WALK_STREAK") ? (uint32_t)atoi(getenv("HSA_WALK_STREAK")) : 2u;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg)) : nullptr;

@@ -89,28 +89,18 @@ void hsa_index_free(hsa_index_t *ix);
 void *hsa_index_stream(const hsa_index_t *ix);
 size_t hsa_index_bytes(const hsa_index_t *ix);
 int  hsa_index_device(const hsa_index_t *ix);
-/* The index's root tries (hsa_amd/csrc/hsa_trie.h): every string of up to *depth
+/* The index's root width trie (hsa_amd/csrc/hsa_trie.h): every string of up to *depth
  * characters with the interval k_widths' forward extension computes for it (0: none;
- * HSA_TRIE_DEPTH at creation, default 12), and the search trie's levels (*sdepth; built
- * only when HSA_TRIE_MODE >= 1 at creation); *bytes of device memory they take.  Their
- * loads are counted in d_counters[10]. */
+ * HSA_TRIE_DEPTH at creation, default 12); *sdepth is 0 (k_search takes rank steps
+ * only); *bytes of device memory it takes.  Its loads are counted in d_counters[10]. */
 int  hsa_index_trie(const hsa_index_t *ix, uint32_t *depth, uint32_t *sdepth, size_t *bytes);
-/* The unique-interval walk of ungapped 32-bit searches (hsa_amd/csrc/hsa_sa.hip): the
- * full suffix array, its inverse and the packed forward text resident on the device
- * (about 8 T + T / 4 bytes), so that k_search matches a one-suffix interval against the
- * text instead of one rank pair per position (the same hits, rank-query and pop counts).
- * d_sa_full: device SA[r] for rows 1..T as hsa_build_bwt_index_device(sa_interval 1)
- * leaves it, or NULL to derive it from the sampled SA of hsa_index_set_sa; d_text_lsb:
- * the text as the builder takes it, or NULL to derive it from the SA and the BWT. */
-int  hsa_index_build_walk(hsa_index_t *ix, const uint32_t *d_sa_full, const uint32_t *d_text_lsb);
 /* A second handle on the same resident index, for passes that run concurrently: the
- * clone shares src's read-only device arrays (rank blocks, wrap tables, tries, SA, walk
- * arrays) and has its own stream, events and search scratch, so hsa_search_device on
+ * clone shares src's read-only device arrays (rank blocks, wrap tables, trie, SA) and
+ * has its own stream, events and search scratch, so hsa_search_device on
  * the two handles may overlap (the next batch's k_widths fills the last waves of this
  * one's k_search).  hsa_index_free(src) while clones are live defers the free of the
  * shared arrays to the last clone's hsa_index_free (src must not be used after it);
- * hsa_index_set_sa and hsa_index_build_walk refuse a clone and an index with live
- * clones.  No reference
+ * hsa_index_set_sa refuses a clone and an index with live clones.  No reference
  * counterpart: the reference searches one batch at a time (bwtaln.c:477, :506). */
 int  hsa_index_clone(hsa_index_t *src, hsa_index_t **out);
 

@@ -60,13 +60,6 @@ void hsa_index_free(hsa_index_t *ix)
 static uint32_t *g_sa_vals, *g_sa_blocks, g_sa_interval;
 static int g_sa_nblocks;
 
-/* the unique-interval walk changes no result: the CPU stand-in has nothing to build */
-int hsa_index_build_walk(hsa_index_t *ix, const uint32_t *d_sa_full, const uint32_t *d_text_lsb)
-{
-    (void)ix; (void)d_sa_full; (void)d_text_lsb;
-    return 0;
-}
-
 int hsa_index_set_sa(hsa_index_t *ix, const uint32_t *sa, uint64_t n, uint32_t interval, const uint32_t *blocks,
                      int n_blocks)
 {

@@ -152,8 +152,10 @@ def test_hg19_sized_clones_search_concurrently():
         torch.cuda.synchronize()
         np.testing.assert_array_equal(t["c"].cpu().numpy()[[1, 2, 4, 7, 8, 11]], g["c"][[1, 2, 4, 7, 8, 11]])
     # the shared arrays cannot be replaced under a clone
+    from hsa_amd import index_io
+    one = index_io.SaFile(interval=8, values=np.zeros(1, np.uint32))
     with pytest.raises(HsaError, match="clone"):
-        cl.build_walk()
+        cl.set_sa(one, np.zeros((0, 4), np.uint32))
     with pytest.raises(HsaError, match="clone"):
-        gi.build_walk()
+        gi.set_sa(one, np.zeros((0, 4), np.uint32))
     cl.close()

@@ -1,10 +1,8 @@
-"""The root tries (hsa_amd/csrc/hsa_trie.h): k_search answers the steps of strings
-shorter than the trie depth D from the search trie (ungapped regimes: expansions from
-the child masks and the last level, exact tails in one jump with the L field's step
-count), k_widths the first D steps after each reset from the width trie.  Every search
+"""The root width trie (hsa_amd/csrc/hsa_trie.h): k_widths answers the first D steps
+after each reset of bwt_cal_width's chain (bwtaln.c:84-97) from the trie.  Every search
 must equal the oracle's bit for bit -- hits, flags, pops and the rank-query count --
-whatever D, including tries far deeper than the text (most strings empty: the L
-accounting of exact tails that empty inside the trie) and D = 0 (no trie)."""
+whatever D, including tries far deeper than the text (most strings empty) and D = 0
+(no trie)."""
 import numpy as np
 import pytest
 
@@ -18,24 +16,19 @@ CASES = [("tiny_mm100_n4o0", None), ("tiny_exact36_n0", None), ("tiny_gap100_n4o
          ("rep_mm100_n4o1", "-n 4 -o 0"), ("tiny_edge_default", "-n 3 -o 0"), ("tiny_opts_seed", "-n 4 -o 0 -l 20 -k 1")]
 
 
-def _index(genome, depth, monkeypatch, mode=1):
-    """An index with width-trie depth `depth` and, for mode >= 1, a search trie of the
-    same depth (k_search uses it under the same HSA_TRIE_MODE)."""
+def _index(genome, depth, monkeypatch):
+    """An index with a width trie of `depth` levels."""
     from hsa_amd._lib import GpuIndex
     monkeypatch.setenv("HSA_TRIE_DEPTH", str(depth))
-    monkeypatch.setenv("HSA_TRIE_SDEPTH", str(depth))
-    monkeypatch.setenv("HSA_TRIE_MODE", str(mode))
     return GpuIndex(*index_io.read_index(INDEX[genome]))
 
 
-@pytest.mark.parametrize("depth,mode", [(0, 1), (3, 1), (9, 1), (12, 1), (9, 2), (12, 0)])
+@pytest.mark.parametrize("depth", [0, 3, 9, 12])
 @pytest.mark.parametrize("case,args", CASES)
-def test_trie_search_matches_oracle(case, args, depth, mode, monkeypatch):
-    """mode 1: both tries; 2: exact tails one trie level per step; 0: the width trie
-    only (the default)."""
+def test_trie_search_matches_oracle(case, args, depth, monkeypatch):
     from golden_io import load_case
     from test_gpu_parity import _device_run
-    ix = _index(load_case(case)["index"], depth, monkeypatch, mode)
+    ix = _index(load_case(case)["index"], depth, monkeypatch)
     got, (e_n, e_f, e_h, st) = _device_run(case, ix=ix, args=args)
     assert got["c"][11] == 0
     assert np.array_equal(got["f"] & 1, e_f & 1)
@@ -49,7 +42,7 @@ def test_trie_search_matches_oracle(case, args, depth, mode, monkeypatch):
     if depth == 0:
         assert got["c"][10] == 0
     else:
-        assert got["c"][10] > 0, "no step answered from the tries"
+        assert got["c"][10] > 0, "no step answered from the trie"
 
 
 def test_trie_off_switch(monkeypatch):
