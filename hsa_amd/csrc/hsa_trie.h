@@ -30,7 +30,7 @@
 
 #include "hsa_device.h"
 
-#define HSA_TRIE_MAX_DEPTH 13u
+#define HSA_TRIE_MAX_DEPTH 15u      // node numbers of a level stay below 2^32 (uint32_t)
 #define HSA_TRIE_DEFAULT_DEPTH 12u
 
 __host__ __device__ __forceinline__ uint64_t trie_base(uint32_t d) { return ((1ull << (2u * d)) - 4ull) / 3ull; }
