@@ -24,6 +24,21 @@
 #define HSA_BLK_CHARS 16u
 #define HSA_SECTOR_BLOCKS 4u   // 16-byte blocks per 64-byte sector (statistics)
 
+// v_c for a runtime base c in 0..3 as a select tree on the two bits of c.  The
+// equality chain c == 0 ? v0 : c == 1 ? v1 : ... was compiled into nested divergent
+// branches (an exec-mask save and restore per element) inside the search loops.
+template <typename V>
+__device__ __forceinline__ V hsa_sel4(uint32_t c, V v0, V v1, V v2, V v3)
+{
+#if HSA_PICK4_CHAIN                 // A/B builds only: the equality chain
+    return c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : v3;
+#else
+    const bool b0 = (c & 1u) != 0;
+    const V lo = b0 ? v1 : v0, hi = b0 ? v3 : v2;
+    return (c & 2u) ? hi : lo;
+#endif
+}
+
 struct RankDir {
     const uint4 *blk;
     uint32_t isa0;
@@ -69,7 +84,7 @@ __device__ __forceinline__ uint32_t hsa_occ1_q(const uint4 q, uint32_t p, uint32
     const uint32_t r = p & 15u;
     const uint32_t x = q.w ^ ~(c * 0x55555555u);
     const uint32_t n = __popc(x & (x >> 1) & 0x55555555u & ((1u << (2u * r)) - 1u));
-    const uint32_t base = c == 0 ? q.x : c == 1 ? q.y : c == 2 ? q.z : (p & ~15u) - q.x - q.y - q.z;
+    const uint32_t base = hsa_sel4(c, q.x, q.y, q.z, (p & ~15u) - q.x - q.y - q.z);
     return base + n;
 }
 
@@ -180,7 +195,7 @@ __device__ __forceinline__ uint64_t hsa_occ1_q64(const uint4 q, const RankDir64 
 {
     uint64_t o[4];
     hsa_occ4_q64(q, d, p, o);
-    return c == 0 ? o[0] : c == 1 ? o[1] : c == 2 ? o[2] : o[3];
+    return hsa_sel4(c, o[0], o[1], o[2], o[3]);
 }
 
 // The same interface as the 32-bit rank functions (k_search / k_widths are templated

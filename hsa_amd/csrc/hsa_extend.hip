@@ -83,7 +83,7 @@ __device__ __forceinline__ int ext_log2(uint32_t v)   // bwtgap.c:107-116
 
 template <typename V> __device__ __forceinline__ V pk4(const V v[4], uint32_t c)
 {
-    return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3];
+    return hsa_sel4<V>(c, v[0], v[1], v[2], v[3]);     // select tree (hsa_device.h)
 }
 
 __global__ void __launch_bounds__(EXT_NT) k_extend(ExtArgs a)

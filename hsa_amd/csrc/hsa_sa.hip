@@ -37,8 +37,8 @@ __device__ __forceinline__ uint32_t psi_minus(const SaArgs &a, uint32_t index)
     const uint32_t c = (q.w >> (2u * r)) & 3u;
     const uint32_t x = q.w ^ ~(c * 0x55555555u);
     const uint32_t n = __popc(x & (x >> 1) & 0x55555555u & ((1u << (2u * r)) - 1u));
-    const uint32_t base = c == 0 ? q.x : c == 1 ? q.y : c == 2 ? q.z : (p & ~15u) - q.x - q.y - q.z;
-    const uint32_t cc = c == 0 ? a.C[0] : c == 1 ? a.C[1] : c == 2 ? a.C[2] : a.C[3];
+    const uint32_t base = hsa_sel4(c, q.x, q.y, q.z, (p & ~15u) - q.x - q.y - q.z);
+    const uint32_t cc = hsa_sel4(c, a.C[0], a.C[1], a.C[2], a.C[3]);
     return cc + base + n + 1u;                 // ... and its count up to and including it
 }
 

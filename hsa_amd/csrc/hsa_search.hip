@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(BLOCK) k_seed_prep(SeedArgs a)
             uint32_t ok, ol;
             hsa_occ1_pair(a.rev, k, l + 1u, c, ok, ol);
             q += 2;
-            const uint32_t cc = c == 0 ? a.C[0] : c == 1 ? a.C[1] : c == 2 ? a.C[2] : a.C[3];
+            const uint32_t cc = hsa_sel4(c, a.C[0], a.C[1], a.C[2], a.C[3]);
             k = cc + ok + 1u;
             l = cc + ol;
         }
@@ -619,7 +619,7 @@ __global__ void __launch_bounds__(BLOCK) k_pf_rows(PfArgs a)
             if (c < 4) {
                 uint32_t ok, ol;
                 hsa_occ1_pair(a.rev, k, l + 1u, c, ok, ol);
-                const uint32_t cc = c == 0 ? a.C[0] : c == 1 ? a.C[1] : c == 2 ? a.C[2] : a.C[3];
+                const uint32_t cc = hsa_sel4(c, a.C[0], a.C[1], a.C[2], a.C[3]);
                 k = cc + ok + 1u;
                 l = cc + ol;
             }
@@ -637,7 +637,7 @@ __global__ void __launch_bounds__(BLOCK) k_pf_rows(PfArgs a)
         if (c < 4) {
             uint32_t ok, ol;
             hsa_occ1_pair(a.fwd, k, l + 1u, c, ok, ol);
-            const uint32_t cc = c == 0 ? a.C[0] : c == 1 ? a.C[1] : c == 2 ? a.C[2] : a.C[3];
+            const uint32_t cc = hsa_sel4(c, a.C[0], a.C[1], a.C[2], a.C[3]);
             k = cc + ok + 1u;
             l = cc + ol;
         }

@@ -176,12 +176,14 @@ __device__ __forceinline__ uint32_t meta_pack(uint32_t i, uint32_t st, uint32_t 
 #define C_SLEN(c) ((int)(((c) >> 20) & 1023u))
 #define SET_PH(c, p) ((c) = ((c) & ~7u) | (p))
 
-// v[c] for a runtime c in 0..3 as selects: a dynamically indexed register array
-// would be lowered through the private segment (scratch) of the dispatch.
+// v[c] for a runtime c in 0..3 as selects (hsa_sel4): a dynamically indexed register
+// array would be lowered through the private segment (scratch) of the dispatch.  The
+// elements are passed by value at constant indices (a select between two element
+// references became a dynamically indexed load).
 template <typename V>
 __device__ __forceinline__ V pick4(const V v[4], uint32_t c)
 {
-    return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3];
+    return hsa_sel4<V>(c, v[0], v[1], v[2], v[3]);
 }
 
 // The interval type of a kernel instantiation: uint32_t (the reference's bwtint_t,
@@ -805,7 +807,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     uint32_t sq0 = 0, sp0 = 0;            // split mode: the counters when the item started
     const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
 #ifdef HSA_DIAG
-    uint32_t dc[18] = {0};
+    uint32_t dc[21] = {0};
     uint64_t tsec[4] = {0, 0, 0, 0};
     uint64_t tt = 0;
 #define TMARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); tsec[k] += t_ - tt; tt = t_; } while (0)
@@ -1219,10 +1221,11 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 continue;
             }
             const int em = m_of(m);
-            if (em < 0) continue;
+            if (em < 0) { DC(18); continue; }
             const int ei = M_I(m);
-            if (ei > 0 && em < (int)(wbg(ei - 1) & F::BIDM)) continue;
+            if (ei > 0 && em < (int)(wbg(ei - 1) & F::BIDM)) { DC(18); continue; }
             if (ei == 0) {
+                DC(20);
                 if (!on_hit(e.x, e.y, e.z, e.z + (e.y - e.x)) && !C_OVF(ctl)) SET_PH(ctl, PH_END);
                 continue;
             }
@@ -1332,30 +1335,29 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             // match/mismatch with child (seq[i] + bit-4) & 3.  All but the last go to the
             // pool in order; the last becomes the virtual top when it is the next pop.
             const uint32_t sc = F::NIB ? cur_c : getc(i);
+            // (as selects over every case: nested ifs here were divergent branches)
             uint32_t cand = 0;
-            if (GAPS && allow_diff && (R_MAXGO > 0 || ego > 0)) {
+            if constexpr (GAPS) {
                 const int ies = RG(indel_end_skip);
                 const int tmp = (R_MODE & MODE_LOGGAP) ? int_log2((uint32_t)(ege + ego)) / 2 + 1 : ego + ege;
-                if (i >= ies + tmp && len - i >= ies + tmp) {
-                    const uint32_t dm = ne;
-                    const IT occ = el - ek + 1u;
-                    if (est == ST_M) {
-                        if (ego < R_MAXGO) cand = 1u | dm << 1;
-                    } else if (est == ST_I) {
-                        if (ege < R_MAXGE) cand = 1u;
-                    } else if (ege < R_MAXGE && (ege + ego < max_diff || occ < (IT)RG(max_del_occ))) {
-                        cand = dm << 1;
-                    }
-                }
+                const bool ok = (allow_diff != 0) & ((R_MAXGO > 0) | (ego > 0)) & (i >= ies + tmp) & (len - i >= ies + tmp);
+                const IT occ = el - ek + 1u;
+                const uint32_t c_m = ego < R_MAXGO ? (1u | ne << 1) : 0u;
+                const uint32_t c_i = ege < R_MAXGE ? 1u : 0u;
+                const bool d_ok = (ege < R_MAXGE) & ((ege + ego < max_diff) | (occ < (IT)RG(max_del_occ)));
+                const uint32_t c_d = d_ok ? ne << 1 : 0u;
+                const uint32_t c_g = est == ST_M ? c_m : est == ST_I ? c_i : c_d;
+                cand = ok ? c_g : 0u;
             }
-            if (allow_diff && allow_M) {
+            {
+                uint32_t c_mm = 0;
 #pragma unroll
                 for (int j = 1; j <= 4; ++j) {
                     const uint32_t c = (sc + (uint32_t)j) & 3u;
-                    cand |= ((ne >> c) & 1u) << (4 + j);
+                    c_mm |= ((ne >> c) & 1u) << (4 + j);
                 }
-            } else if (sc < 4) {
-                cand |= ((ne >> sc) & 1u) << 8;                              // == bit 8: c = sc, no mismatch
+                const uint32_t c_eq = sc < 4 ? ((ne >> (sc & 3u)) & 1u) << 8 : 0u;   // == bit 8: c = sc, no mismatch
+                cand |= (allow_diff & allow_M) ? c_mm : c_eq;
             }
             // entry of candidate bit b
             auto entry = [&](uint32_t b) -> E {
@@ -1373,14 +1375,27 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 }
                 return E{k, l, rk, meta};
             };
+#ifdef HSA_DIAG
+            // pushes whose pop would be pruned under the current max_diff and bids
+            auto doomed = [&](uint32_t mw) {
+                const int em2 = m_of(mw), i2 = M_I(mw);
+                return em2 < 0 || (i2 > 0 && em2 < (int)(wbg(i2 - 1) & F::BIDM));
+            };
+#endif
             if (cand) {
                 const uint32_t last = 31u - (uint32_t)__clz(cand);
                 n_entries += __popc(cand);
                 for (uint32_t rest = cand & ~(1u << last); rest; rest &= rest - 1u) {
                     const E v = entry((uint32_t)__ffs(rest) - 1u);
+#ifdef HSA_DIAG
+                    if (doomed(v.w)) DC(19);
+#endif
                     flush(v, bucket_of(v.w));
                 }
                 const E v = entry(last);
+#ifdef HSA_DIAG
+                if (doomed(v.w)) DC(19);
+#endif
                 const int bk = bucket_of(v.w);
                 if (bk <= mask.lowest()) { e = v; ctl |= 1u << 6; }
                 else flush(v, bk);
@@ -1400,6 +1415,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     }
     for (int i = 0; i < 18; ++i)
         if (i < 9 || i > 12) atomicAdd(&g_dctr[i], (unsigned long long)dc[i]);
+    for (int i = 18; i < 21; ++i) atomicAdd(&g_dctr[i], (unsigned long long)dc[i]);
     if (lane == 0)
         for (int i = 0; i < 4; ++i) atomicAdd(&g_dctr[9 + i], (unsigned long long)tsec[i]);
 #endif
