@@ -463,7 +463,7 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
         # the drop-in end to end on the same files: bwa_seq_t batches of 100 000 reads
         rb = os.path.join(d, "e2e_reads.bin")
         write_reads_bin(rb, reads_all[:e2e_reads])
-        env = dict(os.environ, HSA_VERBOSE="1")
+        env = dict(os.environ, HSA_VERBOSE="1", HSA_MALLOC_TUNE="1")    # the host's heap kept
         j = subprocess.run([probe_gpu, "aln", prefix, rb, os.path.join(d, "gpu_out.bin"), *opt_args, "-B",
                             str(REF_BATCH)], capture_output=True, timeout=900, env=env)
         err = j.stderr.decode(errors="replace")
@@ -587,7 +587,8 @@ def main():
     HW = _lib.ALN64_WORDS if wide else 9      # u32 words per hit record
     # the reference's CPU path runs on rank 0 after the gather, one process per thread of
     # the job's CPU share (16 per GPU rank: the whole share of the node at N = 8)
-    ref_procs = a.ref_procs or cpu_info()["threads"] * world
+    # (never more processes than the CPUs this process may run on: they inherit its affinity)
+    ref_procs = a.ref_procs or min(cpu_info()["threads"] * world, cpu_info()["affinity"])
     if a.ref_sample < 0:
         a.ref_sample = {2: 8_000, 3: 2_000, 4: 1_000}.get(a.config, 0) * ref_procs
     ref_legs = rank == 0 and a.config in (2, 3, 4) and not wide and a.ref_sample > 0 and T < (1 << 32)

@@ -581,11 +581,11 @@ int hsa_gpu_attach(const Idx2BWT *bi)
          * bwtgap.c:137-138) that the host frees before the next batch (bwaseqio.c:244).
          * glibc returns the freed pages to the kernel by default, so each batch re-faults
          * them (~20 ms per 100 000 reads); keeping them in the heap makes the next batch's
-         * arrays reuse them.  Results do not depend on it; HSA_MALLOC_TUNE=0 leaves the
-         * host's malloc as it is. */
+         * arrays reuse them.  It changes the whole process's malloc, so it is opt-in:
+         * HSA_MALLOC_TUNE=1.  Results do not depend on it. */
         const char *mt = getenv("HSA_MALLOC_TUNE");
         static int tuned = 0;
-        if (!tuned && (!mt || atoi(mt) != 0)) {
+        if (!tuned && mt && atoi(mt) != 0) {
             mallopt(M_TRIM_THRESHOLD, 1 << 30);
             mallopt(M_MMAP_THRESHOLD, 64 << 20);
             tuned = 1;
@@ -700,10 +700,27 @@ void hsa_gpu_fatal(const char *what, long rc)
     exit(1);
 }
 
+/* One drop-in call at a time: the batch's splice prefetch table (bwtgap_gpu.c) and the
+ * splice runner's coroutine pool (bwtext_gpu.c) are process-wide, so concurrent callers
+ * (the reference has none: its thread loop is commented out, bwtaln.c:483-506) are
+ * serialised here rather than sharing them. */
+static pthread_mutex_t g_batch_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, const gap_opt_t *copt,
+                                  struct bwt_array_t *arr);
+
 void bwa_cal_sa_reg_gap(int tid, const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, const gap_opt_t *copt,
                         struct bwt_array_t *arr)
 {
     (void)tid;
+    pthread_mutex_lock(&g_batch_mu);
+    cal_sa_reg_gap_locked(bi_bwt, n_seqs, seqs, copt, arr);
+    pthread_mutex_unlock(&g_batch_mu);
+}
+
+static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, const gap_opt_t *copt,
+                                  struct bwt_array_t *arr)
+{
     gap_opt_t *opt = (gap_opt_t *)copt;     /* mutated, as the reference does through aux->opt */
     int n_slots = 1;
     hsa_index_t *const *slots = hsa_gpu_slots_of(bi_bwt, &n_slots);

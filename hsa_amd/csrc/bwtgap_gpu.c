@@ -304,7 +304,13 @@ void hsa_splice_memo_clear(void)
 /* The prefetch for reads aux[0..n) as bwt_splice_match receives them (seq, rc_seq, len,
  * opt = local_opt of that read, stack with the batch's n_stacks), in the order the splice
  * path will run them (hsa_splice_set_read's numbering). */
-int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
+static int prefetch_impl(const Idx2BWT *bi, int n, bwt_aux_t *const *aux, int fatal);
+
+int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux) { return prefetch_impl(bi, n, aux, 1); }
+
+/* fatal == 0: the attach-time warm-up, whose answers are discarded: a failure (e.g. HBM
+ * short at attach) is logged under HSA_VERBOSE and ignored */
+static int prefetch_impl(const Idx2BWT *bi, int n, bwt_aux_t *const *aux, int fatal)
 {
     hsa_splice_memo_clear();
     if (n <= 0) return 0;
@@ -370,6 +376,11 @@ int hsa_splice_prefetch(const Idx2BWT *bi, int n, bwt_aux_t *const *aux)
         hsa_splice_memo_clear();
         return 0;
     }
+    if (rc && !fatal) {
+        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] splice prefetch warm-up failed (ignored): %s\n", hsa_last_error());
+        hsa_splice_memo_clear();
+        return 0;
+    }
     if (rc) hsa_gpu_fatal("GPU splice prefetch", rc);
     g_pf_live = 1;
     if (getenv("HSA_VERBOSE"))
@@ -404,7 +415,7 @@ void hsa_splice_prefetch_warm(const Idx2BWT *bi)
         a[r].stack = &st; a[r].max_len = 100;
         ap[r] = a + r;
     }
-    hsa_splice_prefetch(bi, 2, ap);
+    prefetch_impl(bi, 2, ap, 0);
     hsa_splice_memo_clear();
     }
 }

@@ -417,7 +417,7 @@ extern "C" int hsa_index_clone(hsa_index_t *src, hsa_index_t **out)
     ix->trie_depth = root->trie_depth;
     ix->trie_wide = root->trie_wide; ix->trie_bytes = root->trie_bytes;
     ix->parent = root;
-    ++root->n_clones;
+    __atomic_add_fetch(&root->n_clones, 1, __ATOMIC_ACQ_REL);
     *out = ix;
     return 0;
 }
@@ -433,16 +433,23 @@ int hsa_need_unshared(const hsa_index *ix, const char *what)
 extern "C" void hsa_index_free(hsa_index_t *ix)
 {
     if (!ix) return;
-    if (!ix->parent && ix->n_clones > 0) {
+    if (!ix->parent) {
         // live clones still read the shared arrays: the free is deferred to the last
-        // clone's (the handle stays valid for them, not for the caller)
-        ix->free_pending = true;
-        return;
+        // clone's (the handle stays valid for them, not for the caller).  Clones may be
+        // freed from other threads: the flag is published before the count is re-read,
+        // and the clone that takes the count to 0 reads the flag after its decrement.
+        __atomic_store_n(&ix->free_pending, true, __ATOMIC_SEQ_CST);
+        if (__atomic_load_n(&ix->n_clones, __ATOMIC_SEQ_CST) > 0) return;
+        // no clone left (or none ever): free now, unless the last clone's free races us
+        // to it (exactly one of the two sees free_pending still set and takes it)
+        if (!__atomic_exchange_n(&ix->free_pending, false, __ATOMIC_SEQ_CST)) return;
     }
     (void)hipSetDevice(ix->device);
     hsa_index *orphan = nullptr;
     if (ix->parent) {           // the shared arrays stay with the parent
-        if (--ix->parent->n_clones == 0 && ix->parent->free_pending) orphan = ix->parent;
+        if (__atomic_sub_fetch(&ix->parent->n_clones, 1, __ATOMIC_SEQ_CST) == 0 &&
+            __atomic_exchange_n(&ix->parent->free_pending, false, __ATOMIC_SEQ_CST))
+            orphan = ix->parent;
         ix->blk_base[0] = ix->blk_base[1] = nullptr;
         ix->d_sa = ix->d_blocks = nullptr;
         ix->d_trie_w = nullptr;
