@@ -165,7 +165,7 @@ def host_oracle_index(res, T):
 # its "step" mode, which sums the main path's and the splice seeds' kernels); the
 # kernel-trace summaries next to them (tools/trace_summary.py) give the same runs'
 # per-launch durations
-TRAFFIC_SRCS = {2: "profiles/r03_pmc_summary_config2.json", 3: "profiles/r03_pmc_summary_config3.json",
+TRAFFIC_SRCS = {2: "profiles/r05_pmc_summary_config2.json", 3: "profiles/r05_pmc_summary_config3.json",
                 4: "profiles/r03_pmc_summary_config4.json", 5: "profiles/r03_pmc_summary_config5.json"}
 
 
@@ -549,6 +549,8 @@ def main():
                     help="reference processes (0: the CPU threads of the job's share, 16 per GPU rank)")
     ap.add_argument("--e2e-reads", type=int, default=1_000_000,
                     help="reads of the drop-in end-to-end leg (oracle/_ref/ref_probe_gpu, 100 000 per call)")
+    ap.add_argument("--copies", type=int, default=1,
+                    help="also time the steps with the H2D reads and D2H hits inside them (value_with_copies)")
     ap.add_argument("--rank-parity", type=int, default=100_000,
                     help="with N > 1 ranks: reads of each rank's timed batch checked against the restatement")
     a = ap.parse_args()
@@ -753,6 +755,47 @@ def main():
         roof_sets = [(a.warmup + s) % nd for s in range(R)][-len(w_ms):]
         log(f"[bench] rank {rank}: {R} serialized steps: k_widths {np.mean(w_ms):.2f} ms, k_search "
             f"{np.mean(s_ms):.2f} ms (overlapped in the timed region: {np.mean(ovl_w):.2f} / {np.mean(ovl_s):.2f} ms)")
+    # The same K steps with the PCIe copies inside each step (SURVEY §8d's timing window:
+    # H2D reads -> width + search kernels -> D2H hits): reads from pinned host memory into
+    # the read set's device buffer, the per-read outputs and the batch's hit records back,
+    # all on the step's handle stream, so the copies of one step overlap the other
+    # handle's kernels.  Reported beside `value`, never as it.
+    copies = None
+    if a.copies and world == 1 and a.config != 4:
+        h_codes = [d_codes[j].cpu().pin_memory() for j in range(nd)]
+        nh_set = {j: int(outs[j]["c"][1].item()) for j in range(nd)}       # a read set's hit count: fixed
+        h_out = [dict(n=torch.empty(a.batch, dtype=torch.int32).pin_memory(),
+                      f=torch.empty(a.batch, dtype=torch.int32).pin_memory(),
+                      o=torch.empty(a.batch, dtype=torch.int64).pin_memory(),
+                      h=torch.empty(max(nh_set[j], 1) * HW, dtype=torch.int32).pin_memory()) for j in range(nd)]
+        torch.cuda.synchronize()
+        evc = [torch.cuda.Event() for _ in range(a.steps)]
+        t0 = time.perf_counter()
+        for s, (hi, j, after) in enumerate(step_plan(a.steps, a.warmup, nd, S)):
+            st = lib_streams[hi]
+            with torch.cuda.stream(st):
+                if after is not None:
+                    st.wait_event(evc[after])
+                d_codes[j].copy_(h_codes[j], non_blocking=True)
+                launch(j, hi)
+                o = outs[j]
+                for k in ("n", "f", "o"):
+                    h_out[j][k].copy_(o[k], non_blocking=True)
+                h_out[j]["h"][:nh_set[j] * HW].copy_(o["h"][:nh_set[j] * HW], non_blocking=True)
+                evc[s].record(st)
+        torch.cuda.synchronize()
+        el_c = time.perf_counter() - t0
+        bytes_in = sum(d_codes[(a.warmup + s) % nd].numel() for s in range(a.steps))
+        bytes_out = sum(a.batch * 16 + nh_set[(a.warmup + s) % nd] * HW * 4 for s in range(a.steps))
+        copies = {"value": round(a.batch * a.steps / el_c, 1), "unit": "reads/s",
+                  "ms_per_step": round(el_c * 1e3 / a.steps, 3),
+                  "h2d_bytes_per_step": bytes_in // a.steps, "d2h_bytes_per_step": bytes_out // a.steps,
+                  "what": "the timed steps again with H2D of the reads (pinned) and D2H of n_aln, flags, hit offsets "
+                          "and the hit records inside each step, on the step's handle stream (the copies of one "
+                          "step overlap the other handle's kernels); SURVEY 8d's timing window"}
+        log(f"[bench] rank {rank}: with the copies inside the step: {copies['value']:.0f} reads/s "
+            f"({copies['ms_per_step']:.2f} ms per step)")
+        del h_codes, h_out
     for h in handles[1:]:       # their search scratch (a gapped pool is tens of GB) goes back before the other legs
         h.close()
     if world > 1:
@@ -905,6 +948,8 @@ def main():
             "mapped_frac": round(mapped_all / reads_all, 4), "fallback_frac": round(fallback_all / reads_all, 4),
             "pops_per_read": round(pops / reads_local, 1),
         }
+        if copies is not None:
+            result["value_with_copies"] = copies
         if a.config == 4:
             result["seed_rank_queries_per_read"] = round(seed_queries / reads_local, 1)
             result["roofline"]["splice_seeds_ms"] = round(float(np.mean(seeds_ms)), 3)

@@ -32,8 +32,9 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
     "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced", "hsa_index_trie",
-    "hsa_index_clone", "hsa_splice_prefetch_batch",
+    "hsa_index_clone", "hsa_splice_prefetch_batch", "hsa_index_set_text", "hsa_splice_match_batch",
 ]
+SP_RES_WORDS = 20  # hsa_splice_match_batch's per-read answer (include/hsa_gpu.h)
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
 
 
@@ -137,6 +138,12 @@ class SplicePf(C.Structure):
                 ("n_sa", C.c_uint64), ("kernel_ms", C.c_double)]
 
 
+class SpliceStats(C.Structure):
+    """hsa_splice_stats_t (include/hsa_gpu.h)."""
+    _fields_ = [("kernel_ms", C.c_double), ("extensions", C.c_uint64), ("pops", C.c_uint64),
+                ("sa_lookups", C.c_uint64), ("not_answered", C.c_uint64)]
+
+
 _lib = None
 
 
@@ -204,6 +211,11 @@ def lib():
     if hasattr(L, "hsa_splice_prefetch_batch"):
         L.hsa_splice_prefetch_batch.argtypes = [vp, C.POINTER(Regime), C.POINTER(Regime), C.c_int, u32, u64, u8,
                                                 C.c_size_t, i32, C.POINTER(SplicePf)]
+    if hasattr(L, "hsa_splice_match_batch"):
+        L.hsa_index_set_text.argtypes = [vp, u32, C.c_uint64, C.c_uint32]
+        L.hsa_splice_match_batch.argtypes = [vp, C.POINTER(Regime), C.POINTER(Regime), C.POINTER(Regime), C.c_int, u32,
+                                             u64, u8, C.c_size_t, i32, C.POINTER(SplicePf), u32,
+                                             C.POINTER(SpliceStats)]
     if hasattr(L, "hsa_search_device64"):           # (older A/B builds lack the 64-bit path)
         L.hsa_index_create_device64.argtypes = [C.c_int, C.c_uint64, C.c_uint64, u64, vp, C.c_uint64, C.c_uint64,
                                                 u64, vp, C.POINTER(vp)]
@@ -377,6 +389,26 @@ class GpuIndex:
                     wafter=arr(o.wafter, np.int32, n * 8 * cws * 2).reshape(n, 8, cws, 2),
                     call_sa=arr(o.call_sa, np.uint64, n * 8).reshape(n, 8) if o.call_sa else None,
                     sa=arr(o.sa, np.uint32, int(o.n_sa) * 4).reshape(-1, 4), kernel_ms=o.kernel_ms)
+
+    def set_text(self, packed_words, dna_len):
+        """Upload the packed reference as the HSP holds it (16 codes per u32, the first in
+        the high bits; hsa_index_set_text) for the splice kernel."""
+        w = np.ascontiguousarray(packed_words, np.uint32)
+        check(lib().hsa_index_set_text(self.h, w, len(w), int(dna_len)))
+
+    def splice_match(self, seed_regime, anchor_regime, ext_regime, lens, codes, max_diff):
+        """hsa_splice_match_batch: bwt_splice_match of each read on the device.  Returns
+        (res (n, SP_RES_WORDS) uint32: status, n_aln, res_aln[0], res_aln[1]; stats)."""
+        lens = np.ascontiguousarray(lens, np.uint32)
+        codes = np.ascontiguousarray(codes, np.uint8)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
+        amd = np.ascontiguousarray(max_diff, np.int32)
+        res = np.zeros((len(lens), SP_RES_WORDS), np.uint32)
+        o, st = SplicePf(), SpliceStats()
+        check(lib().hsa_splice_match_batch(self.h, C.byref(seed_regime), C.byref(anchor_regime), C.byref(ext_regime),
+                                           len(lens), lens, offs, codes, len(codes), amd, C.byref(o), res,
+                                           C.byref(st)))
+        return res, {k: getattr(st, k) for k, _ in SpliceStats._fields_}
 
     def set_sa(self, sa, blocks):
         """Upload the sampled SA (index_io.SaFile) and the block table (rows of

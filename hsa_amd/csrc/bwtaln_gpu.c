@@ -198,6 +198,90 @@ static void *pf_job_run(void *arg)
     return NULL;
 }
 
+/* The prefetch job of reads idx[0..n) as bwt_splice_match receives them (aux of read i:
+ * seq, rc_seq, len, local_opt with the read's max_diff / seed_len, the batch's stack). */
+static void pf_job_init(pf_job_t *pj, const Idx2BWT *bi, struct bwt_array_t *arr, const bwa_seq_t *seqs,
+                        const uint64_t *offs, size_t tot, int max_len, const int *idx, int n, const gap_opt_t *local,
+                        const int32_t *sp, int n_stacks)
+{
+    memset(pj, 0, sizeof *pj);
+    pj->bi = bi;
+    pj->n = n;
+    pj->fa = (bwt_aux_t *)calloc((size_t)n, sizeof(bwt_aux_t));
+    pj->fp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)n);
+    pj->fo = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)n);
+    pj->rc = (ubyte_t *)malloc(tot + 1);
+    pj->st_shape.n_stacks = n_stacks;                /* only n_stacks is read */
+    for (int q = 0; q < n; ++q) {
+        const int i = idx[q];
+        const bwa_seq_t *p = seqs + i;
+        ubyte_t *r = pj->rc + offs[i];
+        for (int j = 0; j < (int)p->len; ++j) {
+            ubyte_t c = p->seq[p->len - 1 - j];
+            r[j] = c < 4 ? (ubyte_t)(3 - c) : c;
+        }
+        pj->fo[q] = *local;
+        pj->fo[q].max_diff = sp[2 * i];
+        pj->fo[q].seed_len = sp[2 * i + 1];
+        bwt_aux_t *x = pj->fa + q;
+        x->bi_bwt = (Idx2BWT *)bi; x->arr = arr; x->max_len = max_len;
+        x->seq = p->seq; x->rc_seq = r; x->len = (int)p->len; x->opt = pj->fo + q;
+        x->stack = &pj->st_shape;
+        pj->fp[q] = x;
+    }
+}
+
+static void pf_job_free(pf_job_t *pj) { free(pj->fa); free(pj->fp); free(pj->fo); free(pj->rc); }
+
+/* bwt_splice_match of a batch's fallback reads on the device (hsa_splice_match_batch). */
+typedef struct {
+    hsa_index_t *ix;
+    int n;
+    const int *fb;                   /* the reads, in order */
+    const bwa_seq_t *seqs;
+    const int32_t *sp;               /* per read: local_opt's max_diff, seed_len */
+    gap_opt_t local;
+    int n_stacks;
+    uint32_t *res;                   /* HSA_SP_RES_WORDS per read */
+    int rc;
+    double secs;
+    hsa_splice_stats_t st;
+} dsp_job_t;
+
+static void *dsp_job_run(void *arg)
+{
+    dsp_job_t *j = (dsp_job_t *)arg;
+    const double t0 = hsa_now();
+    uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)j->n);
+    uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)j->n);
+    int32_t *amd = (int32_t *)malloc(sizeof(int32_t) * (size_t)j->n);
+    size_t tot = 0;
+    int amd_max = 0;
+    for (int k = 0; k < j->n; ++k) {
+        const bwa_seq_t *p = j->seqs + j->fb[k];
+        lens[k] = p->len; offs[k] = tot; tot += p->len;
+        amd[k] = j->sp[2 * j->fb[k]];
+        amd_max = amd[k] > amd_max ? amd[k] : amd_max;
+    }
+    uint8_t *codes = (uint8_t *)malloc(tot + 1);
+    for (int k = 0; k < j->n; ++k) memcpy(codes + offs[k], j->seqs[j->fb[k]].seq, lens[k]);
+    /* aux_seed (bwtgap.c:769-774), aux_ext (:776-782) */
+    gap_opt_t so = j->local, ao = j->local;
+    so.mode &= ~BWA_MODE_GAPE; so.max_gapo = 0; so.max_gape = 0; so.max_diff = j->local.max_seed_diff;
+    ao.max_gape = 3;
+    const hsa_regime_t srg = hsa_regime_of(&so, j->n_stacks, so.max_diff);
+    const hsa_regime_t arg_ = hsa_regime_of(&ao, j->n_stacks, amd_max);
+    hsa_regime_t erg = arg_;
+    erg.mode = ao.mode & (BWA_MODE_GAPE | BWA_MODE_LOGGAP | BWA_MODE_NONSTOP);   /* as the extension reads it */
+    hsa_splice_pf_t pf;
+    hsa_gpu_lock();
+    j->rc = hsa_splice_match_batch(j->ix, &srg, &arg_, &erg, j->n, lens, offs, codes, tot, amd, &pf, j->res, &j->st);
+    hsa_gpu_unlock();
+    free(lens); free(offs); free(amd); free(codes);
+    j->secs = hsa_now() - t0;
+    return NULL;
+}
+
 /* One read of the bwtaln.c:303-337 prologue under regime `cur` (0 = A, 1 = B). */
 static int plan_read(const gap_opt_t *caller, int cur, optstate_t *st, const readinfo_t *ri, int len,
                      int32_t *max_diff, int32_t *seed_len)
@@ -524,6 +608,12 @@ static int attach_slot(const Idx2BWT *bi, int slot, hsa_index_t *const *have, hs
     if (rc == 0 && f->saValue && bi->hsp)
         rc = hsa_index_set_sa(ix, f->saValue, f->saValueSizeInWord, f->saInterval,
                               (const uint32_t *)bi->hsp->blockList, bi->hsp->numOfBlock);
+    /* the splice kernel's motif scan and intron-end check read the packed reference as
+     * the HSP holds it: (dnaLength + 15) / 16 + 1 words (DNALoadPacked,
+     * TextConverter.c:704-707) */
+    if (rc == 0 && bi->hsp && bi->hsp->packedDNA)
+        rc = hsa_index_set_text(ix, bi->hsp->packedDNA, ((uint64_t)bi->hsp->dnaLength + 15) / 16 + 1,
+                                bi->hsp->dnaLength);
     if (rc != 0 && ix) { hsa_index_free(ix); ix = NULL; }
     *out = ix;
     return rc;
@@ -752,81 +842,112 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
     memset(&aux, 0, sizeof aux);
     int have_splice = bwt_splice_match != NULL;
     const int n_stacks = hsa_aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
-    /* the splice path's widths, seed and anchor searches and SA lookups of every fallback
-     * read in one device pass (hsa_splice_prefetch, bwtgap_gpu.c), when the host's
-     * bwt_splice_match calls our bwt_match_gap: on a thread of its own, while this thread
-     * writes the per-read output arrays (so that they come from the host thread's own heap
-     * arena, where the host frees them) */
-    double t_pf = 0.0;
-    const double t1 = hsa_now();
-    /* HSA_SPLICE_PREFETCH=0: no table, every splice-path call goes to the GPU on its own
-     * (tests: misses from several runner threads at once) */
-    const char *pfe = getenv("HSA_SPLICE_PREFETCH");
-    const int want_pf = !pfe || atoi(pfe) != 0;
+    /* the reads that go to bwt_splice_match (bwtaln.c:362-369), in order */
+    int *fb = (int *)malloc(sizeof(int) * ((size_t)n_seqs + 1));
     int nf = 0;
     for (int i = 0; i < n_seqs; ++i)
-        nf += !(flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) && n_aln[i] == 0 && (flags[i] & HSA_F_FALLBACK);
+        if (!(flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) && n_aln[i] == 0 && (flags[i] & HSA_F_FALLBACK) && have_splice)
+            fb[nf++] = i;
+    const double t1 = hsa_now();
+    /* bwt_splice_match of every fallback read on the device (hsa_splice_match_batch: the
+     * prefetch pass and the splice kernel, hsa_splice.hip), on a helper thread while this
+     * thread writes the per-read output arrays (so that they come from the host thread's
+     * own heap arena, where the host frees them).  HSA_SPLICE_DEVICE=0: the host's
+     * bwt_splice_match for all of them. */
+    const char *sde = getenv("HSA_SPLICE_DEVICE");
+    const int want_dev = !sde || atoi(sde) != 0;
+    dsp_job_t dj;
+    memset(&dj, 0, sizeof dj);
+    int dev = want_dev && nf > 0 && n_stacks <= HSA_SP_MAX_STACKS;
+    for (int k = 0; dev && k < nf; ++k)
+        if (seqs[fb[k]].len < 3 || seqs[fb[k]].len > 3 * 1021) dev = 0;   /* the prefetch's read lengths */
+    pthread_t dth;
+    int dev_async = 0;
+    if (dev) {
+        dj.ix = slots[0]; dj.n = nf; dj.fb = fb; dj.seqs = seqs; dj.sp = sp; dj.local = local; dj.n_stacks = n_stacks;
+        dj.res = (uint32_t *)malloc(sizeof(uint32_t) * HSA_SP_RES_WORDS * (size_t)nf);
+        dev_async = pthread_create(&dth, NULL, dsp_job_run, &dj) == 0;
+        if (!dev_async) dsp_job_run(&dj);
+    }
+    /* the reads the host's bwt_splice_match runs: all fallback reads, or those the device
+     * did not answer; hr[] in order, numbered in the prefetch table by their rank in hr */
+    int *hr = fb, nh_r = nf;
+    /* the splice path's widths, seed and anchor searches and SA lookups of the host's reads
+     * in one device pass (hsa_splice_prefetch, bwtgap_gpu.c), when the host's
+     * bwt_splice_match calls our bwt_match_gap.  HSA_SPLICE_PREFETCH=0: no table, every
+     * splice-path call goes to the GPU on its own (tests: misses from several runner
+     * threads at once) */
+    const char *pfe = getenv("HSA_SPLICE_PREFETCH");
+    const int want_pf = !pfe || atoi(pfe) != 0;
+    const int pf_ok = want_pf && have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active();
     pf_job_t pj;
     memset(&pj, 0, sizeof pj);
     pthread_t pth;
-    int pf_async = 0;
-    const int prefetched = want_pf && nf > 0 && have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active();
-    if (prefetched) {
-        pj.bi = bi_bwt;
-        pj.n = nf;
-        pj.fa = (bwt_aux_t *)calloc((size_t)nf, sizeof(bwt_aux_t));
-        pj.fp = (bwt_aux_t **)malloc(sizeof(bwt_aux_t *) * (size_t)nf);
-        pj.fo = (gap_opt_t *)malloc(sizeof(gap_opt_t) * (size_t)nf);
-        pj.rc = (ubyte_t *)malloc(tot + 1);
-        memset(&pj.st_shape, 0, sizeof pj.st_shape);   /* only n_stacks is read */
-        pj.st_shape.n_stacks = n_stacks;
-        int q = 0;
-        for (int i = 0; i < n_seqs; ++i) {
-            if ((flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) || n_aln[i] != 0 || !(flags[i] & HSA_F_FALLBACK)) continue;
-            const bwa_seq_t *p = seqs + i;
-            ubyte_t *r = pj.rc + offs[i];
-            for (int j = 0; j < (int)p->len; ++j) {
-                ubyte_t c = p->seq[p->len - 1 - j];
-                r[j] = c < 4 ? (ubyte_t)(3 - c) : c;
-            }
-            pj.fo[q] = local;
-            pj.fo[q].max_diff = sp[2 * i];
-            pj.fo[q].seed_len = sp[2 * i + 1];
-            bwt_aux_t *x = pj.fa + q;
-            x->bi_bwt = (Idx2BWT *)bi_bwt; x->arr = arr; x->max_len = max_len;
-            x->seq = p->seq; x->rc_seq = r; x->len = (int)p->len; x->opt = pj.fo + q;
-            x->stack = &pj.st_shape;
-            pj.fp[q] = x;
-            ++q;
-        }
+    int pf_async = 0, prefetched = 0;
+    double t_pf = 0.0;
+    if (!dev && pf_ok && nh_r > 0) {         /* beside the per-read outputs */
+        pf_job_init(&pj, bi_bwt, arr, seqs, offs, tot, max_len, hr, nh_r, &local, sp, n_stacks);
         pf_async = pthread_create(&pth, NULL, pf_job_run, &pj) == 0;
         if (!pf_async) pf_job_run(&pj);
+        prefetched = 1;
     }
     const double to = hsa_now();
     write_outputs(seqs, n_seqs, n_aln, flags, hoff, hits);
     const double t_out = hsa_now() - to;
     if (pf_async) pthread_join(pth, NULL);
+    if (dev_async) pthread_join(dth, NULL);
     const double t_join = hsa_now() - to - t_out;
-    if (prefetched) {
-        t_pf = pj.secs;
-        free(pj.fa); free(pj.fp); free(pj.fo); free(pj.rc);
+    int n_dev = 0;
+    if (dev) {
+        if (dj.rc == HSA_E_ARG) {                /* not on this index / these options: the host's path */
+            if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] splice kernel not used: %s\n", hsa_last_error());
+        } else if (dj.rc) {
+            hsa_gpu_fatal("GPU splice path", dj.rc);
+        } else {
+            /* the device's answers; the reads it did not answer go to the host's path */
+            hr = (int *)malloc(sizeof(int) * ((size_t)nf + 1));
+            nh_r = 0;
+            for (int k = 0; k < nf; ++k) {
+                const uint32_t *o = dj.res + (size_t)HSA_SP_RES_WORDS * k;
+                if (o[0] != HSA_SP_OK) { hr[nh_r++] = fb[k]; continue; }
+                bwa_seq_t *p = seqs + fb[k];
+                p->n_aln = (int)o[1];
+                if (o[1] == 0) { p->aln = NULL; continue; }
+                p->aln = (bwt_aln1_t *)calloc(2, sizeof(bwt_aln1_t));     /* res_aln (bwtgap.c:854) */
+                memcpy(p->aln, o + 2, 2 * sizeof(bwt_aln1_t));
+                ++n_dev;
+            }
+            if (getenv("HSA_VERBOSE"))
+                fprintf(stderr, "[hsa] splice kernel: %d reads, %d spliced, %d to the host's path; %llu extensions, %llu "
+                                "pops, %llu SA lookups, %.1f ms of kernel (%.3f s with the prefetch pass)\n", nf, n_dev,
+                        nh_r, (unsigned long long)dj.st.extensions, (unsigned long long)dj.st.pops,
+                        (unsigned long long)dj.st.sa_lookups, dj.st.kernel_ms, dj.secs);
+            if (pf_ok && nh_r > 0) {             /* the host's reads' own prefetch */
+                pf_job_init(&pj, bi_bwt, arr, seqs, offs, tot, max_len, hr, nh_r, &local, sp, n_stacks);
+                pf_job_run(&pj);
+                prefetched = 1;
+            }
+        }
+        t_pf = dj.secs;
+        free(dj.res);
     }
-    /* the host's splice path for the fallback reads: all of them at once as coroutines
-     * whose seed extensions run batched on the GPU, when the host calls our
-     * bwt_extend_* (bwtext_gpu.c); else one read at a time, as the reference */
+    if (prefetched) {
+        t_pf += pj.secs;
+        pf_job_free(&pj);
+    }
+    /* the host's splice path for its reads: all of them at once as coroutines whose seed
+     * extensions run batched on the GPU, when the host calls our bwt_extend_*
+     * (bwtext_gpu.c); else one read at a time, as the reference */
     const int batched = have_splice && hsa_splice_run && hsa_splice_extend_active && hsa_splice_extend_active();
     hsa_splice_read_t *sr = NULL;
     int *sr_idx = NULL, n_sr = 0;
     if (batched) {
-        sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)n_seqs + 1));
-        sr_idx = (int *)malloc(sizeof(int) * ((size_t)n_seqs + 1));
+        sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)nh_r + 1));
+        sr_idx = (int *)malloc(sizeof(int) * ((size_t)nh_r + 1));
     }
-    int q_fb = 0;                                               /* the read's prefetch-table number */
-    for (int i = 0; i < n_seqs; ++i) {                          /* the splice path's reads, in order */
+    for (int q = 0; q < nh_r; ++q) {                            /* q: the read's prefetch-table number */
+        const int i = hr[q];
         bwa_seq_t *p = seqs + i;
-        if ((flags[i] & (HSA_RF_NFILTER | HSA_RF_POLYAT)) || n_aln[i] > 0) continue;
-        if (!(flags[i] & HSA_F_FALLBACK) || !have_splice) continue;
-        const int q_this = q_fb++;
         gap_opt_t lo = local;                                   /* aux->opt = &local_opt (:363) */
         lo.max_diff = sp[2 * i];
         lo.seed_len = sp[2 * i + 1];
@@ -855,7 +976,7 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
             aux.rc_seq[j] = c < 4 ? (ubyte_t)(3 - c) : c;
         }
         int na = 0;
-        if (hsa_splice_set_read) hsa_splice_set_read(prefetched ? q_this : -1);
+        if (hsa_splice_set_read) hsa_splice_set_read(prefetched ? q : -1);
         p->aln = bwt_splice_match(&aux, &na);
         if (hsa_splice_set_read) hsa_splice_set_read(-1);
         p->n_aln = na;
@@ -880,9 +1001,9 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
     free(sr); free(sr_idx);
     if (getenv("HSA_VERBOSE"))
         fprintf(stderr, "[hsa] batch of %d reads: search %.3f s, splice prefetch %.3f s, splice path %.3f s "
-                        "(%d fallback reads; per-read outputs %.1f ms%s, %.1f ms waited for)\n", n_seqs, t1 - t0, t_pf,
-                hsa_now() - t2 + (t2 - t1 - t_pf), n_sr, 1e3 * t_out, prefetched ? " beside the prefetch" : "",
-                1e3 * t_join);
+                        "(%d fallback reads, %d on the device; per-read outputs %.1f ms%s, %.1f ms waited for)\n",
+                n_seqs, t1 - t0, t_pf, hsa_now() - t2 + (t2 - t1 - t_pf), nf, dev ? nf - nh_r : 0, 1e3 * t_out,
+                (prefetched || dev) ? " beside the device pass" : "", 1e3 * t_join);
     if (aux.stack) {
         free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);
         ref_stack_free(aux.stack);
@@ -910,6 +1031,8 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
         }
         hsa_splice_sa_clear();
     }
+    if (hr != fb) free(hr);
+    free(fb);
     hsa_free(hits);
     free(lens); free(offs); free(codes); free(n_aln); free(flags); free(hoff); free(sp);
 }

@@ -315,6 +315,7 @@ static int index_init(int device, hsa_index **out)
     HSA_HIP(hipEventCreate(&ix->ev0));
     HSA_HIP(hipEventCreate(&ix->ev1));
     HSA_HIP(hipEventCreate(&ix->evm));
+    HSA_HIP(hipEventCreate(&ix->ev_sp));
     ix->ev_split = ix->evm;
     HSA_HIP(hipMalloc(&ix->d_ctr, 16 * sizeof(uint64_t)));
     *out = ix;
@@ -412,6 +413,7 @@ extern "C" int hsa_index_clone(hsa_index_t *src, hsa_index_t **out)
     ix->T64 = root->T64; ix->isa0_64 = root->isa0_64; memcpy(ix->C64, root->C64, sizeof ix->C64);
     ix->rT64 = root->rT64; ix->risa0_64 = root->risa0_64; memcpy(ix->rC64, root->rC64, sizeof ix->rC64);
     ix->d_sa = root->d_sa; ix->d_blocks = root->d_blocks;
+    ix->d_text = root->d_text; ix->text_words = root->text_words; ix->dna_len = root->dna_len;
     ix->sa_interval = root->sa_interval; ix->n_blocks = root->n_blocks;
     ix->d_trie_w = root->d_trie_w;
     ix->trie_depth = root->trie_depth;
@@ -452,6 +454,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
             orphan = ix->parent;
         ix->blk_base[0] = ix->blk_base[1] = nullptr;
         ix->d_sa = ix->d_blocks = nullptr;
+        ix->d_text = nullptr;
         ix->d_trie_w = nullptr;
     }
     (void)hipFree(ix->blk_base[0]); (void)hipFree(ix->blk_base[1]);
@@ -465,11 +468,13 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (ix->d_pf2) (void)hipFree(ix->d_pf2);
     if (ix->h_pf) (void)hipHostFree(ix->h_pf);
     (void)hipFree(ix->d_in); (void)hipFree(ix->d_out); (void)hipFree(ix->d_ctr); (void)hipFree(ix->d_wrows); (void)hipFree(ix->d_ovf); (void)hipFree(ix->d_seed); (void)hipFree(ix->d_ext); (void)hipFree(ix->d_slices);
-    (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks);
+    (void)hipFree(ix->d_sa); (void)hipFree(ix->d_blocks); (void)hipFree(ix->d_text);
+    if (ix->d_sp) (void)hipFree(ix->d_sp);
     (void)hipFree(ix->d_trie_w);
     if (ix->ev0) (void)hipEventDestroy(ix->ev0);
     if (ix->ev1) (void)hipEventDestroy(ix->ev1);
     if (ix->evm) (void)hipEventDestroy(ix->evm);
+    if (ix->ev_sp) (void)hipEventDestroy(ix->ev_sp);
     for (int i = 0; i < hsa_index::PASS_RING; ++i)
         for (int j = 0; j < 3; ++j)
             if (ix->pev[i][j]) (void)hipEventDestroy(ix->pev[i][j]);

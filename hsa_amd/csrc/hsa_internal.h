@@ -6,6 +6,7 @@
 
 #include "../../include/hsa_gpu.h"
 #include "hsa_device.h"
+#include "hsa_sa.h"
 
 void hsa_set_error(const char *fmt, ...);
 
@@ -70,6 +71,14 @@ struct hsa_index {
     // sampled suffix array + chromosome blocks (SA -> position, hsa_sa.hip)
     uint32_t *d_sa = nullptr, *d_blocks = nullptr;
     uint32_t sa_interval = 0, n_blocks = 0;
+    // the packed text as the host's HSP holds it (hsa_index_set_text): 16 codes per u32,
+    // the first in the high bits, text_words words as allocated (DNALoadPacked,
+    // TextConverter.c:704-707), dna_len the HSP's dnaLength
+    uint32_t *d_text = nullptr;
+    uint64_t text_words = 0;
+    uint32_t dna_len = 0;
+    // the splice path's kernel (hsa_splice.hip): per-lane state, stacks, buffers
+    void *d_sp = nullptr; size_t d_sp_cap = 0;
     uint64_t *d_ctr = nullptr;
     // the root width trie (hsa_trie.h): every string of up to trie_depth characters;
     // built with the index's interval width (trie_wide: 64-bit entries), 0 = none
@@ -83,6 +92,7 @@ struct hsa_index {
     int staged_ntab = 128;              // staged regimes: score table entries per regime (k_search LDS)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evm = nullptr;           // between k_widths and k_search of the last pass (timing split)
+    hipEvent_t ev_sp = nullptr;         // after the splice kernel (hsa_splice_match_batch: ev1 .. ev_sp)
     // hsa_search_device passes: start / between k_widths and k_search / end, per pass, in a
     // ring (hsa_pass_times), so a caller can time every launch of a back-to-back run
     static constexpr int PASS_RING = 1024;
@@ -100,6 +110,26 @@ struct hsa_index {
 int hsa_need_unshared(const hsa_index *ix, const char *what);
 
 int hsa_grow(void **p, size_t *cap, size_t need);
+SaView hsa_sa_view(const hsa_index *ix);
+
+// The splice prefetch's device outputs (hsa_splice_prefetch_batch, hsa_search.hip), as
+// the splice path's kernel reads them (hsa_splice.hip).
+struct PfDev {
+    uint32_t n, max_len, sc, rs, cws;
+    const uint32_t *lens;
+    const int32_t *amd;            // per read: its local_opt max_diff
+    const uint8_t *scodes;         // strand s of read r at (2 r + s) sc
+    const int32_t *rows;           // 6 rows per read, rs pairs each
+    const int32_t *cw;             // per call: width_back after gap_shadow, cws pairs
+    const int32_t *call_n;         // 8 calls per read: seeds 0-5, anchors 6-7 (-1: not searched)
+    const uint32_t *call_fl;
+    const uint64_t *call_hit;      // record index in hits_s (seeds) / hits_a (anchors)
+    const uint32_t *hits_s, *hits_a;
+};
+// bwt_splice_match for the prefetch's reads on the device (d_res: HSA_SP_RES_WORDS u32
+// per read); ext_rg: the extension regime (local_opt with max_gape 3, bwtgap.c:777-782)
+int hsa_splice_device_launch(hsa_index *ix, const PfDev &pd, const hsa_regime_t &ext_rg, uint32_t *d_res,
+                             unsigned long long *d_ctr, hipStream_t st);
 int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap, size_t link_bytes = 2);
 void hsa_scratch_free(SearchScratch &s);
 // HSA_E_ARG unless the index fits the 32-bit entry points (bwtint_t, 2BWT-Interface.h:26)

@@ -782,11 +782,15 @@ static int mg_passes(hsa_index *ix, const hsa_regime_t *d_reg, const uint8_t *d_
     return 0;
 }
 
-extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
-                                         int n, const uint32_t *lens, const uint64_t *offs, const uint8_t *codes,
-                                         size_t codes_len, const int32_t *anchor_max_diff, hsa_splice_pf_t *out)
+// The prefetch pass, and with ext_rg the splice kernel after it (hsa_splice.hip): res
+// receives its per-read answers.
+static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg, int n,
+                    const uint32_t *lens, const uint64_t *offs, const uint8_t *codes, size_t codes_len,
+                    const int32_t *anchor_max_diff, hsa_splice_pf_t *out, const hsa_regime_t *ext_rg, uint32_t *res,
+                    hsa_splice_stats_t *sst)
 {
     memset(out, 0, sizeof *out);
+    if (sst) memset(sst, 0, sizeof *sst);
     if (n <= 0) return 0;
     if (int rc0 = hsa_need32(ix)) return rc0;
     if (!seed_rg || !anchor_rg || !lens || !offs || !codes || !anchor_max_diff || !out) {
@@ -832,6 +836,7 @@ extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *se
     const size_t q_rows = q_sa + al(calls * 8), q_cw = q_rows + al(N * 6 * rs * 8), q_hs = q_cw + al(calls * cws * 8);
     const size_t q_ha = q_hs + al(cap_s * 36), q_end = q_ha + al(cap_a * 36);
     o += q_end;
+    const size_t o_res = o; o += ext_rg ? al(N * HSA_SP_RES_WORDS * 4) : 0;   // the splice kernel's answers
     if ((rc = hsa_grow(&ix->d_pf, &ix->d_pf_cap, o + 256))) return rc;
     char *d = (char *)ix->d_pf;
     HSA_HIP(hipMemcpyAsync(d + o_lens, lens, N * 4, hipMemcpyHostToDevice, st));
@@ -911,6 +916,16 @@ extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *se
         if ((rc = hsa_sa_position_device(ix, n_sa, d_idx, d_sao, st))) return rc;
     }
     HSA_HIP(hipEventRecord(ix->ev1, st));
+    if (ext_rg) {                                 // bwt_splice_match itself (hsa_splice.hip)
+        PfDev pd;
+        pd.n = (uint32_t)n; pd.max_len = M; pd.sc = sc; pd.rs = rs; pd.cws = cws;
+        pd.lens = A.lens; pd.amd = A.amd; pd.scodes = A.scodes; pd.rows = A.rows; pd.cw = A.cw;
+        pd.call_n = A.call_n; pd.call_fl = A.call_fl; pd.call_hit = (const uint64_t *)(dq + q_ho);
+        pd.hits_s = (const uint32_t *)(dq + q_hs); pd.hits_a = (const uint32_t *)(dq + q_ha);
+        if ((rc = hsa_splice_device_launch(ix, pd, *ext_rg, (uint32_t *)(d + o_res), ctr_s + 40, st))) return rc;
+        HSA_HIP(hipEventRecord(ix->ev_sp, st));
+        HSA_HIP(hipMemcpyAsync(res, d + o_res, N * HSA_SP_RES_WORDS * 4, hipMemcpyDeviceToHost, st));
+    }
     // one copy of the output block (hits up to their counts) into pinned host memory
     const uint64_t nh_s = hc[1] < cap_s ? hc[1] : cap_s, nh_a = hc[16 + 1] < cap_a ? hc[16 + 1] : cap_a;
     const size_t h_need = q_hs + (nh_s + nh_a) * 36 + al(n_sa * 16) + 256;
@@ -929,6 +944,14 @@ extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *se
     HSA_HIP(hipStreamSynchronize(st));
     float ms = 0;
     HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+    if (ext_rg && sst) {
+        float sms = 0;
+        unsigned long long sc4[4];
+        HSA_HIP(hipEventElapsedTime(&sms, ix->ev1, ix->ev_sp));
+        HSA_HIP(hipMemcpy(sc4, ctr_s + 40, sizeof sc4, hipMemcpyDeviceToHost));
+        sst->kernel_ms = sms;
+        sst->extensions = sc4[0]; sst->pops = sc4[1]; sst->sa_lookups = sc4[2]; sst->not_answered = sc4[3];
+    }
     // anchor calls' hit offsets into the one hits array; unfinished calls -2
     int32_t *cn = (int32_t *)(h + q_n);
     const uint32_t *cf = (const uint32_t *)(h + q_fl);
@@ -953,6 +976,26 @@ extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *se
                 (unsigned long long)(nh_s + nh_a), (unsigned long long)n_sa, 1e3 * (t.tv_sec + 1e-9 * t.tv_nsec - t0), ms);
     }
     return 0;
+}
+
+extern "C" int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
+                                         int n, const uint32_t *lens, const uint64_t *offs, const uint8_t *codes,
+                                         size_t codes_len, const int32_t *anchor_max_diff, hsa_splice_pf_t *out)
+{
+    return pf_batch(ix, seed_rg, anchor_rg, n, lens, offs, codes, codes_len, anchor_max_diff, out, nullptr, nullptr,
+                    nullptr);
+}
+
+extern "C" int hsa_splice_match_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
+                                      const hsa_regime_t *ext_rg, int n, const uint32_t *lens, const uint64_t *offs,
+                                      const uint8_t *codes, size_t codes_len, const int32_t *anchor_max_diff,
+                                      hsa_splice_pf_t *pf, uint32_t *res, hsa_splice_stats_t *stats)
+{
+    if (!ext_rg || (n > 0 && !res) || !pf) {
+        hsa_set_error("hsa_splice_match_batch: null argument");
+        return HSA_E_ARG;
+    }
+    return pf_batch(ix, seed_rg, anchor_rg, n, lens, offs, codes, codes_len, anchor_max_diff, pf, ext_rg, res, stats);
 }
 
 extern "C" int hsa_pass_times(hsa_index_t *ix, int n, float *widths_ms, float *search_ms)

@@ -143,6 +143,24 @@ def read_pac(prefix: str, T: int | None = None) -> np.ndarray:
     return codes[:T].astype(np.uint8)
 
 
+def read_packed_dna(prefix: str):
+    """prefix.index.pac as the HSP holds it in memory (DNALoadPacked with word packing,
+    TextConverter.c:677-725): dnaLength = (file bytes - 1) * 4 + the last byte; then
+    (dnaLength + 15) / 16 + 1 words, the file's bytes (less the last) read into them,
+    the last two words zeroed first, and every word but the last byte-swapped so that
+    code k sits at bits (~k & 15) * 2.  Returns (words, dnaLength)."""
+    raw = np.fromfile(prefix + ".index.pac", dtype=np.uint8)
+    flen = len(raw) - 1
+    T = flen * 4 + int(raw[-1])
+    wtp = (T + 15) // 16
+    buf = np.zeros(4 * (wtp + 1), np.uint8)
+    n = min(flen, len(buf))
+    buf[:n] = raw[:n]
+    w = buf.view("<u4").copy()
+    w[:wtp] = buf[:4 * wtp].view(">u4")
+    return w.astype(np.uint32), T
+
+
 def pack_lsb_u32(codes: np.ndarray) -> np.ndarray:
     """2-bit codes -> 16 per u32, code j at bits 2j..2j+1 (the device text layout)."""
     n = len(codes)

@@ -337,6 +337,43 @@ int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, cons
                               const uint32_t *lens, const uint64_t *offs, const uint8_t *codes, size_t codes_len,
                               const int32_t *anchor_max_diff, hsa_splice_pf_t *out);
 
+/* ---- the splice path itself on the device ----
+ * bwt_splice_match (bwtgap.c:748-1332) for the same n reads: the prefetch pass above,
+ * then one persistent kernel that runs each read's seed correlation
+ * (bwt_aln_corelate_check, :669), motif scan of the reference (splice_site_search_from_pos,
+ * :523), seed extensions (bwt_extend_backward / _foreward, :640-663) and intron-end
+ * checks (check_site_by_intron_end, :602) on the device (hsa_amd/csrc/hsa_splice.hip).
+ * ext_rg is the extensions' regime: the read's local_opt with max_gape 3 (aux_ext,
+ * :776-782; its GAPE bit is the local_opt's, the kernel clears and sets it where the
+ * reference does); max_diff per read is anchor_max_diff[r]; n_stacks <=
+ * HSA_SP_MAX_STACKS.  Needs hsa_index_set_sa and hsa_index_set_text.
+ * res: HSA_SP_RES_WORDS u32 per read: status, n_aln (0, 1 or 2), then res_aln[0] and
+ * res_aln[1] (9 words each, bwt_aln1_t) as bwt_splice_match returns them.  status 0: the
+ * answer; HSA_SP_* > 0: not answered (the reference's code leaves that read undefined
+ * here, or it outgrew the kernel's per-lane stack of HSA_SPLICE_CAP entries, or a
+ * prefetched search of it did not finish) -- run the host's bwt_splice_match for it.
+ * `pf` receives the prefetch tables as hsa_splice_prefetch_batch does (for those reads). */
+#define HSA_SP_RES_WORDS 20
+#define HSA_SP_MAX_STACKS 128
+#define HSA_SP_OK     0
+#define HSA_SP_CALL   1   /* a seed or anchor search of the read did not finish */
+#define HSA_SP_CAP    2   /* an extension outgrew the per-lane stack */
+#define HSA_SP_SCORE  3   /* an extension entry's score past the stack's buckets */
+#define HSA_SP_RANK   4   /* a rank position past the text */
+#define HSA_SP_WIN    5   /* a read or width position outside the read */
+#define HSA_SP_SA     6   /* an SA position in no chromosome block (stale seq id in the reference) */
+#define HSA_SP_TEXT   7   /* a text position past the packed reference */
+#define HSA_SP_LOOP   8   /* a loop bound the reference does not keep (u32 wrap, buffer) */
+int hsa_index_set_text(hsa_index_t *ix, const uint32_t *packed, uint64_t n_words, uint32_t dna_len);
+typedef struct {
+    double kernel_ms;             /* the splice kernel's device time */
+    uint64_t extensions, pops, sa_lookups, not_answered;
+} hsa_splice_stats_t;
+int hsa_splice_match_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
+                           const hsa_regime_t *ext_rg, int n, const uint32_t *lens, const uint64_t *offs,
+                           const uint8_t *codes, size_t codes_len, const int32_t *anchor_max_diff, hsa_splice_pf_t *pf,
+                           uint32_t *res, hsa_splice_stats_t *stats);
+
 /* SA index -> text position (BWTSaValue BWT.c:1195 + BWTRetrievePositionFromSAIndex
  * 2BWT-Interface.c:329), batched.  hsa_index_set_sa uploads the sampled suffix array
  * as BWTLoad holds it (values[0] = -1, (T+s)/s values, interval s) and the chromosome

@@ -344,3 +344,22 @@ int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, cons
     out->n_hits = g_pf_hits.n; out->n_sa = g_pf_nsa;
     return 0;
 }
+
+/* The splice kernel (hsa_splice.hip) has no restatement here: the sanitized drop-in takes
+ * the host's bwt_splice_match for every fallback read, as it does on an index without the
+ * packed text. */
+int hsa_index_set_text(hsa_index_t *ix, const uint32_t *packed, uint64_t n_words, uint32_t dna_len)
+{
+    (void)ix; (void)packed; (void)n_words; (void)dna_len;
+    return 0;
+}
+
+int hsa_splice_match_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
+                           const hsa_regime_t *ext_rg, int n, const uint32_t *lens, const uint64_t *offs,
+                           const uint8_t *codes, size_t codes_len, const int32_t *anchor_max_diff, hsa_splice_pf_t *pf,
+                           uint32_t *res, hsa_splice_stats_t *stats)
+{
+    (void)ix; (void)seed_rg; (void)anchor_rg; (void)ext_rg; (void)n; (void)lens; (void)offs; (void)codes;
+    (void)codes_len; (void)anchor_max_diff; (void)pf; (void)res; (void)stats;
+    return HSA_E_ARG;
+}

@@ -77,17 +77,25 @@ HSA_GPU_ALL = os.path.join(ROOT, "oracle", "_ref", "HSA_gpu_all")
                                             ("splice_default", "splice_reads", {}), ("splice_n4o1", "splice_reads", {}),
                                             ("splice_n4o1O120", "splice_reads", {}),
                                             ("splice_n4o1", "splice_reads",
-                                             {"HSA_SPLICE_PREFETCH": "0", "HSA_SPLICE_THREADS": "4"})])
+                                             {"HSA_SPLICE_PREFETCH": "0", "HSA_SPLICE_THREADS": "4",
+                                              "HSA_SPLICE_DEVICE": "0"}),
+                                            ("splice_default", "splice_reads", {"HSA_SPLICE_DEVICE": "0"}),
+                                            ("splice_n4o1", "splice_reads", {"HSA_SPLICE_CAP": "6"})])
 def test_dropin_all_entry_points_sam_identical(name, reads, env):
     """Every drop-in entry point replaced at once (oracle/ref.mk HSA_gpu_all):
     bwa_cal_sa_reg_gap, bwt_match_gap, and the SAM stage's bwa_cal_pac_pos, whose SA ->
     position lookups (seq_id, position and the duplicate filter of the extra hits in
     every SAM line) run as one GPU batch per read batch (hsa_amd/csrc/bwtse_gpu.c).
-    splice_n4o1O120 (-O 120): n_stacks 283, more score LIFOs than an extension slice slot
-    holds, so the splice path's extensions run through hsa_extend_batch.
-    HSA_SPLICE_PREFETCH=0 with 4 runner threads: no splice tables, so every seed and
-    anchor search and every width of the splice path is a direct GPU call, made from
-    four host threads at once (the calls serialise on slot 0's index)."""
+    By default the splice path runs on the device (hsa_splice.hip).
+    splice_n4o1O120 (-O 120): n_stacks 283, more score buckets than the splice kernel and
+    an extension slice slot hold, so the host's bwt_splice_match runs with its extensions
+    through hsa_extend_batch.
+    HSA_SPLICE_DEVICE=0: the host's bwt_splice_match for every fallback read (coroutine
+    runner); with HSA_SPLICE_PREFETCH=0 and 4 runner threads there are no splice tables,
+    so every seed and anchor search and every width of the splice path is a direct GPU
+    call, made from four host threads at once (the calls serialise on slot 0's index).
+    HSA_SPLICE_CAP=6: the splice kernel's per-lane stack holds 6 entries, so most reads
+    outgrow it and go to the host's path while the rest are answered on the device."""
     idx = os.path.join(GOLD, "index", "tiny.fa")
     fq = os.path.join(GOLD, MAN[reads])
     r = subprocess.run([HSA_GPU_ALL, "aln", *MAN[name]["args"], idx, fq], capture_output=True, timeout=120,

@@ -10,7 +10,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 5 --warmup 1 --streams 1 --cpu-sample 0 --parity-sample 0 --ref-sample 0 --dropin 0 --e2e-reads 0 $BENCH_ARGS"
+BENCH="$R/bench.py --steps 5 --warmup 1 --streams 1 --cpu-sample 0 --parity-sample 0 --ref-sample 0 --dropin 0 --e2e-reads 0 --copies 0 $BENCH_ARGS"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $BENCH > $OUT/trace.json 2> $OUT/trace.err || exit 11
 pmc() {  # name, counters...
