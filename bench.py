@@ -458,8 +458,9 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
                          f"single-threaded), index files from the device-built BWTs; search seconds per process "
                          f"{min(ts):.1f}-{max(ts):.1f} (index load excluded)"}
         log(f"[bench] reference CPU path: {ref['value']:.0f} reads/s on {procs} cores ({ref['value_1core']:.0f} per core)")
+        r_n, r_h = read_probe_out(os.path.join(d, "ref_out0.bin"))      # process 0: the first `per` reads
         if e2e_reads <= 0:
-            return {"reference": ref, "dropin_e2e": None}
+            return {"reference": ref, "dropin_e2e": None, "ref0": (r_n, r_h)}
         # the drop-in end to end on the same files: bwa_seq_t batches of 100 000 reads
         rb = os.path.join(d, "e2e_reads.bin")
         write_reads_bin(rb, reads_all[:e2e_reads])
@@ -487,7 +488,6 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
         # parity through the real entry point: rank 0's reads are a prefix of the first
         # 100 000-read batch in both runs, so their hits (splice path's included) agree
         g_n, g_h = read_probe_out(os.path.join(d, "gpu_out.bin"))
-        r_n, r_h = read_probe_out(os.path.join(d, "ref_out0.bin"))
         m = len(r_n)
         go = np.concatenate([[0], np.cumsum(np.maximum(g_n, 0).astype(np.int64))])
         ro = np.concatenate([[0], np.cumsum(np.maximum(r_n, 0).astype(np.int64))])
@@ -506,7 +506,7 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
         log(f"[bench] drop-in end to end: {e2e['value']:.0f} reads/s ({e2e_reads} reads in calls of {REF_BATCH}, "
             f"{n_fb} fallback reads; main search {search_s:.3f} s, splice prefetch {prefetch_s:.3f} s, splice path "
             f"{splice_s:.3f} s); {len(bad)} of {m} reads differ from the reference")
-        return {"reference": ref, "dropin_e2e": e2e}
+        return {"reference": ref, "dropin_e2e": e2e, "ref0": (r_n, r_h)}
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -652,16 +652,16 @@ def main():
                          o=torch.zeros(a.batch, dtype=torch.int64, device="cuda"),
                          h=torch.zeros(hit_cap * HW, dtype=torch.int32, device="cuda"),
                          c=torch.zeros(16, dtype=torch.int64, device="cuda")))
-        if a.config == 4:   # the splice seeds: six records per read
-            outs[-1].update(sn=torch.zeros(6 * a.batch, dtype=torch.int32, device="cuda"),
-                            so=torch.zeros(6 * a.batch, dtype=torch.int64, device="cuda"),
-                            sh=torch.zeros(6 * a.batch * 4 * 9, dtype=torch.int32, device="cuda"),
-                            sc=torch.zeros(16, dtype=torch.int64, device="cuda"))
+        if a.config == 4:   # the splice path's answers: HSA_SP_RES_WORDS words per read
+            outs[-1].update(res=torch.zeros(a.batch * _lib.SP_RES_WORDS, dtype=torch.int32, device="cuda"),
+                            sc=torch.zeros(8, dtype=torch.int64, device="cuda"))
     if a.config == 4:
         from hsa_amd import splice
-        from hsa_amd._lib import SeedBatch, regime_of
+        from hsa_amd._lib import SpliceBatch, anchor_regime, ext_regime, regime_of
         so_opt = splice.seed_options(opt.as_dict())
         srg = regime_of(so_opt, n_stacks, so_opt["max_diff"])
+        arg_ = anchor_regime(opt.as_dict(), n_stacks, opt.max_diff)
+        erg = ext_regime(opt.as_dict(), n_stacks, opt.max_diff)
 
     handles = [gi] + [gi.clone() for _ in range(max(1, a.streams) - 1)]
 
@@ -674,11 +674,10 @@ def main():
                         d_hits=o["h"].data_ptr(), hit_cap=hit_cap, d_counters=o["c"].data_ptr(),
                         max_len=RL, max_seed=opt.seed_len)
         (gi.search_device64 if wide else gi.search_device)([rg], b)
-        if a.config == 4:   # same stream: the seeds read the main pass's flags
-            gi.splice_seeds_device(srg, SeedBatch(
+        if a.config == 4:   # same stream: the splice path of the main pass's fallback reads
+            gi.splice_device(srg, arg_, erg, SpliceBatch(
                 d_jobs=d_jobs.data_ptr(), n_jobs=a.batch, d_codes=d_codes[j].data_ptr(), d_flags=o["f"].data_ptr(),
-                d_n_aln=o["sn"].data_ptr(), d_hit_off=o["so"].data_ptr(), d_hits=o["sh"].data_ptr(),
-                hit_cap=6 * a.batch * 4, d_counters=o["sc"].data_ptr(), max_len=RL))
+                d_n_aln=o["n"].data_ptr(), d_res=o["res"].data_ptr(), d_counters=o["sc"].data_ptr(), max_len=RL))
 
     # the measured ceiling for this access pattern: random whole 64-B blocks over a
     # table as large as the rank index (before the timed region, same process)
@@ -734,9 +733,9 @@ def main():
     w_ms = np.concatenate([p[0] for p in pt]).astype(float)
     s_ms = np.concatenate([p[1] for p in pt]).astype(float)
     n_pt = len(w_ms)
-    seeds_ms = float(np.mean(kms[-n_pt:]) - np.mean(w_ms) - np.mean(s_ms)) if a.config == 4 else None
+    splice_ms = float(np.mean(kms[-n_pt:]) - np.mean(w_ms) - np.mean(s_ms)) if a.config == 4 else None
     log(f"[bench] rank {rank}: per-step kernels: k_widths {np.mean(w_ms):.2f} ms, k_search {np.mean(s_ms):.2f} ms"
-        + (f", splice seeds {np.mean(seeds_ms):.2f} ms" if a.config == 4 else ""))
+        + (f", splice path {splice_ms:.2f} ms" if a.config == 4 else ""))
     if os.environ.get("HSA_DIAG_OUT"):
         diag_dump(os.environ["HSA_DIAG_OUT"])
     log(f"[bench] rank {rank}: per-step device ms {[round(x, 2) for x in kms]}, wall {elapsed * 1e3:.1f} ms")
@@ -815,10 +814,23 @@ def main():
     if unfinished:
         log(f"[bench] WARNING: {unfinished} reads unfinished (hit buffer too small)")
     seed_queries = 0
-    if a.config == 4:   # the seed searches' rank queries and their prefix widths'
+    splice = None
+    if a.config == 4:   # the splice path: its seed and anchor searches' rank queries (with their widths)
         sctr = np.stack([outs[j]["sc"].cpu().numpy() * per[j] for j in used])
-        seed_queries = int(sctr[:, 2].sum() + sctr[:, 7].sum())
+        seed_queries = int(sctr[:, 5].sum())
         queries += seed_queries
+        nfb = max(int(sctr[:, 0].sum()), 1)
+        res_all = [outs[j]["res"].cpu().numpy().view(np.uint32).reshape(-1, _lib.SP_RES_WORDS) for j in used]
+        splice = {"reads": int(sctr[:, 0].sum()), "extensions_per_read": round(int(sctr[:, 1].sum()) / nfb, 2),
+                  "extension_pops_per_read": round(int(sctr[:, 2].sum()) / nfb, 1),
+                  "sa_lookups_per_read": round(int(sctr[:, 3].sum()) / nfb, 1),
+                  "not_answered": int(sctr[:, 4].sum()),
+                  "spliced_reads": int(sum(int(((r[:, 0] == 0) & (r[:, 1] > 0)).sum()) * per[j]
+                                           for r, j in zip(res_all, used))),
+                  "what": "bwt_splice_match of every fallback read on the device (hsa_splice_device: the seed and "
+                          "anchor searches, then hsa_splice.hip's kernel: correlation, motif scan, extensions, "
+                          "intron-end checks); not_answered = reads the kernel hands to the host's bwt_splice_match "
+                          "(outside the timed step)"}
     blocks = int(ctr[:, 3].sum())
     pops = int(ctr[:, 4].sum())
     flags = np.concatenate([np.tile(outs[j]["f"].cpu().numpy(), per[j]) for j in used])
@@ -898,9 +910,9 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "u64" if wide else "u32", "data": "synthetic",
             "config": {"workload": f"{a.batch // 1000}k x {RL}bp reads per step and GPU, "
                                    + {2: "0-4 substitutions", 3: "one 1-3 bp indel + 0-2 substitutions",
-                                      4: "spliced (exon 40-110 bp, GT..AG intron 200-5000 bp), main path + the splice "
-                                         "path's 6 seed searches per fallback read on the GPU (the host's "
-                                         "correlation/extension not included)",
+                                      4: "spliced (exon 40-110 bp, GT..AG intron 200-5000 bp), main path + the whole "
+                                         "splice path of every fallback read on the GPU (seeds, anchors, correlation, "
+                                         "motif scan, extensions, intron-end checks: hsa_splice_device)",
                                       5: "0-4 substitutions, 64-bit SA intervals (hsa_search_device64)"}[a.config]
                                    + f", 50% rc, vs synthetic {'plant-scale' if T >= 1 << 32 else 'hg19-sized'} 2BWT ({T} bp, "
                                    f"{RECORDS} records), {opt_str} (BASELINE configs[{a.config - 1}]); "
@@ -952,7 +964,8 @@ def main():
             result["value_with_copies"] = copies
         if a.config == 4:
             result["seed_rank_queries_per_read"] = round(seed_queries / reads_local, 1)
-            result["roofline"]["splice_seeds_ms"] = round(float(np.mean(seeds_ms)), 3)
+            result["roofline"]["splice_path_ms"] = round(splice_ms, 3)
+            result["splice_path"] = splice
         if gather is not None:
             result["gather"] = gather
 
@@ -1079,39 +1092,6 @@ def main():
                     bad += 1
             result["parity_sample"] = {"reads": n, "mismatching_reads": bad, "against": "oracle (C restatement)"}
             log(f"[bench] parity sample: {n} reads, {bad} differ from the CPU restatement")
-            if a.config == 4:   # the seed searches of the sample's first fallback reads
-                fb = np.flatnonzero(o_f & 1)[:300]
-                sb = splice.seed_calls_fixed(r0[fb], od, lambda wl, wc: cpu_widths(ox, wl, wc))
-                g_sn = last["sn"].cpu().numpy()
-                g_so = last["so"].cpu().numpy()
-                g_sh = last["sh"].cpu().numpy().view(np.uint32).reshape(-1, 9)
-                sbad = 0
-                for c in sb["calls"]:
-                    o = Opt.from_dict(dict(sb["opt"], seed_len=int(c["len"])))
-                    exp, _ = ox.match_gap(o, n_stacks, sb["codes"][c["off"]:c["off"] + c["len"]], c["strand"],
-                                          sb["widths"][c["wb_off"]:c["wb_off"] + c["len"] + 1], 2)
-                    r = 6 * int(fb[c["read"]]) + int(c["i"])
-                    sbad += not np.array_equal(g_sh[g_so[r]:g_so[r] + g_sn[r]], exp)
-                result["parity_sample"]["seed_calls"] = len(sb["calls"])
-                result["parity_sample"]["mismatching_seed_calls"] = sbad
-                log(f"[bench] parity sample: {len(sb['calls'])} seed calls, {sbad} differ from the CPU restatement")
-        if a.cpu_sample and a.config == 4:
-            # main path + the seed searches of its fallback reads, 1 thread (the seed calls
-            # are driven from Python one by one, so threads would contend on the GIL)
-            n = min(a.cpu_sample // 4, a.batch)
-            rs = batches[(a.warmup + 1) % nd][-n:]
-            t0 = time.perf_counter()
-            _, fl, _, _ = ox.cal_sa_reg_gap(np.full(n, RL, np.uint32), rs.reshape(-1), Opt.from_dict(od))
-            sb = splice.seed_calls_fixed(rs[np.flatnonzero(fl & 1)], od, lambda wl, wc: cpu_widths(ox, wl, wc))
-            for c in sb["calls"]:
-                ox.match_gap(Opt.from_dict(dict(sb["opt"], seed_len=int(c["len"]))), n_stacks,
-                             sb["codes"][c["off"]:c["off"] + c["len"]], c["strand"],
-                             sb["widths"][c["wb_off"]:c["wb_off"] + c["len"] + 1], 2)
-            dt1 = time.perf_counter() - t0
-            result["cpu_baseline"] = {"value": round(n / dt1, 1), "unit": "reads/s", "cores": 1, "kind": "port",
-                                      "sample": f"{n} reads of the same workload: bwa_cal_sa_reg_gap restatement + "
-                                                f"the 6 seed searches of its {int((fl & 1).sum())} fallback reads, "
-                                                f"1 thread, in {dt1:.1f} s"}
     # the reference's own CPU path, and the drop-in end to end (rank 0, configs 2-4; config
     # 4's end to end runs the whole splice path of its fallback reads)
     # With N ranks it runs after the gather on rank 0, over the CPU share of all N ranks
@@ -1120,7 +1100,9 @@ def main():
     if ref_legs:
         procs = ref_procs
         j0 = a.warmup % nd
-        opt_args = ["-n", "4", "-o", str(max_gapo)]
+        # -G: the reference starts in the steady state of a process's later batches, the
+        # state of the timed batches (GAPE cleared in the caller's block)
+        opt_args = ["-n", "4", "-o", str(max_gapo), "-G"]
         try:
             legs = reference_legs(T, res, extra, batches[j0], opt_args, min(a.ref_sample, a.batch), procs,
                                   min(a.e2e_reads, a.batch) if world == 1 else 0)
@@ -1149,6 +1131,38 @@ def main():
                                "may use 16 CPU processes on the box"}
             if legs.get("dropin_e2e"):
                 result["dropin_e2e"] = legs["dropin_e2e"]
+            if a.config == 4 and legs.get("ref0"):
+                # the timed step's results (main path, then the splice path on the device)
+                # against the reference's own bwa_cal_sa_reg_gap on the same reads
+                r_n, r_h = legs["ref0"]
+                o = outs[j0]
+                g_n, g_f, g_o = o["n"].cpu().numpy(), o["f"].cpu().numpy(), o["o"].cpu().numpy()
+                g_h = o["h"].cpu().numpy().view(np.uint32).reshape(-1, HW)
+                g_r = o["res"].cpu().numpy().view(np.uint32).reshape(-1, _lib.SP_RES_WORDS)
+                ro = np.concatenate([[0], np.cumsum(np.maximum(r_n, 0).astype(np.int64))])
+                bad, na_, spl = [], 0, 0
+                for i in range(len(r_n)):
+                    if g_n[i] > 0:
+                        got = g_h[g_o[i]:g_o[i] + g_n[i]]
+                    elif g_f[i] & 1:
+                        if g_r[i, 0] != 0:
+                            na_ += 1
+                            continue
+                        got = g_r[i, 2:2 + 9 * g_r[i, 1]].reshape(-1, 9)
+                        spl += g_r[i, 1] > 0
+                    else:
+                        got = np.zeros((0, 9), np.uint32)
+                    if len(got) != max(r_n[i], 0) or not np.array_equal(got, r_h[ro[i]:ro[i + 1]]):
+                        bad.append(i)
+                result["parity_reference"] = {
+                    "reads": len(r_n), "mismatching_reads": len(bad), "first_mismatch": bad[0] if bad else None,
+                    "not_answered_on_device": na_, "spliced_reads": int(spl),
+                    "against": "the reference's own bwa_cal_sa_reg_gap (oracle/_ref/ref_probe -G, steady-state "
+                               "batch) on the first reads of the timed read set: n_aln and every bwt_aln1_t word of "
+                               "every hit, main path and splice path"}
+                log(f"[bench] the timed step vs the reference: {len(r_n)} reads, {len(bad)} differ ({spl} spliced, "
+                    f"{na_} not answered on the device)")
+
         else:
             result["reference_legs"] = legs
     if rank == 0:

@@ -33,6 +33,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
     "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced", "hsa_index_trie",
     "hsa_index_clone", "hsa_splice_prefetch_batch", "hsa_index_set_text", "hsa_splice_match_batch",
+    "hsa_splice_device",
 ]
 SP_RES_WORDS = 20  # hsa_splice_match_batch's per-read answer (include/hsa_gpu.h)
 ALN64_WORDS = 14   # hsa_aln64_t (include/hsa_gpu.h)
@@ -138,6 +139,26 @@ class SplicePf(C.Structure):
                 ("n_sa", C.c_uint64), ("kernel_ms", C.c_double)]
 
 
+class SpliceBatch(C.Structure):
+    """hsa_splice_batch_t (include/hsa_gpu.h): the splice path of a device batch."""
+    _fields_ = [("d_jobs", C.c_void_p), ("n_jobs", C.c_int), ("d_codes", C.c_void_p), ("d_flags", C.c_void_p),
+                ("d_n_aln", C.c_void_p), ("d_res", C.c_void_p), ("d_counters", C.c_void_p), ("max_len", C.c_int32)]
+
+
+def ext_regime(local_opt: dict, n_stacks: int, max_diff: int) -> "Regime":
+    """The splice path's extension regime (aux_ext: local_opt with max_gape 3,
+    bwtgap.c:776-782); GAPE / LOGGAP as the extension reads them, whatever max_gapo."""
+    ao = dict(local_opt, max_gape=3)
+    r = regime_of(ao, n_stacks, max_diff)
+    r.mode = ao["mode"] & (0x01 | 0x04 | 0x10)
+    return r
+
+
+def anchor_regime(local_opt: dict, n_stacks: int, max_diff: int) -> "Regime":
+    """The 12-mer anchors' regime (aux_ext's options, bwt_match_gap with width_seed NULL)."""
+    return regime_of(dict(local_opt, max_gape=3), n_stacks, max_diff)
+
+
 class SpliceStats(C.Structure):
     """hsa_splice_stats_t (include/hsa_gpu.h)."""
     _fields_ = [("kernel_ms", C.c_double), ("extensions", C.c_uint64), ("pops", C.c_uint64),
@@ -211,6 +232,9 @@ def lib():
     if hasattr(L, "hsa_splice_prefetch_batch"):
         L.hsa_splice_prefetch_batch.argtypes = [vp, C.POINTER(Regime), C.POINTER(Regime), C.c_int, u32, u64, u8,
                                                 C.c_size_t, i32, C.POINTER(SplicePf)]
+    if hasattr(L, "hsa_splice_device"):
+        L.hsa_splice_device.argtypes = [vp, C.POINTER(Regime), C.POINTER(Regime), C.POINTER(Regime),
+                                        C.POINTER(SpliceBatch), vp]
     if hasattr(L, "hsa_splice_match_batch"):
         L.hsa_index_set_text.argtypes = [vp, u32, C.c_uint64, C.c_uint32]
         L.hsa_splice_match_batch.argtypes = [vp, C.POINTER(Regime), C.POINTER(Regime), C.POINTER(Regime), C.c_int, u32,
@@ -395,6 +419,12 @@ class GpuIndex:
         the high bits; hsa_index_set_text) for the splice kernel."""
         w = np.ascontiguousarray(packed_words, np.uint32)
         check(lib().hsa_index_set_text(self.h, w, len(w), int(dna_len)))
+
+    def splice_device(self, seed_regime, anchor_regime, ext_regime, batch: "SpliceBatch"):
+        """bwt_splice_match of every fallback read of a device batch, on the device
+        (hsa_splice_device): HSA_SP_RES_WORDS words per job at batch.d_res."""
+        check(lib().hsa_splice_device(self.h, C.byref(seed_regime), C.byref(anchor_regime), C.byref(ext_regime),
+                                      C.byref(batch), None))
 
     def splice_match(self, seed_regime, anchor_regime, ext_regime, lens, codes, max_diff):
         """hsa_splice_match_batch: bwt_splice_match of each read on the device.  Returns

@@ -125,6 +125,8 @@ struct PfDev {
     const uint32_t *call_fl;
     const uint64_t *call_hit;      // record index in hits_s (seeds) / hits_a (anchors)
     const uint32_t *hits_s, *hits_a;
+    const unsigned long long *d_n; // the reads' count on the device (hsa_splice_device), or null: n
+    const int32_t *idx;            // answer of read r at res[idx[r]] (hsa_splice_device), or null: r
 };
 // bwt_splice_match for the prefetch's reads on the device (d_res: HSA_SP_RES_WORDS u32
 // per read); ext_rg: the extension regime (local_opt with max_gape 3, bwtgap.c:777-782)

@@ -589,7 +589,10 @@ struct PfArgs {
     int32_t *call_n;                        // 8 n
     uint32_t *call_fl;
     unsigned long long *acount;             // anchor calls listed
+    const unsigned long long *d_n;          // the reads' count on the device (hsa_splice_device), or null: n
 };
+
+__device__ __forceinline__ uint32_t pf_n(const PfArgs &a) { return a.d_n ? (uint32_t)*a.d_n : a.n; }
 
 __device__ __forceinline__ uint32_t pf_base(const PfArgs &a, uint32_t r, uint32_t s, uint32_t p)
 {
@@ -605,7 +608,7 @@ __global__ void __launch_bounds__(BLOCK) k_pf_rows(PfArgs a)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t r = t / 6u, s = (t % 6u) & 1u, kind = (t % 6u) >> 1;
-    if (r >= a.n) return;
+    if (r >= pf_n(a)) return;
     const uint32_t L = a.lens[r];
     int32_t *const o = a.rows + 2 * ((size_t)r * 6u + kind * 2u + s) * a.rs;
     uint32_t k = 0, l = a.T, bid = 0;
@@ -656,7 +659,7 @@ __global__ void __launch_bounds__(BLOCK) k_pf_seeds(PfArgs a)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t r = t / 6u, i = t % 6u, s = i / 3u, tt = i % 3u;
-    if (r >= a.n) return;
+    if (r >= pf_n(a)) return;
     const uint32_t L = a.lens[r], sl = L / 3u, la = sl + (tt == 2u ? L % 3u : 0u);
     const uint32_t call = 8u * r + i;
     a.list[6u * r + i] = (int32_t)call;
@@ -688,7 +691,7 @@ __global__ void __launch_bounds__(BLOCK) k_pf_anchors(PfArgs a)
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t r = t >> 1, s = t & 1u;
-    if (r >= a.n) return;
+    if (r >= pf_n(a)) return;
     const uint32_t L = a.lens[r], call = 8u * r + 6u + s;
     const int32_t *const cn = a.call_n + 8u * r + 3u * s;
     const uint32_t *const cf = a.call_fl + 8u * r + 3u * s;
@@ -862,6 +865,7 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
     A.cw = (int32_t *)(dq + q_cw); A.list = (int32_t *)(d + o_list);
     A.call_n = (int32_t *)(dq + q_n); A.call_fl = (uint32_t *)(dq + q_fl);
     A.acount = acnt;
+    A.d_n = nullptr;
     HSA_HIP(hipMemsetAsync(d + o_sc, 4, 2 * N * sc + 64, st));         // padding reads as N
     hipLaunchKernelGGL(k_pf_rows, dim3((unsigned)((6 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
     hipLaunchKernelGGL(k_pf_seeds, dim3((unsigned)((6 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
@@ -922,6 +926,7 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
         pd.lens = A.lens; pd.amd = A.amd; pd.scodes = A.scodes; pd.rows = A.rows; pd.cw = A.cw;
         pd.call_n = A.call_n; pd.call_fl = A.call_fl; pd.call_hit = (const uint64_t *)(dq + q_ho);
         pd.hits_s = (const uint32_t *)(dq + q_hs); pd.hits_a = (const uint32_t *)(dq + q_ha);
+        pd.d_n = nullptr; pd.idx = nullptr;
         if ((rc = hsa_splice_device_launch(ix, pd, *ext_rg, (uint32_t *)(d + o_res), ctr_s + 40, st))) return rc;
         HSA_HIP(hipEventRecord(ix->ev_sp, st));
         HSA_HIP(hipMemcpyAsync(res, d + o_res, N * HSA_SP_RES_WORDS * 4, hipMemcpyDeviceToHost, st));
@@ -975,6 +980,139 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
                         "lookups, %.1f ms (kernels %.1f ms)\n", n, (unsigned long long)n_seed, (unsigned long long)hc[32],
                 (unsigned long long)(nh_s + nh_a), (unsigned long long)n_sa, 1e3 * (t.tv_sec + 1e-9 * t.tv_nsec - t0), ms);
     }
+    return 0;
+}
+
+// ---------------------------------------------------------------- hsa_splice_device
+// The fallback reads of a device batch (the main pass flagged them), compacted: their
+// order does not matter, a read's splice path depends on the read alone.
+__global__ void __launch_bounds__(BLOCK) k_sp_prep(const hsa_job_t *jobs, const uint32_t *flags, const int32_t *n_aln,
+                                                   uint32_t n, uint32_t *lens, uint64_t *offs, int32_t *amd, int32_t *idx,
+                                                   unsigned long long *cnt)
+{
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n || !(flags[j] & HSA_F_FALLBACK) || n_aln[j] != 0) return;
+    const uint32_t r = (uint32_t)atomicAdd(cnt, 1ull);
+    const hsa_job_t J = jobs[j];
+    lens[r] = J.len;
+    offs[r] = J.off;
+    amd[r] = J.max_diff;
+    idx[r] = (int32_t)j;
+}
+
+__global__ void k_sp_calls(const unsigned long long *cnt, unsigned long long *scnt) { *scnt = 6ull * *cnt; }
+
+// the batch's counters: [0] reads, [5] rank queries of the seed and anchor searches and
+// their widths, [6] their hits ([1]-[4] come from the splice kernel)
+__global__ void k_sp_stats(const unsigned long long *cnt, const unsigned long long *ctr_s,
+                           const unsigned long long *ctr_a, unsigned long long *out)
+{
+    out[0] = *cnt;
+    out[5] = ctr_s[2] + ctr_s[7] + ctr_a[2] + ctr_a[7];
+    out[6] = ctr_s[1] + ctr_a[1];
+}
+
+extern "C" int hsa_splice_device(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
+                                 const hsa_regime_t *ext_rg, const hsa_splice_batch_t *b, void *stream)
+{
+    if (int rc0 = hsa_need32(ix)) return rc0;
+    if (!seed_rg || !anchor_rg || !ext_rg || !b) { hsa_set_error("hsa_splice_device: null argument"); return HSA_E_ARG; }
+    const hsa_regime_t rg2[2] = {*seed_rg, *anchor_rg};
+    int rc = check_regimes(rg2, 2);
+    if (rc) return rc;
+    if (seed_rg->max_gapo != 0) { hsa_set_error("seed searches have no gap opens (bwtgap.c:772)"); return HSA_E_ARG; }
+    if (!fast_regimes(rg2, 2)) { hsa_set_error("splice path: options outside k_search's layouts"); return HSA_E_ARG; }
+    if (b->max_len < 3 || b->max_len > 3 * (FAST_MAX_LEN - 2) || b->n_jobs < 0) {
+        hsa_set_error("hsa_splice_device: max_len %d / n_jobs %d out of range", b->max_len, b->n_jobs);
+        return HSA_E_ARG;
+    }
+    if (b->n_jobs == 0) return 0;
+    HSA_HIP(hipSetDevice(ix->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+    const size_t N = (size_t)b->n_jobs, calls = 8 * N;
+    const uint32_t M = (uint32_t)b->max_len;
+    const uint32_t sc = (M + 15u) / 16u * 16u + 16u, rs = M + 1u, cws = M / 3u + 3u > 13u ? M / 3u + 3u : 13u;
+    const uint64_t cap_s = 6 * N * 16 + 65536, cap_a = 2 * N * 16 + 16384;
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    size_t o = 0;
+    const size_t o_lens = o; o += al(N * 4);
+    const size_t o_offs = o; o += al(N * 8);
+    const size_t o_amd = o; o += al(N * 4);
+    const size_t o_idx = o; o += al(N * 4);
+    const size_t o_sc = o; o += al(2 * N * sc + 64);
+    const size_t o_jobs = o; o += al(calls * sizeof(hsa_job_t));
+    const size_t o_mg = o; o += al(calls * sizeof(hsa_mg_job_t));
+    const size_t o_list = o; o += al(8 * N * 4);
+    const size_t o_ctr = o; o += 1024;
+    const size_t o_n = o; o += al(calls * 4);
+    const size_t o_fl = o; o += al(calls * 4);
+    const size_t o_ho = o; o += al(calls * 8);
+    const size_t o_rows = o; o += al(N * 6 * rs * 8);
+    const size_t o_cw = o; o += al(calls * cws * 8);
+    const size_t o_hs = o; o += al(cap_s * 36);
+    const size_t o_ha = o; o += al(cap_a * 36);
+    if ((rc = hsa_grow(&ix->d_pf, &ix->d_pf_cap, o + 256))) return rc;
+    char *d = (char *)ix->d_pf;
+    unsigned long long *ctr_s = (unsigned long long *)(d + o_ctr), *ctr_a = ctr_s + 16, *acnt = ctr_s + 32,
+                       *scnt = ctr_s + 34, *rcnt = ctr_s + 35;
+    unsigned long long *out_ctr = (unsigned long long *)b->d_counters;
+    HSA_HIP(hipMemsetAsync(ctr_s, 0, 1024, st));
+    HSA_HIP(hipMemsetAsync(out_ctr, 0, 8 * sizeof(unsigned long long), st));
+    PfArgs A;
+    A.fwd = RankDir{ix->blk[0], ix->isa0};
+    A.rev = RankDir{ix->blk[1], ix->risa0};
+    A.T = ix->T;
+    memcpy(A.C, ix->C, sizeof A.C);
+    A.n = (uint32_t)N; A.max_len = M; A.sc = sc; A.rs = rs; A.cws = cws;
+    A.lens = (const uint32_t *)(d + o_lens); A.offs = (const uint64_t *)(d + o_offs);
+    A.codes = b->d_codes; A.amd = (const int32_t *)(d + o_amd);
+    A.seed_max_diff = seed_rg->max_diff;
+    A.scodes = (uint8_t *)(d + o_sc);
+    A.rows = (int32_t *)(d + o_rows);
+    A.jobs = (hsa_job_t *)(d + o_jobs); A.mg = (hsa_mg_job_t *)(d + o_mg);
+    A.cw = (int32_t *)(d + o_cw); A.list = (int32_t *)(d + o_list);
+    A.call_n = (int32_t *)(d + o_n); A.call_fl = (uint32_t *)(d + o_fl);
+    A.acount = acnt;
+    A.d_n = rcnt;
+    const unsigned grid_n = (unsigned)((N + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(k_sp_prep, dim3(grid_n), dim3(BLOCK), 0, st, b->d_jobs, b->d_flags, b->d_n_aln, (uint32_t)N,
+                       (uint32_t *)(d + o_lens), (uint64_t *)(d + o_offs), (int32_t *)(d + o_amd), (int32_t *)(d + o_idx),
+                       rcnt);
+    hipLaunchKernelGGL(k_sp_calls, dim3(1), dim3(1), 0, st, (const unsigned long long *)rcnt, scnt);
+    HSA_HIP(hipMemsetAsync(d + o_sc, 4, 2 * N * sc + 64, st));         // padding reads as N
+    hipLaunchKernelGGL(k_pf_rows, dim3((unsigned)((6 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
+    hipLaunchKernelGGL(k_pf_seeds, dim3((unsigned)((6 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
+    HSA_HIP(hipGetLastError());
+    void *before = ix->d_in;
+    if ((rc = hsa_grow(&ix->d_in, &ix->d_in_cap, 1536))) return rc;
+    int nb = 0;
+    if ((rc = stage_regimes(ix, rg2, 2, (char *)ix->d_in, nb, st, before != ix->d_in))) return rc;
+    const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
+    const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
+    const bool wide = need_wide(rg2, 2);
+    const MgPass mgp{A.mg, A.cw};
+    // no host round trip: the passes take their job counts from the device (the seed
+    // calls' 6 per read, the anchors k_pf_anchors listed), planned for their upper bounds
+    if ((rc = mg_passes(ix, d_reg, d_bmap, nb, A.jobs, A.list, scnt, (int)(6 * N), (int)(M / 3u + 2u), false, wide,
+                        seed_rg->max_entries, A.scodes, mgp, A.call_n, A.call_fl, (uint64_t *)(d + o_ho),
+                        (uint32_t *)(d + o_hs), cap_s, ctr_s, st)))
+        return rc;
+    hipLaunchKernelGGL(k_pf_anchors, dim3((unsigned)((2 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
+    HSA_HIP(hipGetLastError());
+    if ((rc = mg_passes(ix, d_reg, d_bmap, nb, A.jobs, A.list + 6 * N, acnt, (int)(2 * N), 12, anchor_rg->max_gapo > 0,
+                        wide, anchor_rg->max_entries, A.scodes, mgp, A.call_n, A.call_fl, (uint64_t *)(d + o_ho),
+                        (uint32_t *)(d + o_ha), cap_a, ctr_a, st)))
+        return rc;
+    PfDev pd;
+    pd.n = (uint32_t)N; pd.max_len = M; pd.sc = sc; pd.rs = rs; pd.cws = cws;
+    pd.lens = A.lens; pd.amd = A.amd; pd.scodes = A.scodes; pd.rows = A.rows; pd.cw = A.cw;
+    pd.call_n = A.call_n; pd.call_fl = A.call_fl; pd.call_hit = (const uint64_t *)(d + o_ho);
+    pd.hits_s = (const uint32_t *)(d + o_hs); pd.hits_a = (const uint32_t *)(d + o_ha);
+    pd.d_n = rcnt; pd.idx = (const int32_t *)(d + o_idx);
+    if ((rc = hsa_splice_device_launch(ix, pd, *ext_rg, b->d_res, out_ctr + 1, st))) return rc;
+    hipLaunchKernelGGL(k_sp_stats, dim3(1), dim3(1), 0, st, (const unsigned long long *)rcnt,
+                       (const unsigned long long *)ctr_s, (const unsigned long long *)ctr_a, out_ctr);
+    HSA_HIP(hipGetLastError());
     return 0;
 }
 

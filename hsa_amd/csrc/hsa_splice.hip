@@ -310,7 +310,7 @@ __device__ void sp_skip_motif(SpLane &S, const uint32_t *sites)   // bwtgap.c:94
 
 __device__ void sp_finish(const SpArgs &a, SpLane &S)
 {
-    uint32_t *o = a.res + (size_t)S.read * HSA_SP_RES_WORDS;
+    uint32_t *o = a.res + (size_t)(a.pf.idx ? (uint32_t)a.pf.idx[S.read] : (uint32_t)S.read) * HSA_SP_RES_WORDS;
     o[0] = (uint32_t)S.status;
     o[1] = S.status ? 0u : (uint32_t)S.n_out;
 #pragma unroll
@@ -858,10 +858,11 @@ __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
     S.n_sa = 0;
     bool done = false;
     int cur = -1;
+    const unsigned long long n_reads = a.pf.d_n ? *a.pf.d_n : a.pf.n;
     for (;;) {
         if (!done && cur < 0 && !x_on) {
             const unsigned long long q = atomicAdd(a.next, 1ull);
-            if (q >= a.pf.n) done = true;
+            if (q >= n_reads) done = true;
             else { sp_init(a, S, (int)q); cur = (int)q; }
         }
         if (!__any(!done)) break;                       // every lane of the wave: queue empty, reads done

@@ -369,6 +369,24 @@ typedef struct {
     double kernel_ms;             /* the splice kernel's device time */
     uint64_t extensions, pops, sa_lookups, not_answered;
 } hsa_splice_stats_t;
+/* The same for a device batch: the reads the main pass (hsa_search_device) left with
+ * HSA_F_FALLBACK and no hit go through the prefetch pass and the splice kernel, all on
+ * the device and without a host round trip.  d_res: HSA_SP_RES_WORDS u32 per job of the
+ * batch, written for those reads only; d_counters (>= 8 u64): [0] reads sent to the
+ * splice path, [1] extensions, [2] extension pops, [3] SA lookups, [4] reads not answered,
+ * [5] rank queries of the seed and anchor searches with their widths, [6] their hits.
+ * Each read's max_diff is its job's; max_len the longest read (3 * 1021 at most). */
+typedef struct {
+    const hsa_job_t *d_jobs; int n_jobs;
+    const uint8_t *d_codes;
+    const uint32_t *d_flags;              /* the main pass's per-read flags */
+    const int32_t *d_n_aln;               /* the main pass's per-read hit counts */
+    uint32_t *d_res;
+    uint64_t *d_counters;
+    int32_t max_len;
+} hsa_splice_batch_t;
+int hsa_splice_device(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
+                      const hsa_regime_t *ext_rg, const hsa_splice_batch_t *b, void *stream);
 int hsa_splice_match_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regime_t *anchor_rg,
                            const hsa_regime_t *ext_rg, int n, const uint32_t *lens, const uint64_t *offs,
                            const uint8_t *codes, size_t codes_len, const int32_t *anchor_max_diff, hsa_splice_pf_t *pf,
