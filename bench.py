@@ -136,6 +136,41 @@ def build_index64(T, seed, device):
     return gi, res, {}
 
 
+def msb_words(lsb):
+    """16 two-bit codes per u32: LSB-first (code j at bits 2j) <-> MSB-first (code j at
+    bits 30 - 2j, the .bwt / HSP packedDNA order)."""
+    x = lsb.astype(np.uint32, copy=True)
+    x = (x >> 16) | (x << 16)
+    x = ((x & 0xFF00FF00) >> 8) | ((x & 0x00FF00FF) << 8)
+    x = ((x & 0xF0F0F0F0) >> 4) | ((x & 0x0F0F0F0F) << 4)
+    x = ((x & 0xCCCCCCCC) >> 2) | ((x & 0x33333333) << 2)
+    return x
+
+
+def attach_splice_arrays(gi, T, extra):
+    """What the splice kernel reads besides the rank blocks, as the reference's loaded
+    index holds it: the sampled SA (BWTLoad: values[0] = -1, BWT.c:222) with the record
+    blocks of the synthetic genome's .ann, and the packed text as the HSP holds it
+    ((T + 15) / 16 + 1 words, first code in the high bits; DNALoadPacked)."""
+    from hsa_amd import synth
+    vals = np.ascontiguousarray(extra["sa"], np.uint32).copy()
+    vals[0] = 0xFFFFFFFF
+    blocks = np.array([[r, s0, s0 + n - 1, 0] for r, (s0, n) in enumerate(synth.record_layout(T, RECORDS))],
+                      np.int64).astype(np.uint32)
+    gi.set_sa(index_io_sa(vals), blocks)
+    nw = (T + 15) // 16
+    words = np.zeros(nw + 1, np.uint32)
+    words[:nw] = msb_words(extra["text"][:nw])
+    if T % 16:                  # the .pac holds zero bits past the text (its last byte masked)
+        words[nw - 1] &= np.uint32((0xFFFFFFFF << (32 - 2 * (T % 16))) & 0xFFFFFFFF)
+    gi.set_text(words, T)
+
+
+def index_io_sa(vals):
+    from hsa_amd import index_io
+    return index_io.SaFile(interval=SA_INTERVAL, values=vals)
+
+
 def host_oracle_index64(res, T):
     """The 64-bit restatement's index (liboracle64.so) from the device-built BWTs."""
     from oracle_ctypes import OracleIndex64
@@ -598,7 +633,9 @@ def main():
     if wide:
         gi, res, extra = build_index64(T, GENOME_SEED, device)
     else:
-        gi, res, extra = build_index(T, GENOME_SEED, device, with_files=ref_legs)
+        gi, res, extra = build_index(T, GENOME_SEED, device, with_files=ref_legs or a.config == 4)
+        if a.config == 4:       # the splice kernel's SA -> position and motif scans
+            attach_splice_arrays(gi, T, extra)
     trie_d, trie_sd, trie_b = gi.trie()
     log(f"[bench] rank {rank}: index ready ({gi.nbytes() / 2**30:.2f} GiB of rank blocks, root tries {trie_d}/{trie_sd} "
         f"levels in {trie_b / 2**20:.0f} MiB) in {time.time() - t0:.1f} s")
