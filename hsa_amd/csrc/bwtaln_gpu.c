@@ -901,6 +901,11 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
     if (dev) {
         if (dj.rc == HSA_E_ARG) {                /* not on this index / these options: the host's path */
             if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] splice kernel not used: %s\n", hsa_last_error());
+            if (pf_ok && nh_r > 0) {
+                pf_job_init(&pj, bi_bwt, arr, seqs, offs, tot, max_len, hr, nh_r, &local, sp, n_stacks);
+                pf_job_run(&pj);
+                prefetched = 1;
+            }
         } else if (dj.rc) {
             hsa_gpu_fatal("GPU splice path", dj.rc);
         } else {
