@@ -94,6 +94,9 @@ struct SpArgs {
     PfDev pf;
     hsa_regime_t rg;             // the extension regime; max_diff per read from pf.amd
     uint32_t nb, cap, site_cap, ref_cap, lbuf_words;
+    // score -> bucket over the scores an extension can reach (dense, in score order;
+    // 0xff: none -- a push there is handed back as HSA_SP_SCORE)
+    uint8_t bmap[HSA_SP_MAX_STACKS];
     uint4 *pool;                 // per lane: cap entries x 2 uint4
     SpLane *lanes;
     uint32_t *lbuf;              // per lane: positions (3 x SP_POS_MAX) | sites | reference bytes
@@ -616,12 +619,15 @@ __device__ __forceinline__ int sp_log2(uint32_t v)   // bwtgap.c:107-116
 __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
 {
     extern __shared__ uint32_t s_hn[];                 // per bucket: head | count << 16, lane-interleaved
+    __shared__ uint8_t s_bmap[HSA_SP_MAX_STACKS];
+    for (uint32_t i = threadIdx.x; i < HSA_SP_MAX_STACKS; i += SP_NT) s_bmap[i] = a.bmap[i];
+    __syncthreads();
     const uint32_t lane = blockIdx.x * SP_NT + threadIdx.x;
     SpLane &S = a.lanes[lane];
     uint32_t *const lb = a.lbuf + (size_t)lane * a.lbuf_words;
     uint4 *const P = a.pool + (size_t)lane * a.cap * 2;
     uint32_t *const hn = s_hn + threadIdx.x;
-    const int nst = a.rg.n_stacks;
+    const int nst = (int)a.nb;                          // dense buckets
     const hsa_regime_t &R = a.rg;
 
     // ---- the extension in flight (bwt_backtracing_search, bwtgap.c:346-511; k_extend)
@@ -659,14 +665,16 @@ __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
     };
     auto push = [&](int i, uint32_t k, uint32_t l, uint32_t rk, uint32_t rl, int mm, int go, int ge, int st) {
         const int score = mm * R.s_mm + go * R.s_gapo + ge * R.s_gape;      // gap_push (bwtgap.c:46-75)
-        if (score < 0 || score >= nst) { x_err = HSA_SP_SCORE; return; }
+        if (score < 0 || score >= R.n_stacks) { x_err = HSA_SP_SCORE; return; }
+        const uint32_t bk = s_bmap[score];
+        if (bk == 0xffu) { x_err = HSA_SP_SCORE; return; }
         if (x_pend) flush();
         x_pe0 = make_uint4(k, l, rk, rl);
         x_pe1 = make_uint4((uint32_t)score << 21 | (uint32_t)i,
                            (uint32_t)(mm & 255) | (uint32_t)(go & 255) << 8 | (uint32_t)(ge & 255) << 16 |
                                (uint32_t)(st & 3) << 24,
                            0u, 0u);
-        x_pscore = score;
+        x_pscore = (int)bk;                             // the bucket (score order)
         x_pend = true;
         ++x_nent;
     };
@@ -929,10 +937,27 @@ int hsa_splice_device_launch(hsa_index *ix, const PfDev &pd, const hsa_regime_t 
         return HSA_E_ARG;
     }
     if (pd.n == 0) return 0;
-    const uint32_t nb = (uint32_t)rg.n_stacks;
+    // The buckets: the scores an extension can reach, in score order.  Its entries'
+    // counts: n_mm <= max(max_diff, max_seed_diff) (a seed's hit, or a child of an entry
+    // with a difference left, bwtgap.c:389, :493-502), n_gapo <= max_gapo, n_gape <=
+    // max_gape (:456, :472, :476; the anchors' hits have the same bounds).  A push outside
+    // them is handed back (HSA_SP_SCORE), so the map never changes an answer.
+    uint8_t bmap[HSA_SP_MAX_STACKS];
+    memset(bmap, 0xff, sizeof bmap);
+    const int mmx = rg.max_diff > rg.max_seed_diff ? rg.max_diff : rg.max_seed_diff;
+    for (int mm = 0; mm <= mmx; ++mm)
+        for (int go = 0; go <= rg.max_gapo; ++go)
+            for (int ge = 0; ge <= rg.max_gape; ++ge) {
+                const int sc = mm * rg.s_mm + go * rg.s_gapo + ge * rg.s_gape;
+                if (sc >= 0 && sc < rg.n_stacks) bmap[sc] = 0;
+            }
+    uint32_t nb = 0;
+    for (int sc = 0; sc < rg.n_stacks; ++sc)
+        if (bmap[sc] == 0) bmap[sc] = (uint8_t)nb++;
+    if (nb == 0) nb = 1;
     // workgroups per CU by the bucket table's LDS (160 KB per CU, 16 waves)
     const size_t lds = (size_t)nb * SP_NT * 4;
-    int wpc = (int)((160u << 10) / lds);
+    int wpc = (int)((160u << 10) / (lds + HSA_SP_MAX_STACKS));
     wpc = wpc > 16 ? 16 : wpc < 1 ? 1 : wpc;
     const size_t resident = (size_t)(ix->n_cu > 0 ? ix->n_cu : 256) * (size_t)wpc * SP_NT;
     const size_t want = ((size_t)pd.n + SP_NT - 1) / SP_NT * SP_NT;
@@ -952,6 +977,7 @@ int hsa_splice_device_launch(hsa_index *ix, const PfDev &pd, const hsa_regime_t 
     A.pf = pd;
     A.rg = rg;
     A.nb = nb;
+    memcpy(A.bmap, bmap, sizeof bmap);
     A.cap = cap;
     A.site_cap = 3 * pd.max_len + 8;
     A.ref_cap = pd.max_len + 8;
