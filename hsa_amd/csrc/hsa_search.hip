@@ -904,6 +904,34 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
     S.call_n = A.call_n; S.call_hit = (const uint64_t *)(dq + q_ho);
     S.hits_s = (const uint32_t *)(dq + q_hs); S.hits_a = (const uint32_t *)(dq + q_ha);
     S.call_sa = (unsigned long long *)(dq + q_sa); S.total = satot; S.idx = nullptr;
+    if (ext_rg) {
+        // bwt_splice_match itself (hsa_splice.hip); the host tables (SA lookups, the pinned
+        // copy) serve only the host's bwt_splice_match, which the caller runs with its own
+        // prefetch for the reads the kernel hands back
+        HSA_HIP(hipEventRecord(ix->ev1, st));
+        PfDev pd;
+        pd.n = (uint32_t)n; pd.max_len = M; pd.sc = sc; pd.rs = rs; pd.cws = cws;
+        pd.lens = A.lens; pd.amd = A.amd; pd.scodes = A.scodes; pd.rows = A.rows; pd.cw = A.cw;
+        pd.call_n = A.call_n; pd.call_fl = A.call_fl; pd.call_hit = (const uint64_t *)(dq + q_ho);
+        pd.hits_s = (const uint32_t *)(dq + q_hs); pd.hits_a = (const uint32_t *)(dq + q_ha);
+        pd.d_n = nullptr; pd.idx = nullptr;
+        if ((rc = hsa_splice_device_launch(ix, pd, *ext_rg, (uint32_t *)(d + o_res), ctr_s + 40, st))) return rc;
+        HSA_HIP(hipEventRecord(ix->ev_sp, st));
+        HSA_HIP(hipMemcpyAsync(res, d + o_res, N * HSA_SP_RES_WORDS * 4, hipMemcpyDeviceToHost, st));
+        unsigned long long sc4[4];
+        HSA_HIP(hipMemcpyAsync(sc4, ctr_s + 40, sizeof sc4, hipMemcpyDeviceToHost, st));
+        HSA_HIP(hipStreamSynchronize(st));
+        float ms = 0, sms = 0;
+        HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+        HSA_HIP(hipEventElapsedTime(&sms, ix->ev1, ix->ev_sp));
+        out->n = n; out->max_len = (int)M; out->row_stride = (int)rs; out->cw_stride = (int)cws;
+        out->kernel_ms = ms;
+        if (sst) {
+            sst->kernel_ms = sms;
+            sst->extensions = sc4[0]; sst->pops = sc4[1]; sst->sa_lookups = sc4[2]; sst->not_answered = sc4[3];
+        }
+        return 0;
+    }
     const bool with_sa = ix->d_sa != nullptr;
     if (with_sa) hipLaunchKernelGGL(k_pf_sa, dim3((unsigned)((calls + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, S, 0);
     HSA_HIP(hipGetLastError());
@@ -920,17 +948,6 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
         if ((rc = hsa_sa_position_device(ix, n_sa, d_idx, d_sao, st))) return rc;
     }
     HSA_HIP(hipEventRecord(ix->ev1, st));
-    if (ext_rg) {                                 // bwt_splice_match itself (hsa_splice.hip)
-        PfDev pd;
-        pd.n = (uint32_t)n; pd.max_len = M; pd.sc = sc; pd.rs = rs; pd.cws = cws;
-        pd.lens = A.lens; pd.amd = A.amd; pd.scodes = A.scodes; pd.rows = A.rows; pd.cw = A.cw;
-        pd.call_n = A.call_n; pd.call_fl = A.call_fl; pd.call_hit = (const uint64_t *)(dq + q_ho);
-        pd.hits_s = (const uint32_t *)(dq + q_hs); pd.hits_a = (const uint32_t *)(dq + q_ha);
-        pd.d_n = nullptr; pd.idx = nullptr;
-        if ((rc = hsa_splice_device_launch(ix, pd, *ext_rg, (uint32_t *)(d + o_res), ctr_s + 40, st))) return rc;
-        HSA_HIP(hipEventRecord(ix->ev_sp, st));
-        HSA_HIP(hipMemcpyAsync(res, d + o_res, N * HSA_SP_RES_WORDS * 4, hipMemcpyDeviceToHost, st));
-    }
     // one copy of the output block (hits up to their counts) into pinned host memory
     const uint64_t nh_s = hc[1] < cap_s ? hc[1] : cap_s, nh_a = hc[16 + 1] < cap_a ? hc[16 + 1] : cap_a;
     const size_t h_need = q_hs + (nh_s + nh_a) * 36 + al(n_sa * 16) + 256;
@@ -949,14 +966,6 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
     HSA_HIP(hipStreamSynchronize(st));
     float ms = 0;
     HSA_HIP(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
-    if (ext_rg && sst) {
-        float sms = 0;
-        unsigned long long sc4[4];
-        HSA_HIP(hipEventElapsedTime(&sms, ix->ev1, ix->ev_sp));
-        HSA_HIP(hipMemcpy(sc4, ctr_s + 40, sizeof sc4, hipMemcpyDeviceToHost));
-        sst->kernel_ms = sms;
-        sst->extensions = sc4[0]; sst->pops = sc4[1]; sst->sa_lookups = sc4[2]; sst->not_answered = sc4[3];
-    }
     // anchor calls' hit offsets into the one hits array; unfinished calls -2
     int32_t *cn = (int32_t *)(h + q_n);
     const uint32_t *cf = (const uint32_t *)(h + q_fl);

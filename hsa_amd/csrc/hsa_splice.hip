@@ -636,7 +636,7 @@ __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
     int x_err = 0, x_ret = 0, x_mode = 0, x_md = 0, x_L = 0, x_bscore = 0;
     uint32_t x_top = 0, x_freel = SP_NIL;
     uint4 x_pe0 = make_uint4(0, 0, 0, 0), x_pe1 = make_uint4(0, 0, 0, 0);
-    uint32_t x_aln[9];
+    uint32_t *x_aln = nullptr;           // the hit being extended: A.a0 (foreward) or C.a0 (backward), in place
     const uint8_t *x_seq = nullptr;
     const int32_t *x_w = nullptr, *x_w6 = nullptr;
     unsigned long long n_pops = 0, n_ext = 0, n_sa = 0;
@@ -708,9 +708,7 @@ __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
         const int rr = S.read;
         x_dir = S.xdir;
         x_len = S.xl;
-        const uint32_t *src = x_dir ? S.C.a0 : S.A.a0;
-#pragma unroll
-        for (int w = 0; w < 9; ++w) x_aln[w] = src[w];
+        x_aln = x_dir ? S.C.a0 : S.A.a0;
         x_start = (int)x_aln[6];
         x_end = (int)x_aln[7];
         x_mp0 = x_mp = S.max_pos;
@@ -888,9 +886,6 @@ __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
                     sp_finish(a, S);
                     cur = -1;
                 } else {
-                    uint32_t *dst = x_dir ? S.C.a0 : S.A.a0;
-#pragma unroll
-                    for (int w = 0; w < 9; ++w) dst[w] = x_aln[w];
                     S.max_pos = x_mp;
                     S.ext_ret = x_ret;
                 }

@@ -351,8 +351,9 @@ int hsa_splice_prefetch_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, cons
  * res_aln[1] (9 words each, bwt_aln1_t) as bwt_splice_match returns them.  status 0: the
  * answer; HSA_SP_* > 0: not answered (the reference's code leaves that read undefined
  * here, or it outgrew the kernel's per-lane stack of HSA_SPLICE_CAP entries, or a
- * prefetched search of it did not finish) -- run the host's bwt_splice_match for it.
- * `pf` receives the prefetch tables as hsa_splice_prefetch_batch does (for those reads). */
+ * prefetched search of it did not finish) -- run the host's bwt_splice_match for it
+ * (with hsa_splice_prefetch_batch of those reads for its tables).  `pf` receives the
+ * pass's shape and kernel_ms only (no tables). */
 #define HSA_SP_RES_WORDS 20
 #define HSA_SP_MAX_STACKS 128
 #define HSA_SP_OK     0
