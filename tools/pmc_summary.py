@@ -25,7 +25,8 @@ import statistics
 import sys
 
 
-STEP_KERNELS = ("k_widths", "k_widths_reads", "k_search", "k_seed_prep", "k_widths_import", "k_widths_export")
+STEP_KERNELS = ("k_widths", "k_widths_reads", "k_search", "k_seed_prep", "k_widths_import", "k_widths_export",
+                "k_sp_prep", "k_pf_rows", "k_pf_seeds", "k_pf_anchors", "k_splice")
 
 
 def counters(d, kernel, every=False):
