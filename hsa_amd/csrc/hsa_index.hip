@@ -5,6 +5,7 @@
 // BWT.c:1018-1059) and answers a rank with two dependent-ish loads and an SSE
 // popcount (BWT.c:532-679).  Here one 16-byte block carries the absolute counts
 // and the 16 codes they precede (hsa_device.h), so one rank query = one load.
+#include <chrono>
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -60,18 +61,27 @@ extern "C" int hsa_configure(int waves_per_cu, int pool_entries, int hit_cap)
     return 0;
 }
 
+// HSA_VERBOSE: device allocations that take more than 5 ms (a first batch's stall)
+static void hsa_log_alloc(const char *what, size_t bytes, std::chrono::steady_clock::time_point t0)
+{
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > 5.0 && getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] %s: hipMalloc of %.2f GB took %.1f ms\n", what, bytes / 1e9, ms);
+}
+
 int hsa_grow(void **p, size_t *cap, size_t need)
 {
     if (need <= *cap && *p) return 0;
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     size_t n = need + need / 4 + 4096;
+    const auto t0 = std::chrono::steady_clock::now();
     if (hipMalloc(p, n) != hipSuccess) {
         *p = nullptr; *cap = 0;
         hsa_set_error("hipMalloc(%zu) failed", n);
         return HSA_E_MEM;
     }
     *cap = n;
+    hsa_log_alloc("buffer", n, t0);
     return 0;
 }
 
@@ -91,6 +101,7 @@ int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap
     he = he > s.hit_entries ? he : s.hit_entries;
     hsa_scratch_free(s);
     s.link_bytes = link_bytes;
+    const auto t0 = std::chrono::steady_clock::now();
     if (hipMalloc(&s.pool, pe * sizeof(uint4)) != hipSuccess ||
         hipMalloc(&s.nxt, pe * link_bytes) != hipSuccess ||
         hipMalloc(&s.hbuf, he * 9 * sizeof(uint32_t)) != hipSuccess) {
@@ -100,6 +111,7 @@ int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap
         return HSA_E_MEM;
     }
     s.pool_entries = pe; s.hit_entries = he;
+    hsa_log_alloc("search scratch", pe * (sizeof(uint4) + link_bytes) + he * 9 * sizeof(uint32_t), t0);
     return 0;
 }
 

@@ -590,6 +590,10 @@ struct PfArgs {
     uint32_t *call_fl;
     unsigned long long *acount;             // anchor calls listed
     const unsigned long long *d_n;          // the reads' count on the device (hsa_splice_device), or null: n
+    uint64_t cwd;                           // the caller-width base is rows: cw starts cwd pairs after it
+    uint32_t prefix;                        // seeds read their widths from the W1 rows (HSA_MG_PREFIX)
+    const void *ktw;                        // the width trie (hsa_trie.h) for type-1 rows, depth ktd (0: none)
+    uint32_t ktd;
 };
 
 __device__ __forceinline__ uint32_t pf_n(const PfArgs &a) { return a.d_n ? (uint32_t)*a.d_n : a.n; }
@@ -616,17 +620,24 @@ __global__ void __launch_bounds__(BLOCK) k_pf_rows(PfArgs a)
         if (kind == 1 && L < 12u) return;
         const uint32_t p0 = kind == 1 ? L - 12u : 0u, n = kind == 1 ? 12u : L;
         uint8_t *const sc = a.scodes + (size_t)(2u * r + s) * a.sc;
+        uint32_t tl = 0, tix = 0;            // characters since the last reset and their trie node
         for (uint32_t i = 0; i < n; ++i) {
             const uint32_t c = pf_base(a, r, s, p0 + i);
             if (kind == 0) sc[i] = (uint8_t)c;
             if (c < 4) {
-                uint32_t ok, ol;
-                hsa_occ1_pair(a.rev, k, l + 1u, c, ok, ol);
-                const uint32_t cc = hsa_sel4(c, a.C[0], a.C[1], a.C[2], a.C[3]);
-                k = cc + ok + 1u;
-                l = cc + ol;
+                if (tl < a.ktd) {            // the same forward extension, from the width trie
+                    tix = tix * 4u + c;
+                    ++tl;
+                    trie_w_load<uint32_t>(a.ktw, trie_base(tl) + tix, k, l);
+                } else {
+                    uint32_t ok, ol;
+                    hsa_occ1_pair(a.rev, k, l + 1u, c, ok, ol);
+                    const uint32_t cc = hsa_sel4(c, a.C[0], a.C[1], a.C[2], a.C[3]);
+                    k = cc + ok + 1u;
+                    l = cc + ol;
+                }
             }
-            if (k > l || c > 3) { k = 0; l = a.T; ++bid; }
+            if (k > l || c > 3) { k = 0; l = a.T; ++bid; tl = 0; tix = 0; }
             o[2 * i] = (int32_t)(l - k + 1u);
             o[2 * i + 1] = (int32_t)bid;
         }
@@ -664,10 +675,18 @@ __global__ void __launch_bounds__(BLOCK) k_pf_seeds(PfArgs a)
     const uint32_t call = 8u * r + i;
     a.list[6u * r + i] = (int32_t)call;
     const int32_t *const w1 = a.rows + 2 * ((size_t)r * 6u + s) * a.rs;
-    int32_t *const cw = a.cw + 2 * (size_t)call * a.cws;
-    for (uint32_t p = 0; p < la; ++p) { cw[2 * p] = w1[2 * p]; cw[2 * p + 1] = w1[2 * p + 1]; }
-    cw[2 * la] = 0;
-    cw[2 * la + 1] = (la ? w1[2 * (la - 1u) + 1] : 0) + 1;
+    hsa_mg_job_t M;
+    if (a.prefix) {                         // the search reads the W1 row's prefix itself
+        M.wb_off = ((uint64_t)r * 6u + s) * a.rs;
+        M.ws_off = HSA_MG_PREFIX;
+    } else {                                // a copy, which the search's width_back export rewrites
+        int32_t *const cw = a.cw + 2 * (size_t)call * a.cws;
+        for (uint32_t p = 0; p < la; ++p) { cw[2 * p] = w1[2 * p]; cw[2 * p + 1] = w1[2 * p + 1]; }
+        cw[2 * la] = 0;
+        cw[2 * la + 1] = (la ? w1[2 * (la - 1u) + 1] : 0) + 1;
+        M.wb_off = a.cwd + (uint64_t)call * a.cws;
+        M.ws_off = 0;
+    }
     hsa_job_t J;
     J.off = (uint64_t)(2u * r + s) * a.sc + tt * sl;
     J.len = la;
@@ -675,9 +694,6 @@ __global__ void __launch_bounds__(BLOCK) k_pf_seeds(PfArgs a)
     J.seed_len = (int32_t)la;
     J.regime = 0;
     a.jobs[call] = J;
-    hsa_mg_job_t M;
-    M.wb_off = (uint64_t)call * a.cws;
-    M.ws_off = 0;
     M.strand = (int32_t)s;
     M.seed = HSA_SEED_ALIAS;
     a.mg[call] = M;
@@ -710,7 +726,7 @@ __global__ void __launch_bounds__(BLOCK) k_pf_anchors(PfArgs a)
     J.regime = 1;
     a.jobs[call] = J;
     hsa_mg_job_t M;
-    M.wb_off = (uint64_t)call * a.cws;
+    M.wb_off = a.cwd + (uint64_t)call * a.cws;
     M.ws_off = 0;
     M.strand = (int32_t)s;
     M.seed = HSA_SEED_NONE;
@@ -866,6 +882,14 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
     A.call_n = (int32_t *)(dq + q_n); A.call_fl = (uint32_t *)(dq + q_fl);
     A.acount = acnt;
     A.d_n = nullptr;
+    A.cwd = (q_cw - q_rows) / 8;
+    {
+        const char *te = getenv("HSA_TRIE");
+        const bool tr = ix->trie_depth > 0 && !ix->trie_wide && !(te && atoi(te) == 0);
+        A.ktw = tr ? ix->d_trie_w : nullptr;
+        A.ktd = tr ? ix->trie_depth : 0u;
+    }
+    A.prefix = ext_rg ? 1u : 0u;             // the host tables want every call's width_back after it
     HSA_HIP(hipMemsetAsync(d + o_sc, 4, 2 * N * sc + 64, st));         // padding reads as N
     hipLaunchKernelGGL(k_pf_rows, dim3((unsigned)((6 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
     hipLaunchKernelGGL(k_pf_seeds, dim3((unsigned)((6 * N + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, A);
@@ -878,7 +902,7 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
     const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
     const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
     const bool wide = need_wide(rg2, 2);
-    const MgPass mgp{A.mg, A.cw};
+    const MgPass mgp{A.mg, A.rows};          // widths at rows + wb_off (a row's prefix, or cw + call * cws)
     const unsigned long long n_seed = 6 * N;
     HSA_HIP(hipMemcpyAsync(scnt, &n_seed, 8, hipMemcpyHostToDevice, st));
     HSA_HIP(hipEventRecord(ix->ev0, st));
@@ -1083,6 +1107,14 @@ extern "C" int hsa_splice_device(hsa_index_t *ix, const hsa_regime_t *seed_rg, c
     A.call_n = (int32_t *)(d + o_n); A.call_fl = (uint32_t *)(d + o_fl);
     A.acount = acnt;
     A.d_n = rcnt;
+    A.cwd = (o_cw - o_rows) / 8;
+    {
+        const char *te = getenv("HSA_TRIE");
+        const bool tr = ix->trie_depth > 0 && !ix->trie_wide && !(te && atoi(te) == 0);
+        A.ktw = tr ? ix->d_trie_w : nullptr;
+        A.ktd = tr ? ix->trie_depth : 0u;
+    }
+    A.prefix = 1;
     const unsigned grid_n = (unsigned)((N + BLOCK - 1) / BLOCK);
     hipLaunchKernelGGL(k_sp_prep, dim3(grid_n), dim3(BLOCK), 0, st, b->d_jobs, b->d_flags, b->d_n_aln, (uint32_t)N,
                        (uint32_t *)(d + o_lens), (uint64_t *)(d + o_offs), (int32_t *)(d + o_amd), (int32_t *)(d + o_idx),
@@ -1099,7 +1131,7 @@ extern "C" int hsa_splice_device(hsa_index_t *ix, const hsa_regime_t *seed_rg, c
     const hsa_regime_t *d_reg = (const hsa_regime_t *)ix->d_in;
     const uint8_t *d_bmap = (const uint8_t *)ix->d_in + 256;
     const bool wide = need_wide(rg2, 2);
-    const MgPass mgp{A.mg, A.cw};
+    const MgPass mgp{A.mg, A.rows};          // widths at rows + wb_off (a row's prefix, or cw + call * cws)
     // no host round trip: the passes take their job counts from the device (the seed
     // calls' 6 per read, the anchors k_pf_anchors listed), planned for their upper bounds
     if ((rc = mg_passes(ix, d_reg, d_bmap, nb, A.jobs, A.list, scnt, (int)(6 * N), (int)(M / 3u + 2u), false, wide,

@@ -157,6 +157,10 @@ __global__ void __launch_bounds__(64) k_search_any(AnyArgs a)
             if (M) {
                 const int32_t *w = a.cw + 2 * M->wb_off;
                 for (int t = 0; t <= len; ++t) { ww[t] = (IT)(uint32_t)w[2 * t]; wbid[t] = w[2 * t + 1]; }
+                if (seed_kind == HSA_SEED_ALIAS && M->ws_off == HSA_MG_PREFIX) {   // a row's prefix: terminal
+                    ww[len] = 0;
+                    wbid[len] = (len ? wbid[len - 1] : 0) + 1;
+                }
                 if (seed_kind == HSA_SEED_OWN) {
                     const int32_t *v = a.cw + 2 * M->ws_off;
                     for (int t = 0; t <= slen; ++t) { sw[t] = (IT)(uint32_t)v[2 * t]; sbid[t] = v[2 * t + 1]; }
@@ -379,7 +383,7 @@ __global__ void __launch_bounds__(64) k_search_any(AnyArgs a)
             }
             if (err) { atomicAdd(&a.ctr[5], 1ull); fl = HSA_F_OVERFLOW; done = true; break; }
             if (ovf) { fl = HSA_F_OVERFLOW; done = true; break; }
-            if (M) {                                      // width_back back to the caller (Q6)
+            if (M && !(seed_kind == HSA_SEED_ALIAS && M->ws_off == HSA_MG_PREFIX)) {   // width_back back (Q6)
                 int32_t *w = a.cw + 2 * M->wb_off;
                 for (int t = 0; t <= len; ++t) { w[2 * t] = (int32_t)(uint32_t)ww[t]; w[2 * t + 1] = wbid[t]; }
             }

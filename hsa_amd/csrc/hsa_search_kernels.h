@@ -588,13 +588,16 @@ __global__ void __launch_bounds__(BLOCK) k_widths_import(SearchArgs a)
     uint32_t *const srow = reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(a.ws)) + rb * (a.rs / 4) * 64 + rl;
     uint32_t *const wrow = a.wg + rb * a.rg * 64 + rl;
     int32_t *const drow = a.wbid + rb * a.rg * 64 + rl;
-    // elements 0..n of one row; element t: min(bid, BIDM) | (w[t] == w[t+1]) | base code
+    // elements 0..n of one row; element t: min(bid, BIDM) | (w[t] == w[t+1]) | base code.
+    // A prefix row (HSA_MG_PREFIX: the first n entries of a longer bwt_cal_width row, the
+    // splice seeds' widths, bwtgap.c:807) has the terminal {0, bid of entry n - 1, + 1}.
+    const bool prefix = M.seed == HSA_SEED_ALIAS && M.ws_off == HSA_MG_PREFIX;
     auto emit = [&](uint32_t *row, const int32_t *w, uint32_t n, bool read_row) {
         uint32_t acc = 0;
         uint32_t wt = (uint32_t)w[0];
         for (uint32_t t = 0; t <= n; ++t) {
-            const uint32_t bid = (uint32_t)w[2 * t + 1];
-            const uint32_t wn = t < n ? (uint32_t)w[2 * t + 2] : 0u;
+            const uint32_t bid = prefix && t == n ? (n ? (uint32_t)w[2 * t - 1] + 1u : 1u) : (uint32_t)w[2 * t + 1];
+            const uint32_t wn = t + 1 < n || (t + 1 == n && !prefix) ? (uint32_t)w[2 * t + 2] : 0u;
             uint32_t e = bid < F::BIDM ? bid : F::BIDM;
             if (t < n && wt == wn) e |= F::EQ;
             if (read_row && t < n) e |= F::code_bits(a.codes[J.off + t]);
@@ -620,6 +623,7 @@ static __global__ void __launch_bounds__(BLOCK) k_widths_export(SearchArgs a)
     if (a.flags[job] & HSA_F_OVERFLOW) return;
     const hsa_job_t J = a.jobs[job];
     const hsa_mg_job_t M = a.mg[job];
+    if (M.seed == HSA_SEED_ALIAS && M.ws_off == HSA_MG_PREFIX) return;   // a row's prefix, read only
     const uint32_t R = q * 2u + (uint32_t)(M.strand & 1);
     const size_t base = (R >> 6) * (size_t)a.rg * 64 + (R & 63u);
     int32_t *const o = a.cw + 2 * M.wb_off;
