@@ -201,7 +201,7 @@ def host_oracle_index(res, T):
 # kernel-trace summaries next to them (tools/trace_summary.py) give the same runs'
 # per-launch durations
 TRAFFIC_SRCS = {2: "profiles/r05_pmc_summary_config2.json", 3: "profiles/r05_pmc_summary_config3.json",
-                4: "profiles/r03_pmc_summary_config4.json", 5: "profiles/r03_pmc_summary_config5.json"}
+                4: "profiles/r05_pmc_summary_config4.json", 5: "profiles/r05_pmc_summary_config5.json"}
 
 
 def traffic_per_kernel(config):

@@ -644,6 +644,58 @@ static void search_warm(const Idx2BWT *bi)
     }
 }
 
+/* The device splice path once at attach, on a batch the size of a host's batch of
+ * 150 bp reads (131 072 random reads; answers discarded): the prefetch pass's and the
+ * splice kernel's buffers and search scratch are allocated here instead of inside the
+ * first batch (their first allocation was 0.2 s of a 0.26 s first call).  Non-fatal:
+ * a failure is logged under HSA_VERBOSE and the first batch allocates as before. */
+static void splice_device_warm(const Idx2BWT *bi)
+{
+    const char *sde = getenv("HSA_SPLICE_DEVICE"), *w = getenv("HSA_SPLICE_WARM");
+    if ((sde && atoi(sde) == 0) || (w && atoi(w) == 0)) return;
+    int n_slots = 0;
+    hsa_index_t *const *slots = hsa_gpu_slots_of(bi, &n_slots);
+    if (n_slots < 1) return;
+    enum { N_WARM = 131072, L_WARM = 150 };
+    uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * N_WARM);
+    uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * N_WARM);
+    int32_t *amd = (int32_t *)malloc(sizeof(int32_t) * N_WARM);
+    uint8_t *codes = (uint8_t *)malloc((size_t)N_WARM * L_WARM);
+    uint32_t *res = (uint32_t *)malloc(sizeof(uint32_t) * HSA_SP_RES_WORDS * (size_t)N_WARM);
+    if (lens && offs && amd && codes && res) {
+        uint64_t x = 0x9E3779B97F4A7C15ull;
+        for (size_t j = 0; j < (size_t)N_WARM * L_WARM; ++j) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            codes[j] = (uint8_t)(x >> 62);
+        }
+        for (int k = 0; k < N_WARM; ++k) { lens[k] = L_WARM; offs[k] = (uint64_t)k * L_WARM; amd[k] = 4; }
+        gap_opt_t o;                                  /* gap_init_opt, -n 4 -o 1 */
+        memset(&o, 0, sizeof o);
+        o.s_mm = 3; o.s_gapo = 11; o.s_gape = 4; o.max_diff = 4; o.max_gapo = 1; o.max_gape = 6;
+        o.max_seed_diff = 2; o.seed_len = 32; o.max_entries = 2000000; o.max_top2 = 30; o.indel_end_skip = 5;
+        o.max_del_occ = 10; o.fnr = -1.0f;
+        const int n_stacks = hsa_aln_score(&o, o.max_diff + 1, o.max_gapo + 1, o.max_gape + 1);
+        gap_opt_t so = o, ao = o;                     /* as dsp_job_run builds them */
+        so.mode &= ~BWA_MODE_GAPE; so.max_gapo = 0; so.max_gape = 0; so.max_diff = o.max_seed_diff;
+        ao.max_gape = 3;
+        const hsa_regime_t srg = hsa_regime_of(&so, n_stacks, so.max_diff);
+        const hsa_regime_t arg_ = hsa_regime_of(&ao, n_stacks, 4);
+        hsa_regime_t erg = arg_;
+        erg.mode = ao.mode & (BWA_MODE_GAPE | BWA_MODE_LOGGAP | BWA_MODE_NONSTOP);
+        hsa_splice_pf_t pf;
+        hsa_splice_stats_t st;
+        const double t0 = hsa_now();
+        hsa_gpu_lock();
+        const int rc = hsa_splice_match_batch(slots[0], &srg, &arg_, &erg, N_WARM, lens, offs, codes,
+                                              (size_t)N_WARM * L_WARM, amd, &pf, res, &st);
+        hsa_gpu_unlock();
+        if (getenv("HSA_VERBOSE"))
+            fprintf(stderr, "[hsa] splice path warm-up: %d reads, %.3f s%s%s\n", N_WARM, hsa_now() - t0,
+                    rc ? ", failed: " : "", rc ? hsa_last_error() : "");
+    }
+    free(lens); free(offs); free(amd); free(codes); free(res);
+}
+
 /* Upload the bidirectional BWT of a loaded Idx2BWT once per slot in use (hook after
  * BWTLoad2BWT); slots added later by hsa_gpu_set_devices are attached on first use. */
 int hsa_gpu_attach(const Idx2BWT *bi)
@@ -693,6 +745,7 @@ int hsa_gpu_attach(const Idx2BWT *bi)
         if (hsa_splice_warm && hsa_splice_extend_active && hsa_splice_extend_active()) hsa_splice_warm(4096);
         if (hsa_splice_prefetch_warm && hsa_splice_prefetch_active && hsa_splice_prefetch_active())
             hsa_splice_prefetch_warm(bi);
+        splice_device_warm(bi);
     }
     return rc;
 }

@@ -68,18 +68,40 @@ static void hsa_log_alloc(const char *what, size_t bytes, std::chrono::steady_cl
     if (ms > 5.0 && getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] %s: hipMalloc of %.2f GB took %.1f ms\n", what, bytes / 1e9, ms);
 }
 
+// A new device buffer of `bytes` in *out, and the old one (*old, contents not kept)
+// freed: allocated BEFORE the old one is freed where HBM allows, since a large hipMalloc
+// right after the hipFree of a large block was measured at ~115 ms per GB (6.9 s for a
+// first batch's 59.6 GB search scratch), a fresh one at a few ms.  *old is null after.
+int hsa_realloc_device(void **out, void **old, size_t bytes)
+{
+    *out = nullptr;
+    if (hipMalloc(out, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = nullptr;
+        (void)hipFree(*old);                       // no room for both: the slow path
+        *old = nullptr;
+        if (hipMalloc(out, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            *out = nullptr;
+            hsa_set_error("hipMalloc(%zu) failed", bytes);
+            return HSA_E_MEM;
+        }
+        return 0;
+    }
+    (void)hipFree(*old);
+    *old = nullptr;
+    return 0;
+}
+
 int hsa_grow(void **p, size_t *cap, size_t need)
 {
     if (need <= *cap && *p) return 0;
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
     size_t n = need + need / 4 + 4096;
     const auto t0 = std::chrono::steady_clock::now();
-    if (hipMalloc(p, n) != hipSuccess) {
-        *p = nullptr; *cap = 0;
-        hsa_set_error("hipMalloc(%zu) failed", n);
-        return HSA_E_MEM;
-    }
+    void *np = nullptr;
+    *cap = 0;
+    if (hsa_realloc_device(&np, p, n)) return HSA_E_MEM;
+    *p = np;
     *cap = n;
     hsa_log_alloc("buffer", n, t0);
     return 0;
@@ -95,23 +117,39 @@ void hsa_scratch_free(SearchScratch &s)
 
 int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap, size_t link_bytes)
 {
-    size_t pe = lanes * pcap, he = lanes * hcap;
-    if (pe <= s.pool_entries && he <= s.hit_entries && s.pool && link_bytes == s.link_bytes) return 0;
-    pe = pe > s.pool_entries ? pe : s.pool_entries;
-    he = he > s.hit_entries ? he : s.hit_entries;
-    hsa_scratch_free(s);
-    s.link_bytes = link_bytes;
-    const auto t0 = std::chrono::steady_clock::now();
-    if (hipMalloc(&s.pool, pe * sizeof(uint4)) != hipSuccess ||
-        hipMalloc(&s.nxt, pe * link_bytes) != hipSuccess ||
-        hipMalloc(&s.hbuf, he * 9 * sizeof(uint32_t)) != hipSuccess) {
+    const size_t pe = lanes * pcap, he = lanes * hcap;
+    // The pool (+ links) and the staged hits grow separately: a wide pass that needs more
+    // hit slots must not free and re-allocate a deep pass's tens of GB of pool (measured:
+    // 6.9 s for a 59.6 GB hipMalloc right after the hipFree of the old one)
+    auto fail = [&]() {
         hsa_set_error("scratch allocation failed (lanes %zu, pool %zu, hits %zu)", lanes, pcap, hcap);
         (void)hipGetLastError();    // not sticky: a caller may free memory and go on
         hsa_scratch_free(s);
         return HSA_E_MEM;
+    };
+    if (!s.pool || pe > s.pool_entries || link_bytes != s.link_bytes) {
+        const size_t npe = pe > s.pool_entries ? pe : s.pool_entries;
+        const auto t0 = std::chrono::steady_clock::now();
+        void *np = nullptr, *nn = nullptr;
+        if (hsa_realloc_device(&np, (void **)&s.pool, npe * sizeof(uint4)) ||
+            hsa_realloc_device(&nn, &s.nxt, npe * link_bytes)) {
+            (void)hipFree(np);
+            return fail();
+        }
+        s.pool = (uint4 *)np; s.nxt = nn;
+        s.pool_entries = npe;
+        s.link_bytes = link_bytes;
+        hsa_log_alloc("search scratch pool", npe * (sizeof(uint4) + link_bytes), t0);
     }
-    s.pool_entries = pe; s.hit_entries = he;
-    hsa_log_alloc("search scratch", pe * (sizeof(uint4) + link_bytes) + he * 9 * sizeof(uint32_t), t0);
+    if (!s.hbuf || he > s.hit_entries) {
+        const size_t nhe = he > s.hit_entries ? he : s.hit_entries;
+        const auto t0 = std::chrono::steady_clock::now();
+        void *nh = nullptr;
+        if (hsa_realloc_device(&nh, (void **)&s.hbuf, nhe * 9 * sizeof(uint32_t))) return fail();
+        s.hbuf = (uint32_t *)nh;
+        s.hit_entries = nhe;
+        hsa_log_alloc("search scratch hits", nhe * 9 * sizeof(uint32_t), t0);
+    }
     return 0;
 }
 

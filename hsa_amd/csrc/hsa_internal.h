@@ -110,6 +110,7 @@ struct hsa_index {
 int hsa_need_unshared(const hsa_index *ix, const char *what);
 
 int hsa_grow(void **p, size_t *cap, size_t need);
+int hsa_realloc_device(void **out, void **old, size_t bytes);
 // hsa_mg_job_t.ws_off of an HSA_SEED_ALIAS job whose width_back is the first len entries
 // of a longer row (internal: the splice seeds, hsa_search.hip): terminal computed, no export
 #define HSA_MG_PREFIX 0xFFFFFFFFFFFFFFFFull

@@ -1389,12 +1389,58 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             if (cand) {
                 const uint32_t last = 31u - (uint32_t)__clz(cand);
                 n_entries += __popc(cand);
-                for (uint32_t rest = cand & ~(1u << last); rest; rest &= rest - 1u) {
-                    const E v = entry((uint32_t)__ffs(rest) - 1u);
+                uint32_t rest = cand & ~(1u << last);
+                if constexpr (HUGE) {
+                    for (; rest; rest &= rest - 1u) {
+                        const E v = entry((uint32_t)__ffs(rest) - 1u);
 #ifdef HSA_DIAG
-                    if (doomed(v.w)) DC(19);
+                        if (doomed(v.w)) DC(19);
 #endif
-                    flush(v, bucket_of(v.w));
+                        flush(v, bucket_of(v.w));
+                    }
+                } else if (rest) {
+                    // Every candidate but the last, in push order (gap_push, bwtgap.c:46-75),
+                    // with each group's meta word and bucket computed once: the insertion
+                    // and the deletions share one score, the mismatches another, the bit-8
+                    // match child has the parent's.  The groups' bucket heads are kept in
+                    // registers across the loop (equal buckets updated together, so the
+                    // links are flush()'s) and written back once: the divergent loop does
+                    // two stores per candidate and no LDS round trip.
+                    const uint32_t g_go = (uint32_t)ego + (est == ST_M), g_ge = (uint32_t)ege + (est != ST_M);
+                    const uint32_t mI = meta_pack((uint32_t)i, ST_I, 1u, (uint32_t)emm, g_go, g_ge);
+                    const uint32_t mD = meta_pack((uint32_t)(i + 1), ST_D, 1u, (uint32_t)emm, g_go, g_ge);
+                    const uint32_t mM = meta_pack((uint32_t)i, ST_M, 1u, (uint32_t)emm + 1u, (uint32_t)ego, (uint32_t)ege);
+                    const uint32_t mP = meta_pack((uint32_t)i, ST_M, 0u, (uint32_t)emm, (uint32_t)ego, (uint32_t)ege);
+                    const int bG = GAPS ? bucket_of(mI) : -1, bM = bucket_of(mM), bP = bucket_of(mP);
+                    auto head0 = [&](int b) -> uint32_t {
+                        return b >= 0 && (uint32_t)b < a.nb && mask.test(b) ? (uint32_t)HEAD(b) : NIL;
+                    };
+                    const uint32_t hG0 = GAPS ? head0(bG) : NIL, hM0 = head0(bM), hP0 = head0(bP);
+                    uint32_t hG = hG0, hM = hM0, hP = hP0;
+                    for (; rest; rest &= rest - 1u) {
+                        const uint32_t b = (uint32_t)__ffs(rest) - 1u;
+                        const bool ins = GAPS && b == 0, gap = GAPS && b <= 4u;
+                        const bool mt = b == 8u && sc < 4;               // the match child
+                        const uint32_t c = gap ? b - 1u : (sc + b - 4u) & 3u;
+                        IT k = pick4(oa, c), l = pick4(ob, c), rk = pick4(srk, c);
+                        if (ins) { k = ek; l = el; rk = erk; }
+                        const uint32_t meta = ins ? mI : gap ? mD : mt ? mP : mM;
+                        const int bk = gap ? bG : mt ? bP : bM;
+#ifdef HSA_DIAG
+                        if (doomed(meta)) DC(19);
+#endif
+                        if ((uint32_t)bk >= a.nb || pool_top >= a.pcap) { ctl |= 1u << 8; continue; }
+                        const uint32_t slot = pool_top++;
+                        DC(8);
+                        ent_store<IT>(a.pool, pbase, slot, E{k, l, rk, meta});
+                        NXT(slot) = (LT)(bk == bG ? hG : bk == bM ? hM : hP);
+                        hG = bk == bG ? slot : hG;
+                        hM = bk == bM ? slot : hM;
+                        hP = bk == bP ? slot : hP;
+                    }
+                    if (GAPS && hG != hG0) { HEAD(bG) = (LT)hG; mask.set(bG); }
+                    if (hM != hM0) { HEAD(bM) = (LT)hM; mask.set(bM); }
+                    if (hP != hP0) { HEAD(bP) = (LT)hP; mask.set(bP); }
                 }
                 const E v = entry(last);
 #ifdef HSA_DIAG
@@ -1637,7 +1683,9 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     // deeper main-pass pool keeps the long gapped searches inside the main pass, where
     // their tails overlap other lanes' work, instead of the serial overflow re-run:
     // config 4 (150 bp, -o 1) 2.36 -> 2.07 s per 1M reads at 32768 (49152: same)
-    P.pcap = big ? 65535u : (uint32_t)(g_pool_entries ? g_pool_entries : (gaps ? 32768 : 8192));
+    static const int pool_env = getenv("HSA_POOL_ENTRIES") ? atoi(getenv("HSA_POOL_ENTRIES")) : 0;   // A/B runs
+    const int pool_main = g_pool_entries ? g_pool_entries : pool_env > 0 && pool_env <= 65535 ? pool_env : 0;
+    P.pcap = big ? 65535u : (uint32_t)(pool_main ? pool_main : (gaps ? 32768 : 8192));
     P.hcap = big ? 16384u : (uint32_t)g_hit_cap;
     if (P.huge) {
         // live entries never exceed max_entries + 9 (bwtgap.c:150-151); the pool is

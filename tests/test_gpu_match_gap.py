@@ -117,7 +117,10 @@ MAN = json.load(open(os.path.join(GOLD, "manifest_dropin.json")))
                                         ("default", "reads"), ("n4o0", "reads")])
 def test_dropin_both_entry_points_sam_identical(name, reads):
     fq = os.path.join(GOLD, MAN[reads])
-    env = dict(os.environ, HSA_VERBOSE="1")
+    # the host's bwt_splice_match (HSA_SPLICE_DEVICE=0), so that its bwt_match_gap calls
+    # reach our entry point; the device's splice path has its own tests (test_gpu_dropin.py,
+    # test_gpu_splice_device.py)
+    env = dict(os.environ, HSA_VERBOSE="1", HSA_SPLICE_DEVICE="0")
     r = subprocess.run([HSA_GPU_MG, "aln", *MAN[name]["args"], INDEX["tiny"], fq], capture_output=True, timeout=300,
                        env=env)
     assert r.returncode == 0, r.stderr.decode()[-2000:]

@@ -98,7 +98,7 @@ def main():
     else:
         # one step = k_widths + k_search launches: per-kernel medians, summed
         out["per_kernel"] = {}
-    for k in (() if launches else ("k_widths", "k_search")):
+    for k in (() if launches else ("k_widths", "k_widths_reads", "k_search")):
         f, dur = counters(os.path.join(src, "pmc_fetch"), k)
         w, _ = counters(os.path.join(src, "pmc_write"), k)
         if not f:
