@@ -644,15 +644,17 @@ static void search_warm(const Idx2BWT *bi)
     }
 }
 
-/* The device splice path once at attach, on a batch the size of a host's batch of
- * 150 bp reads (131 072 random reads; answers discarded): the prefetch pass's and the
- * splice kernel's buffers and search scratch are allocated here instead of inside the
- * first batch (their first allocation was 0.2 s of a 0.26 s first call).  Non-fatal:
- * a failure is logged under HSA_VERBOSE and the first batch allocates as before. */
+/* HSA_SPLICE_WARM=1: the device splice path once at attach, on a batch the size of a
+ * host's batch of 150 bp reads (131 072 random reads; answers discarded), so that the
+ * prefetch pass's and the splice kernel's buffers exist before the first batch (their
+ * first allocation is ~0.2 s of the first call).  Opt-in: the buffers it sizes for a
+ * full-chip pass stay allocated, which raised the footprint enough to slow a second
+ * process sharing the GPU (the bench's end-to-end leg beside the bench itself) from
+ * 0.26 s to 11 s per call.  Non-fatal: a failure is logged under HSA_VERBOSE. */
 static void splice_device_warm(const Idx2BWT *bi)
 {
     const char *sde = getenv("HSA_SPLICE_DEVICE"), *w = getenv("HSA_SPLICE_WARM");
-    if ((sde && atoi(sde) == 0) || (w && atoi(w) == 0)) return;
+    if ((sde && atoi(sde) == 0) || !w || atoi(w) == 0) return;
     int n_slots = 0;
     hsa_index_t *const *slots = hsa_gpu_slots_of(bi, &n_slots);
     if (n_slots < 1) return;
