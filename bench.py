@@ -513,12 +513,17 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
                                                      "stderr_tail": tail}}
         t_gpu = float(j.stdout.decode().split()[-1])
         splice_s, n_fb, search_s, prefetch_s = 0.0, 0, 0.0, 0.0
+        calls = []                                         # per call: search + splice prefetch + path
         for ln in err.splitlines():
             if ln.startswith("[hsa] batch of"):
                 parts = ln.replace(",", "").split()
-                splice_s += float(parts[parts.index("path") + 1])
-                search_s += float(parts[parts.index("search") + 1])
-                prefetch_s += float(parts[parts.index("prefetch") + 1])
+                c_path = float(parts[parts.index("path") + 1])
+                c_search = float(parts[parts.index("search") + 1])
+                c_pf = float(parts[parts.index("prefetch") + 1])
+                splice_s += c_path
+                search_s += c_search
+                prefetch_s += c_pf
+                calls.append(c_path + c_search + c_pf)
                 n_fb += int(ln.split("(")[-1].split()[0])
         # parity through the real entry point: rank 0's reads are a prefix of the first
         # 100 000-read batch in both runs, so their hits (splice path's included) agree
@@ -531,10 +536,12 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
                "seconds": round(t_gpu, 3), "splice_fallback_reads": n_fb, "splice_path_s": round(splice_s, 3),
                "main_search_s": round(search_s, 3), "splice_prefetch_s": round(prefetch_s, 3),
                "splice_path_us_per_fallback_read": round(1e6 * splice_s / n_fb, 1) if n_fb else None,
+               "first_call_s": round(calls[0], 3) if calls else None,
+               "median_later_call_s": round(float(np.median(calls[1:])), 3) if len(calls) > 1 else None,
                "what": "the reference's driver (ref_probe.c) linked with every drop-in entry point of ours "
                        "(oracle/_ref/ref_probe_gpu, as HSA_gpu_all): bwa_cal_sa_reg_gap on bwa_seq_t batches from "
-                       "host memory, the reference's bwt_splice_match for the fallback reads with our seed searches, "
-                       "extensions, widths and SA lookups inside; wall time of the calls",
+                       "host memory, bwt_splice_match of the fallback reads on the device (the prefetch pass and the "
+                       "splice kernel; the host's own for reads the kernel hands back); wall time of the calls",
                "parity_vs_reference": {"reads": m, "mismatching_reads": len(bad), "first_mismatch": bad[0] if bad else None,
                                        "fields": "n_aln and every bwt_aln1_t field of every hit, splice-path hits "
                                                  "included, hit order"}}
