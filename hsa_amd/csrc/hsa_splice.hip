@@ -41,7 +41,9 @@
 
 #define SP_NT 64                 // lanes per workgroup
 #define SP_NIL 0xFFFFu           // empty bucket / free list (16-bit slot numbers)
+#ifndef HSA_SP_BUDGET
 #define HSA_SP_BUDGET 16         // extension pops per lane per pass of the main loop
+#endif
 #define SP_POS_MAX 100           // bwt_aln_corelate_check: <= 10 hits x 10 positions (bwtgap.c:684-706)
 #define MODE_GAPE 0x01
 #define MODE_LOGGAP 0x04
@@ -616,6 +618,9 @@ __device__ __forceinline__ int sp_log2(uint32_t v)   // bwtgap.c:107-116
     return c;
 }
 
+#ifdef HSA_SP_DIAG
+__device__ unsigned long long g_spd[8];
+#endif
 __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
 {
     extern __shared__ uint32_t s_hn[];                 // per bucket: head | count << 16, lane-interleaved
@@ -858,6 +863,11 @@ __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
         if (x_err) ext_end();
     };
 
+#ifdef HSA_SP_DIAG
+    // diagnostic builds: wave time in the control and extension phases, lanes active in each
+    uint64_t dg_ctrl = 0, dg_ext = 0, dg_all = __builtin_amdgcn_s_memtime();
+    uint64_t dg_lctrl = 0, dg_lext = 0, dg_nctrl = 0, dg_next = 0;
+#endif
     // ---- the lane's reads, one after another, from the batch's queue
     S.read = -1;
     S.n_ext = 0;
@@ -872,12 +882,21 @@ __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
             else { sp_init(a, S, (int)q); cur = (int)q; }
         }
         if (!__any(!done)) break;                       // every lane of the wave: queue empty, reads done
+#ifdef HSA_SP_DIAG
+        const uint64_t dg_t1 = __builtin_amdgcn_s_memtime();
+        const uint64_t dg_bc = __ballot(!done && !x_on && cur >= 0);
+#endif
         if (!done && !x_on && cur >= 0) {
             int c;
             do { c = sp_ctrl(a, S, lb); } while (c == SP_AGAIN);
             if (c == SP_EXT) ext_start();
             else cur = -1;
         }
+#ifdef HSA_SP_DIAG
+        const uint64_t dg_t2 = __builtin_amdgcn_s_memtime();
+        const uint64_t dg_be = __ballot(x_on);
+        if (dg_bc) { dg_ctrl += dg_t2 - dg_t1; dg_lctrl += (uint64_t)__popcll(dg_bc); ++dg_nctrl; }
+#endif
         if (x_on) {                                     // one place for every lane's extension
             for (int q = 0; q < HSA_SP_BUDGET && x_on; ++q) ext_pop();
             if (!x_on) {
@@ -891,7 +910,26 @@ __global__ void __launch_bounds__(SP_NT, 4) k_splice(SpArgs a)
                 }
             }
         }
+#ifdef HSA_SP_DIAG
+        if (dg_be) { dg_ext += __builtin_amdgcn_s_memtime() - dg_t2; dg_lext += (uint64_t)__popcll(dg_be); ++dg_next; }
+#endif
     }
+#ifdef HSA_SP_DIAG
+    if ((threadIdx.x & 63u) == 0) {
+        atomicAdd(&g_spd[0], dg_ctrl); atomicAdd(&g_spd[1], dg_ext);
+        atomicAdd(&g_spd[2], __builtin_amdgcn_s_memtime() - dg_all);
+        atomicAdd(&g_spd[3], dg_lctrl); atomicAdd(&g_spd[4], dg_nctrl);
+        atomicAdd(&g_spd[5], dg_lext); atomicAdd(&g_spd[6], dg_next);
+        __threadfence();
+        if (atomicAdd(&g_spd[7], 1ull) + 1ull == (unsigned long long)gridDim.x * (SP_NT / 64)) {
+            printf("[sp_diag] waves %llu: wave cycles control %llu ext %llu total %llu; control passes %llu (lanes %.1f per "
+                   "pass), extension passes %llu (lanes %.1f per pass)\n", g_spd[7], g_spd[0], g_spd[1], g_spd[2], g_spd[4],
+                   (double)g_spd[3] / (double)(g_spd[4] ? g_spd[4] : 1), g_spd[6],
+                   (double)g_spd[5] / (double)(g_spd[6] ? g_spd[6] : 1));
+            for (int i = 0; i < 8; ++i) g_spd[i] = 0;
+        }
+    }
+#endif
     n_sa = S.n_sa;
     atomicAdd(a.ctr + 0, n_ext);
     atomicAdd(a.ctr + 1, n_pops);
