@@ -1580,6 +1580,7 @@ struct LaunchPlan {
     bool huge;                       // PASS_HUGE: 32-bit links, reused slots
     uint32_t ntab;                   // score table entries per regime in LDS
     size_t resident;                 // lanes resident on the chip (every CU full)
+    size_t res_lanes = 0;            // lanes the scratch is reserved for (BIG: all its lanes)
 };
 
 // The capacity passes of one search: MAIN (every read), BIG (the reads that overflowed
@@ -1666,6 +1667,10 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
         static const size_t big_lanes = getenv("HSA_BIG_LANES") ? strtoull(getenv("HSA_BIG_LANES"), nullptr, 10) : 4096;
         const size_t big_blocks = big_lanes / NTB > 0 ? big_lanes / NTB : 1;
         blocks = need_blocks < big_blocks ? need_blocks : big_blocks;
+        // the BIG pass's scratch is reserved for all its lanes whatever the pass's size:
+        // the attach-time warm-up then allocates it (7.3 GB at the default shape) instead
+        // of a process's first full batch
+        P.res_lanes = big_blocks * NTB;
     } else if (need_blocks < blocks) {
         blocks = need_blocks;
     }
@@ -1821,9 +1826,10 @@ static int scratch_fit(hsa_index *ix, SearchScratch &S, LaunchPlan &P, size_t EW
 {
     const size_t lb = P.huge ? 4 : 2, floor_cap = 512;
     auto pe_of = [&](uint32_t pc) { return (size_t)((pc + 31u) & ~31u) * EW; };
-    auto bytes = [&](uint32_t pc) { return P.lanes * (pe_of(pc) * (16 + lb) + (size_t)P.hcap * EW * 36); };
-    const bool held = S.pool && lb == S.link_bytes && P.lanes * pe_of(P.pcap) <= S.pool_entries &&
-                      P.lanes * (size_t)P.hcap * EW <= S.hit_entries;
+    const size_t rl = P.res_lanes > P.lanes ? P.res_lanes : P.lanes;
+    auto bytes = [&](uint32_t pc) { return rl * (pe_of(pc) * (16 + lb) + (size_t)P.hcap * EW * 36); };
+    const bool held = S.pool && lb == S.link_bytes && rl * pe_of(P.pcap) <= S.pool_entries &&
+                      rl * (size_t)P.hcap * EW <= S.hit_entries;
     if (!held && !P.huge) {
         const char *cm = getenv("HSA_SCRATCH_MB");      // read per pass: tests set it mid-process
         const size_t cap_mb = cm ? strtoull(cm, nullptr, 10) : 0;
@@ -1839,7 +1845,7 @@ static int scratch_fit(hsa_index *ix, SearchScratch &S, LaunchPlan &P, size_t EW
                             "available)\n", want, P.pcap, bytes(P.pcap) / 1e9, P.lanes, avail / 1e9);
     }
     for (;;) {
-        const int rc = hsa_scratch_reserve(S, P.lanes, pe_of(P.pcap), (size_t)P.hcap * EW, lb);
+        const int rc = hsa_scratch_reserve(S, rl, pe_of(P.pcap), (size_t)P.hcap * EW, lb);
         if (rc != HSA_E_MEM || P.huge || P.pcap <= floor_cap) return rc;
         P.pcap = P.pcap / 2 > floor_cap ? P.pcap / 2 : floor_cap;
         if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] search scratch: allocation failed, pool -> %u per lane\n", P.pcap);
