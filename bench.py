@@ -457,6 +457,25 @@ def reference_files(d, T, res, extra):
     return prefix
 
 
+def parse_batch_stages(err):
+    """The drop-in's per-call stage lines (HSA_VERBOSE, bwtaln_gpu.c: "[hsa] batch of N reads:
+    search S s, splice prefetch P s, splice path H s (F fallback reads, ...") -> the sums of
+    the three stages, the fallback reads and each call's total."""
+    splice_s, search_s, prefetch_s, n_fb, calls = 0.0, 0.0, 0.0, 0, []
+    for ln in err.splitlines():
+        if ln.startswith("[hsa] batch of"):
+            parts = ln.replace(",", "").split()
+            c_path = float(parts[parts.index("path") + 1])
+            c_search = float(parts[parts.index("search") + 1])
+            c_pf = float(parts[parts.index("prefetch") + 1])
+            splice_s += c_path
+            search_s += c_search
+            prefetch_s += c_pf
+            calls.append(c_path + c_search + c_pf)
+            n_fb += int(ln.split("(")[-1].split()[0])
+    return splice_s, search_s, prefetch_s, n_fb, calls
+
+
 def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
     """The reference's own bwa_cal_sa_reg_gap on the box's cores, and the drop-in end to
     end (ref_probe_gpu), on the same index files; returns the bench fields."""
@@ -512,19 +531,7 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
             return {"reference": ref, "dropin_e2e": {"error": f"ref_probe_gpu exit {j.returncode}",
                                                      "stderr_tail": tail}}
         t_gpu = float(j.stdout.decode().split()[-1])
-        splice_s, n_fb, search_s, prefetch_s = 0.0, 0, 0.0, 0.0
-        calls = []                                         # per call: search + splice prefetch + path
-        for ln in err.splitlines():
-            if ln.startswith("[hsa] batch of"):
-                parts = ln.replace(",", "").split()
-                c_path = float(parts[parts.index("path") + 1])
-                c_search = float(parts[parts.index("search") + 1])
-                c_pf = float(parts[parts.index("prefetch") + 1])
-                splice_s += c_path
-                search_s += c_search
-                prefetch_s += c_pf
-                calls.append(c_path + c_search + c_pf)
-                n_fb += int(ln.split("(")[-1].split()[0])
+        splice_s, search_s, prefetch_s, n_fb, calls = parse_batch_stages(err)
         # parity through the real entry point: rank 0's reads are a prefix of the first
         # 100 000-read batch in both runs, so their hits (splice path's included) agree
         g_n, g_h = read_probe_out(os.path.join(d, "gpu_out.bin"))

@@ -120,3 +120,21 @@ def test_step_plan_never_overlaps_writers_of_one_read_set(S, nd, warmup):
             if plan[a][1] == plan[b][1]:
                 assert a in before[b], (a, b, plan[a], plan[b])
     assert [h for h, _, _ in plan[:S]] == list(range(S))
+
+
+def test_parse_batch_stages_sums_the_calls():
+    """bench.py's drop-in end-to-end leg: the per-call stage lines the drop-in prints under
+    HSA_VERBOSE (bwtaln_gpu.c) -> stage sums, fallback reads, per-call totals."""
+    err = "\n".join([
+        "[hsa] launch: 256 CUs x 9 workgroups of 64 lanes, LDS 17296 B, 1563 workgroups, 39 buckets",
+        "[hsa] batch of 100000 reads: search 0.177 s, splice prefetch 0.269 s, splice path 0.002 s (100000 fallback "
+        "reads, 100000 on the device; per-read outputs 0.4 ms beside the device pass, 269.0 ms waited for)",
+        "[hsa] splice kernel: 100000 reads, 54255 spliced, 0 to the host's path",
+        "[hsa] batch of 100000 reads: search 0.176 s, splice prefetch 0.061 s, splice path 0.004 s (2362 fallback "
+        "reads, 2362 on the device; per-read outputs 0.4 ms beside the device pass, 61.0 ms waited for)",
+    ])
+    splice_s, search_s, prefetch_s, n_fb, calls = bench.parse_batch_stages(err)
+    assert n_fb == 102362
+    assert abs(search_s - 0.353) < 1e-9 and abs(prefetch_s - 0.330) < 1e-9 and abs(splice_s - 0.006) < 1e-9
+    assert len(calls) == 2 and abs(calls[0] - 0.448) < 1e-9 and abs(calls[1] - 0.241) < 1e-9
+    assert bench.parse_batch_stages("no stage lines\n") == (0.0, 0.0, 0.0, 0, [])
