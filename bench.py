@@ -1154,6 +1154,13 @@ def main():
     if ref_legs:
         procs = ref_procs
         j0 = a.warmup % nd
+        if world == 1 and a.e2e_reads > 0:
+            # the drop-in end to end is a second process on this GPU: this one's search
+            # scratch (tens of GB for the gapped regimes) goes back first
+            for h in handles:
+                if getattr(h, "h", None):
+                    h.release_scratch()
+            torch.cuda.empty_cache()
         # -G: the reference starts in the steady state of a process's later batches, the
         # state of the timed batches (GAPE cleared in the caller's block)
         opt_args = ["-n", "4", "-o", str(max_gapo), "-G"]

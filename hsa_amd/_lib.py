@@ -22,6 +22,7 @@ HSA_RF_POLYAT = 0x20
 
 EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_device_count", "hsa_last_error", "hsa_index_create", "hsa_index_create_device", "hsa_index_free",
+    "hsa_index_release_scratch",
     "hsa_index_bytes", "hsa_index_device", "hsa_occ4_batch", "hsa_step_batch", "hsa_width_batch",
     "hsa_search_batch", "hsa_search_device", "hsa_configure", "hsa_free", "hsa_synth_genome_device",
     "hsa_build_bwt_device", "bwa_cal_sa_reg_gap", "hsa_gpu_attach", "hsa_gpu_detach", "hsa_gpu_set_devices",
@@ -203,6 +204,7 @@ def lib():
     L.hsa_index_create_device.argtypes = [C.c_int, C.c_uint32, C.c_uint32, u32, vp, C.c_uint32, C.c_uint32, u32, vp,
                                           C.POINTER(vp)]
     L.hsa_index_free.argtypes = [vp]
+    L.hsa_index_release_scratch.argtypes = [vp]
     L.hsa_index_bytes.restype = C.c_size_t
     L.hsa_index_bytes.argtypes = [vp]
     L.hsa_index_trie.argtypes = [vp, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -363,6 +365,12 @@ class GpuIndex:
             self._clones = weakref.WeakSet()
         self._clones.add(c)
         return c
+
+    def release_scratch(self):
+        """hsa_index_release_scratch: the handle's search and splice working buffers go back
+        (the next call allocates them again)."""
+        if getattr(self, "h", None):
+            check(lib().hsa_index_release_scratch(self.h))
 
     def close(self):
         for c in list(getattr(self, "_clones", ())):

@@ -115,6 +115,22 @@ void hsa_scratch_free(SearchScratch &s)
     s.link_bytes = lb;
 }
 
+extern "C" int hsa_index_release_scratch(hsa_index_t *ix)
+{
+    if (!ix) { hsa_set_error("hsa_index_release_scratch: null handle"); return HSA_E_ARG; }
+    (void)hipSetDevice(ix->device);
+    HSA_HIP(hipStreamSynchronize(ix->stream));
+    hsa_scratch_free(ix->main); hsa_scratch_free(ix->big); hsa_scratch_free(ix->huge);
+    void **bufs[] = {&ix->d_pf, &ix->d_pf2, &ix->d_sp, &ix->d_any, &ix->d_any_aux};
+    size_t *caps[] = {&ix->d_pf_cap, &ix->d_pf2_cap, &ix->d_sp_cap, &ix->d_any_cap, &ix->d_any_aux_cap};
+    for (int i = 0; i < 5; ++i) {
+        if (*bufs[i]) (void)hipFree(*bufs[i]);
+        *bufs[i] = nullptr;
+        *caps[i] = 0;
+    }
+    return 0;
+}
+
 int hsa_scratch_reserve(SearchScratch &s, size_t lanes, size_t pcap, size_t hcap, size_t link_bytes)
 {
     const size_t pe = lanes * pcap, he = lanes * hcap;

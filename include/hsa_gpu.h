@@ -85,6 +85,11 @@ int  hsa_index_create_device(int device, uint32_t T, uint32_t isa0, const uint32
                              uint32_t rT, uint32_t risa0, const uint32_t rC[5], const uint32_t *d_rcode_lsb,
                              hsa_index_t **out);
 void hsa_index_free(hsa_index_t *ix);
+/* Give back the handle's grown working buffers (search scratch of every capacity pass,
+ * the splice prefetch's and splice kernel's buffers) after its stream's work is done;
+ * the next call allocates them again.  For a process that hands the GPU's memory to
+ * another one between batches (no reference counterpart: the reference has no device). */
+int hsa_index_release_scratch(hsa_index_t *ix);
 /* The HIP stream (hipStream_t) the library launches on for this index. */
 void *hsa_index_stream(const hsa_index_t *ix);
 size_t hsa_index_bytes(const hsa_index_t *ix);
