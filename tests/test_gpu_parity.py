@@ -102,6 +102,19 @@ def test_search_matches_reference(name):
     _compare(name)
 
 
+@pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "rep_gap60_default"])
+def test_search_after_scratch_release(name):
+    """hsa_index_release_scratch gives the handle's working buffers back between calls;
+    the next search allocates them again and its results are the reference's."""
+    ix = gpu_index(load_case(name)["index"])
+    _compare(name)
+    ix.release_scratch()
+    _compare(name)
+    ix.release_scratch()
+    ix.release_scratch()                      # twice in a row: nothing left to free
+    _compare(name)
+
+
 @pytest.mark.parametrize("name", ["tiny_gap100_n4o1", "tiny_edge_default", "rep_gap60_default", "tiny_gap100_n4o1_b400"])
 def test_search_matches_reference_one_lane_per_read(name, monkeypatch):
     """Batches smaller than the chip run strand-split (each read's rc and fwd searches on
