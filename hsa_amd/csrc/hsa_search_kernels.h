@@ -1691,9 +1691,11 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     static const int pool_env = getenv("HSA_POOL_ENTRIES") ? atoi(getenv("HSA_POOL_ENTRIES")) : 0;   // A/B runs
     const int pool_main = g_pool_entries ? g_pool_entries : pool_env > 0 && pool_env <= 65535 ? pool_env : 0;
     P.pcap = big ? 65535u : (uint32_t)(pool_main ? pool_main : (gaps ? 32768 : 8192));
-    // A/B runs: the main-pass pool of searches of at most 32 bases (the splice path's
-    // 12-mer anchors, which run on every resident lane: 155 GB of scratch at 32 768)
-    static const int pool_short = getenv("HSA_POOL_SHORT") ? atoi(getenv("HSA_POOL_SHORT")) : 0;
+    // searches of at most 32 bases (the splice path's 12-mer anchors, which run on every
+    // resident lane) keep 8 192 entries with gap opens too: 155 -> 39 GB of scratch per
+    // handle at config 4, the anchors' time unchanged (profiles/r05_pool_short_ab.log);
+    // HSA_POOL_SHORT=n sets it (0: the regime's default)
+    static const int pool_short = getenv("HSA_POOL_SHORT") ? atoi(getenv("HSA_POOL_SHORT")) : 8192;
     if (!big && !pool_main && max_len <= 32 && pool_short > 0 && pool_short <= 65535) P.pcap = (uint32_t)pool_short;
     P.hcap = big ? 16384u : (uint32_t)g_hit_cap;
     if (P.huge) {
