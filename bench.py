@@ -605,7 +605,9 @@ def main():
                     help="with N > 1 ranks: reads of each rank's timed batch checked against the restatement")
     a = ap.parse_args()
     if a.streams <= 0:
-        a.streams = 3 if a.config == 2 else 2     # config 2: +1.8 % on three (profiles/r05_streams3_ab.log)
+        # three handles where three handles' scratch fits: config 2 +1.8 % (profiles/r05_streams3_ab.log),
+        # config 3 +0.8-1.6 % with its 16 384-entry pools (profiles/r05_pool16k_ab.log)
+        a.streams = 3 if a.config in (2, 3) else 2
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
 

@@ -1690,7 +1690,10 @@ static int plan_launch(hsa_index *ix, int n_jobs, int max_len, int max_seed, int
     // config 4 (150 bp, -o 1) 2.36 -> 2.07 s per 1M reads at 32768 (49152: same)
     static const int pool_env = getenv("HSA_POOL_ENTRIES") ? atoi(getenv("HSA_POOL_ENTRIES")) : 0;   // A/B runs
     const int pool_main = g_pool_entries ? g_pool_entries : pool_env > 0 && pool_env <= 65535 ? pool_env : 0;
-    P.pcap = big ? 65535u : (uint32_t)(pool_main ? pool_main : (gaps ? 32768 : 8192));
+    // gapped reads of up to 128 bases: 16 384 (config 3 at 32 768: 106 GB of scratch per
+    // handle; at 16 384 53 GB and k_search 284.9 -> 283.7 ms, profiles/r05_pool16k_ab.log);
+    // longer gapped reads keep 32 768 (config 4 at 8 192: 32 s against 1.2 s)
+    P.pcap = big ? 65535u : (uint32_t)(pool_main ? pool_main : (gaps ? (max_len <= 128 ? 16384 : 32768) : 8192));
     // searches of at most 32 bases (the splice path's 12-mer anchors, which run on every
     // resident lane) keep 8 192 entries with gap opens too: 155 -> 39 GB of scratch per
     // handle at config 4, the anchors' time unchanged (profiles/r05_pool_short_ab.log);
