@@ -589,8 +589,8 @@ def main():
     ap.add_argument("--streams", type=int, default=0,
                     help="handles on the index (hsa_index_clone) that consecutive steps alternate over, so step "
                          "s+1's kernels fill the last waves of step s's k_search; handles past the second whose "
-                         "search scratch does not fit are dropped (0: 3 for config 2, else 2; the gapped configs 3 "
-                         "and 4 take ~110 GB of scratch per handle)")
+                         "search scratch does not fit are dropped (0: 3 for configs 2 and 3, else 2; config 4 "
+                         "takes ~115 GB of scratch per handle)")
     ap.add_argument("--ref-sample", type=int, default=-1,
                     help="reads the REFERENCE's own CPU path (oracle/_ref/ref_probe) searches, over --ref-procs "
                          "processes (-1: 8 000 per process for config 2, 2 000 for config 3, 1 000 for config 4; 0: "
