@@ -40,6 +40,14 @@ def test_no_gpu_fails_loudly():
         _lib.GpuIndex(*index_io.read_index(INDEX["tiny"]))
 
 
+def test_release_scratch_rejects_a_null_handle():
+    """hsa_index_release_scratch checks its handle before any HIP call."""
+    from hsa_amd import _lib
+    L = _lib.lib()
+    assert L.hsa_index_release_scratch(None) == -2            # HSA_E_ARG (include/hsa_gpu.h)
+    assert b"null" in L.hsa_last_error()
+
+
 def test_struct_sizes_match_reference():
     probe = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
     if not os.path.exists(probe):
