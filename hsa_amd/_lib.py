@@ -30,7 +30,7 @@ EXPORTS = [  # every symbol include/hsa_gpu.h and include/hsa_bwtaln.h declare
     "hsa_index_set_sa", "hsa_sa_position_batch", "hsa_sa_position_device", "hsa_match_gap_batch",
     "bwt_match_gap", "bwt_match_gap_batch", "hsa_splice_seeds_device", "hsa_pass_times",
     "hsa_cal_sa_reg_gap_multi", "hsa_index_create_device64", "hsa_index_is64", "hsa_occ4_batch64",
-    "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos",
+    "hsa_search_device64", "hsa_build_bwt_device64", "bwa_cal_pac_pos", "generate_sam_se_core",
     "hsa_build_bwt_index_device", "hsa_extend_batch", "bwt_extend_foreward", "bwt_extend_backward",
     "hsa_width0_batch", "bwt_cal_width", "hsa_extend_sliced", "hsa_index_trie",
     "hsa_index_clone", "hsa_splice_prefetch_batch", "hsa_index_set_text", "hsa_splice_match_batch",

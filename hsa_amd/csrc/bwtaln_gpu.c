@@ -243,6 +243,7 @@ typedef struct {
     gap_opt_t local;
     int n_stacks;
     uint32_t *res;                   /* HSA_SP_RES_WORDS per read */
+    int lock;                        /* slot 0: its index is shared with direct calls (hsa_gpu_lock) */
     int rc;
     double secs;
     hsa_splice_stats_t st;
@@ -274,9 +275,9 @@ static void *dsp_job_run(void *arg)
     hsa_regime_t erg = arg_;
     erg.mode = ao.mode & (BWA_MODE_GAPE | BWA_MODE_LOGGAP | BWA_MODE_NONSTOP);   /* as the extension reads it */
     hsa_splice_pf_t pf;
-    hsa_gpu_lock();
+    if (j->lock) hsa_gpu_lock();
     j->rc = hsa_splice_match_batch(j->ix, &srg, &arg_, &erg, j->n, lens, offs, codes, tot, amd, &pf, j->res, &j->st);
-    hsa_gpu_unlock();
+    if (j->lock) hsa_gpu_unlock();
     free(lens); free(offs); free(amd); free(codes);
     j->secs = hsa_now() - t0;
     return NULL;
@@ -608,13 +609,20 @@ static int attach_slot(const Idx2BWT *bi, int slot, hsa_index_t *const *have, hs
     if (rc == 0 && f->saValue && bi->hsp)
         rc = hsa_index_set_sa(ix, f->saValue, f->saValueSizeInWord, f->saInterval,
                               (const uint32_t *)bi->hsp->blockList, bi->hsp->numOfBlock);
+    if (rc != 0 && ix) { hsa_index_free(ix); ix = NULL; }
     /* the splice kernel's motif scan and intron-end check read the packed reference as
      * the HSP holds it: (dnaLength + 15) / 16 + 1 words (DNALoadPacked,
-     * TextConverter.c:704-707) */
-    if (rc == 0 && bi->hsp && bi->hsp->packedDNA)
-        rc = hsa_index_set_text(ix, bi->hsp->packedDNA, ((uint64_t)bi->hsp->dnaLength + 15) / 16 + 1,
-                                bi->hsp->dnaLength);
-    if (rc != 0 && ix) { hsa_index_free(ix); ix = NULL; }
+     * TextConverter.c:704-707).  Only the splice kernel reads it: not uploaded with
+     * HSA_SPLICE_DEVICE=0, and a failed upload (e.g. no HBM left) leaves the index without
+     * it -- hsa_splice_device_launch then answers HSA_E_ARG and the host's path runs. */
+    const char *sde = getenv("HSA_SPLICE_DEVICE");
+    if (rc == 0 && ix && bi->hsp && bi->hsp->packedDNA && !(sde && atoi(sde) == 0)) {
+        const int trc = hsa_index_set_text(ix, bi->hsp->packedDNA, ((uint64_t)bi->hsp->dnaLength + 15) / 16 + 1,
+                                           bi->hsp->dnaLength);
+        if (trc && getenv("HSA_VERBOSE"))
+            fprintf(stderr, "[hsa] packed reference not uploaded (%s): the splice path runs on the host\n",
+                    hsa_last_error());
+    }
     *out = ix;
     return rc;
 }
@@ -851,6 +859,139 @@ void hsa_gpu_fatal(const char *what, long rc)
  * serialised here rather than sharing them. */
 static pthread_mutex_t g_batch_mu = PTHREAD_MUTEX_INITIALIZER;
 
+/* The splice kernel's guard: the kernel restates the reference's bwt_splice_match
+ * (bwtgap.c:748-1332) and the drop-in uses it in place of the host's function, which is
+ * right only while the host's function is the reference's (its splice-site record,
+ * bwt_array_insert / bwt_find_split_pos_by_record, returns at entry: bwt_array.c:34,
+ * :77).  So on the first batch with device answers the host's own function also runs
+ * for the first SP_GUARD answered reads; any difference turns the device path off for
+ * the rest of the process (logged once).  0 unchecked, 1 checked, -1 off.  Guarded by
+ * g_batch_mu. */
+#define SP_GUARD 64
+static int g_sp_guard = 0;
+
+/* a device answer (HSA_SP_RES_WORDS words: status, n_aln, res_aln[0..1]) as the host's
+ * bwt_splice_match would leave it: a calloc(2) result array (bwtgap.c:854) */
+static void put_device_answer(bwa_seq_t *p, const uint32_t *o)
+{
+    p->n_aln = (int)o[1];
+    if (o[1] == 0) { p->aln = NULL; return; }
+    p->aln = (bwt_aln1_t *)calloc(2, sizeof(bwt_aln1_t));
+    memcpy(p->aln, o + 2, 2 * sizeof(bwt_aln1_t));
+}
+
+/* What the host's splice path of one batch needs. */
+typedef struct {
+    const Idx2BWT *bi;
+    struct bwt_array_t *arr;
+    bwa_seq_t *seqs;
+    const uint64_t *offs;
+    size_t tot;
+    int max_len;
+    const gap_opt_t *local;
+    const int32_t *sp;
+    int n_stacks;
+    int have_splice;
+    int pf_ok;
+} host_ctx_t;
+
+/* The host's bwt_splice_match for reads hr[0..n) (ascending; read q of them is number q
+ * of the batch's prefetch table when `prefetched`): all of them at once as coroutines
+ * whose seed extensions run batched on the GPU, when the host calls our bwt_extend_*
+ * (bwtext_gpu.c); else one read at a time, as the reference. */
+static void run_host_reads(const host_ctx_t *c, const int *hr, int n, int prefetched)
+{
+    const int batched = c->have_splice && hsa_splice_run && hsa_splice_extend_active && hsa_splice_extend_active();
+    hsa_splice_read_t *sr = NULL;
+    int *sr_idx = NULL, n_sr = 0;
+    bwt_aux_t aux;
+    memset(&aux, 0, sizeof aux);
+    if (batched) {
+        sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)n + 1));
+        sr_idx = (int *)malloc(sizeof(int) * ((size_t)n + 1));
+    }
+    for (int q = 0; q < n; ++q) {
+        const int i = hr[q];
+        bwa_seq_t *p = c->seqs + i;
+        gap_opt_t lo = *c->local;                               /* aux->opt = &local_opt (:363) */
+        lo.max_diff = c->sp[2 * i];
+        lo.seed_len = c->sp[2 * i + 1];
+        if (batched) {
+            sr[n_sr].seq = p->seq; sr[n_sr].len = (int)p->len; sr[n_sr].opt = lo;
+            sr_idx[n_sr++] = i;
+            continue;
+        }
+        if (!aux.stack) {
+            aux.bi_bwt = (Idx2BWT *)c->bi;
+            aux.arr = c->arr;
+            aux.max_len = c->max_len;
+            aux.width_back = (bwt_width_t *)calloc(c->max_len + 1, sizeof(bwt_width_t));
+            aux.width_fore = (bwt_width_t *)calloc(c->max_len + 1, sizeof(bwt_width_t));
+            aux.width_seed = (bwt_width_t *)calloc(c->max_len + 1, sizeof(bwt_width_t));
+            aux.rc_seq = (ubyte_t *)calloc(c->max_len + 1, 1);
+            aux.stack = ref_stack_new(c->n_stacks);
+        }
+        aux.opt = &lo;
+        aux.seq = p->seq;
+        aux.len = (int)p->len;
+        aux.strand = 0;
+        memset(aux.rc_seq, 0, (size_t)c->max_len);
+        for (int j = 0; j < (int)p->len; ++j) {
+            ubyte_t ch = p->seq[p->len - 1 - j];
+            aux.rc_seq[j] = ch < 4 ? (ubyte_t)(3 - ch) : ch;
+        }
+        int na = 0;
+        if (hsa_splice_set_read) hsa_splice_set_read(prefetched ? q : -1);
+        p->aln = bwt_splice_match(&aux, &na);
+        if (hsa_splice_set_read) hsa_splice_set_read(-1);
+        p->n_aln = na;
+        if (na == 0) { free(p->aln); p->aln = NULL; }
+    }
+    if (n_sr > 0) {
+        bwt_aln1_t **so = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)n_sr);
+        int *sn = (int *)malloc(sizeof(int) * (size_t)n_sr);
+        const long launches = hsa_splice_run(c->bi, c->arr, c->max_len, c->n_stacks, n_sr, sr, so, sn);
+        for (int k = 0; k < n_sr; ++k) {
+            bwa_seq_t *p = c->seqs + sr_idx[k];
+            p->aln = so[k];
+            p->n_aln = sn[k];
+            if (sn[k] == 0) { free(p->aln); p->aln = NULL; }
+        }
+        if (getenv("HSA_VERBOSE"))
+            fprintf(stderr, "[hsa] splice path: %d reads as coroutines, seed extensions in %ld GPU launches\n", n_sr,
+                    launches);
+        free(so); free(sn);
+    }
+    free(sr); free(sr_idx);
+    if (aux.stack) {
+        free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);
+        ref_stack_free(aux.stack);
+    }
+    if (prefetched) {
+        if (getenv("HSA_VERBOSE") && hsa_splice_memo_stats) {
+            uint64_t mh = 0, mm = 0, wh = 0, wm = 0, sh = 0, sm = 0;
+            hsa_splice_memo_stats(&mh, &mm);
+            if (hsa_splice_table_stats) hsa_splice_table_stats(&wh, &wm, &sh, &sm);
+            fprintf(stderr, "[hsa] splice prefetch: %llu bwt_match_gap calls answered from the batch, %llu run alone; "
+                            "%llu bwt_cal_width calls from the batch, %llu alone; %llu SA lookups from the batch, %llu "
+                            "not\n", (unsigned long long)mh, (unsigned long long)mm, (unsigned long long)wh,
+                    (unsigned long long)wm, (unsigned long long)sh, (unsigned long long)sm);
+        }
+        hsa_splice_memo_clear();
+    }
+    /* the runner's rounds add their lookups to the SA table: clear it after every batch
+     * that ran the coroutine runner, so it never outgrows a batch */
+    if (n_sr > 0 && hsa_splice_sa_clear) {
+        if (getenv("HSA_VERBOSE") && hsa_splice_sa_stats) {
+            uint64_t sh = 0, sm = 0;
+            hsa_splice_sa_stats(&sh, &sm);
+            fprintf(stderr, "[hsa] splice SA -> position: %llu lookups answered from the batch, %llu in the runner's "
+                            "rounds\n", (unsigned long long)sh, (unsigned long long)sm);
+        }
+        hsa_splice_sa_clear();
+    }
+}
+
 static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, const gap_opt_t *copt,
                                   struct bwt_array_t *arr);
 
@@ -892,10 +1033,7 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
     if (opt->fnr > 0.0) local.max_diff = cal_maxdiff(max_len, BWA_AVG_ERR, opt->fnr);
     if (local.max_diff < local.max_gapo) local.max_gapo = local.max_diff;
 
-    /* splice fallback state, built lazily (bwtaln.c:264-291) */
-    bwt_aux_t aux;
-    memset(&aux, 0, sizeof aux);
-    int have_splice = bwt_splice_match != NULL;
+    const int have_splice = bwt_splice_match != NULL;
     const int n_stacks = hsa_aln_score(&local, local.max_diff + 1, local.max_gapo + 1, local.max_gape + 1);
     /* the reads that go to bwt_splice_match (bwtaln.c:362-369), in order */
     int *fb = (int *)malloc(sizeof(int) * ((size_t)n_seqs + 1));
@@ -905,28 +1043,30 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
             fb[nf++] = i;
     const double t1 = hsa_now();
     /* bwt_splice_match of every fallback read on the device (hsa_splice_match_batch: the
-     * prefetch pass and the splice kernel, hsa_splice.hip), on a helper thread while this
-     * thread writes the per-read output arrays (so that they come from the host thread's
-     * own heap arena, where the host frees them).  HSA_SPLICE_DEVICE=0: the host's
-     * bwt_splice_match for all of them. */
+     * prefetch pass and the splice kernel, hsa_splice.hip), on helper threads -- the reads
+     * split into contiguous parts, one per device slot -- while this thread writes the
+     * per-read output arrays (so that they come from the host thread's own heap arena,
+     * where the host frees them).  HSA_SPLICE_DEVICE=0, or a host whose bwt_splice_match
+     * answers differently (the guard below): the host's bwt_splice_match for all of them. */
     const char *sde = getenv("HSA_SPLICE_DEVICE");
     const int want_dev = !sde || atoi(sde) != 0;
-    dsp_job_t dj;
-    memset(&dj, 0, sizeof dj);
-    int dev = want_dev && nf > 0 && n_stacks <= HSA_SP_MAX_STACKS;
+    int dev = want_dev && g_sp_guard >= 0 && nf > 0 && n_stacks <= HSA_SP_MAX_STACKS;
     for (int k = 0; dev && k < nf; ++k)
         if (seqs[fb[k]].len < 3 || seqs[fb[k]].len > 3 * 1021) dev = 0;   /* the prefetch's read lengths */
-    pthread_t dth;
-    int dev_async = 0;
-    if (dev) {
-        dj.ix = slots[0]; dj.n = nf; dj.fb = fb; dj.seqs = seqs; dj.sp = sp; dj.local = local; dj.n_stacks = n_stacks;
-        dj.res = (uint32_t *)malloc(sizeof(uint32_t) * HSA_SP_RES_WORDS * (size_t)nf);
-        dev_async = pthread_create(&dth, NULL, dsp_job_run, &dj) == 0;
-        if (!dev_async) dsp_job_run(&dj);
+    const int n_dj = dev ? (n_slots < nf ? n_slots : nf) : 0;
+    dsp_job_t dj[HSA_MAX_SLOTS];
+    pthread_t dth[HSA_MAX_SLOTS];
+    int dev_async[HSA_MAX_SLOTS] = {0};
+    uint32_t *dres = dev ? (uint32_t *)malloc(sizeof(uint32_t) * HSA_SP_RES_WORDS * (size_t)nf) : NULL;
+    for (int k = 0; k < n_dj; ++k) {
+        const int j0 = (int)((long)nf * k / n_dj), j1 = (int)((long)nf * (k + 1) / n_dj);
+        memset(&dj[k], 0, sizeof dj[k]);
+        dj[k].ix = slots[k]; dj[k].n = j1 - j0; dj[k].fb = fb + j0; dj[k].seqs = seqs; dj[k].sp = sp;
+        dj[k].local = local; dj[k].n_stacks = n_stacks; dj[k].res = dres + (size_t)HSA_SP_RES_WORDS * j0;
+        dj[k].lock = k == 0;
+        dev_async[k] = pthread_create(&dth[k], NULL, dsp_job_run, &dj[k]) == 0;
+        if (!dev_async[k]) dsp_job_run(&dj[k]);
     }
-    /* the reads the host's bwt_splice_match runs: all fallback reads, or those the device
-     * did not answer; hr[] in order, numbered in the prefetch table by their rank in hr */
-    int *hr = fb, nh_r = nf;
     /* the splice path's widths, seed and anchor searches and SA lookups of the host's reads
      * in one device pass (hsa_splice_prefetch, bwtgap_gpu.c), when the host's
      * bwt_splice_match calls our bwt_match_gap.  HSA_SPLICE_PREFETCH=0: no table, every
@@ -934,13 +1074,18 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
      * threads at once) */
     const char *pfe = getenv("HSA_SPLICE_PREFETCH");
     const int want_pf = !pfe || atoi(pfe) != 0;
-    const int pf_ok = want_pf && have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active();
+    const host_ctx_t hc = {bi_bwt, arr, seqs, offs, tot, max_len, &local, sp, n_stacks, have_splice,
+                           want_pf && have_splice && hsa_splice_prefetch_active && hsa_splice_prefetch_active()};
+    /* the reads the host's bwt_splice_match runs: all fallback reads, or those the device
+     * did not answer (+ the guard's); hr[] in order, numbered in the prefetch table by
+     * their rank in hr */
+    int *hr = fb, nh_r = nf;
     pf_job_t pj;
     memset(&pj, 0, sizeof pj);
     pthread_t pth;
     int pf_async = 0, prefetched = 0;
     double t_pf = 0.0;
-    if (!dev && pf_ok && nh_r > 0) {         /* beside the per-read outputs */
+    if (!dev && hc.pf_ok && nh_r > 0) {      /* beside the per-read outputs */
         pf_job_init(&pj, bi_bwt, arr, seqs, offs, tot, max_len, hr, nh_r, &local, sp, n_stacks);
         pf_async = pthread_create(&pth, NULL, pf_job_run, &pj) == 0;
         if (!pf_async) pf_job_run(&pj);
@@ -950,147 +1095,106 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
     write_outputs(seqs, n_seqs, n_aln, flags, hoff, hits);
     const double t_out = hsa_now() - to;
     if (pf_async) pthread_join(pth, NULL);
-    if (dev_async) pthread_join(dth, NULL);
+    for (int k = 0; k < n_dj; ++k) if (dev_async[k]) pthread_join(dth[k], NULL);
     const double t_join = hsa_now() - to - t_out;
-    int n_dev = 0;
+    int n_dev = 0, n_guard = 0, *gd = NULL;       /* gd: the guard's reads, their numbers in fb */
     if (dev) {
-        if (dj.rc == HSA_E_ARG) {                /* not on this index / these options: the host's path */
+        int rc = 0;
+        hsa_splice_stats_t st;
+        memset(&st, 0, sizeof st);
+        double dsecs = 0.0;
+        for (int k = 0; k < n_dj; ++k) {
+            if (dj[k].rc && !rc) rc = dj[k].rc;
+            st.extensions += dj[k].st.extensions; st.pops += dj[k].st.pops; st.sa_lookups += dj[k].st.sa_lookups;
+            st.kernel_ms += dj[k].st.kernel_ms;
+            if (dj[k].secs > dsecs) dsecs = dj[k].secs;
+        }
+        if (rc == HSA_E_ARG || rc == HSA_E_MEM) {
+            /* not on this index / these options, or no device memory for its buffers (another
+             * process may hold the HBM): the host's path, as with HSA_SPLICE_DEVICE=0 */
             if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] splice kernel not used: %s\n", hsa_last_error());
-            if (pf_ok && nh_r > 0) {
-                pf_job_init(&pj, bi_bwt, arr, seqs, offs, tot, max_len, hr, nh_r, &local, sp, n_stacks);
-                pf_job_run(&pj);
-                prefetched = 1;
-            }
-        } else if (dj.rc) {
-            hsa_gpu_fatal("GPU splice path", dj.rc);
+        } else if (rc) {
+            hsa_gpu_fatal("GPU splice path", rc);
         } else {
-            /* the device's answers; the reads it did not answer go to the host's path */
+            /* the device's answers; the reads it did not answer go to the host's path.  On the
+             * process's first batch with device answers, the host also runs its own
+             * bwt_splice_match for the first SP_GUARD answered reads (the guard) */
             hr = (int *)malloc(sizeof(int) * ((size_t)nf + 1));
+            gd = (int *)malloc(sizeof(int) * SP_GUARD);
             nh_r = 0;
             for (int k = 0; k < nf; ++k) {
-                const uint32_t *o = dj.res + (size_t)HSA_SP_RES_WORDS * k;
+                const uint32_t *o = dres + (size_t)HSA_SP_RES_WORDS * k;
                 if (o[0] != HSA_SP_OK) { hr[nh_r++] = fb[k]; continue; }
-                bwa_seq_t *p = seqs + fb[k];
-                p->n_aln = (int)o[1];
-                if (o[1] == 0) { p->aln = NULL; continue; }
-                p->aln = (bwt_aln1_t *)calloc(2, sizeof(bwt_aln1_t));     /* res_aln (bwtgap.c:854) */
-                memcpy(p->aln, o + 2, 2 * sizeof(bwt_aln1_t));
+                if (g_sp_guard == 0 && n_guard < SP_GUARD) { gd[n_guard++] = k; hr[nh_r++] = fb[k]; continue; }
+                put_device_answer(seqs + fb[k], o);
                 ++n_dev;
             }
             if (getenv("HSA_VERBOSE"))
-                fprintf(stderr, "[hsa] splice kernel: %d reads, %d spliced, %d to the host's path; %llu extensions, %llu "
-                                "pops, %llu SA lookups, %.1f ms of kernel (%.3f s with the prefetch pass)\n", nf, n_dev,
-                        nh_r, (unsigned long long)dj.st.extensions, (unsigned long long)dj.st.pops,
-                        (unsigned long long)dj.st.sa_lookups, dj.st.kernel_ms, dj.secs);
-            if (pf_ok && nh_r > 0) {             /* the host's reads' own prefetch */
-                pf_job_init(&pj, bi_bwt, arr, seqs, offs, tot, max_len, hr, nh_r, &local, sp, n_stacks);
-                pf_job_run(&pj);
-                prefetched = 1;
-            }
+                fprintf(stderr, "[hsa] splice kernel: %d reads on %d slot(s), %d answered, %d to the host's path "
+                                "(%d of them the guard's); %llu extensions, %llu pops, %llu SA lookups, %.1f ms of "
+                                "kernel (%.3f s with the prefetch pass)\n", nf, n_dj, nf - (nh_r - n_guard), nh_r,
+                        n_guard, (unsigned long long)st.extensions, (unsigned long long)st.pops,
+                        (unsigned long long)st.sa_lookups, st.kernel_ms, dsecs);
         }
-        t_pf = dj.secs;
-        free(dj.res);
+        t_pf = dsecs;
+    }
+    if (dev && hc.pf_ok && nh_r > 0) {          /* the host's reads' own prefetch (all of them when the
+                                                 * device path gave way) */
+        pf_job_init(&pj, bi_bwt, arr, seqs, offs, tot, max_len, hr, nh_r, &local, sp, n_stacks);
+        pf_job_run(&pj);
+        prefetched = 1;
     }
     if (prefetched) {
         t_pf += pj.secs;
         pf_job_free(&pj);
     }
-    /* the host's splice path for its reads: all of them at once as coroutines whose seed
-     * extensions run batched on the GPU, when the host calls our bwt_extend_*
-     * (bwtext_gpu.c); else one read at a time, as the reference */
-    const int batched = have_splice && hsa_splice_run && hsa_splice_extend_active && hsa_splice_extend_active();
-    hsa_splice_read_t *sr = NULL;
-    int *sr_idx = NULL, n_sr = 0;
-    if (batched) {
-        sr = (hsa_splice_read_t *)malloc(sizeof(hsa_splice_read_t) * ((size_t)nh_r + 1));
-        sr_idx = (int *)malloc(sizeof(int) * ((size_t)nh_r + 1));
-    }
-    for (int q = 0; q < nh_r; ++q) {                            /* q: the read's prefetch-table number */
-        const int i = hr[q];
-        bwa_seq_t *p = seqs + i;
-        gap_opt_t lo = local;                                   /* aux->opt = &local_opt (:363) */
-        lo.max_diff = sp[2 * i];
-        lo.seed_len = sp[2 * i + 1];
-        if (batched) {
-            sr[n_sr].seq = p->seq; sr[n_sr].len = (int)p->len; sr[n_sr].opt = lo;
-            sr_idx[n_sr++] = i;
-            continue;
-        }
-        if (!aux.stack) {
-            aux.bi_bwt = (Idx2BWT *)bi_bwt;
-            aux.arr = arr;
-            aux.max_len = max_len;
-            aux.width_back = (bwt_width_t *)calloc(max_len + 1, sizeof(bwt_width_t));
-            aux.width_fore = (bwt_width_t *)calloc(max_len + 1, sizeof(bwt_width_t));
-            aux.width_seed = (bwt_width_t *)calloc(max_len + 1, sizeof(bwt_width_t));
-            aux.rc_seq = (ubyte_t *)calloc(max_len + 1, 1);
-            aux.stack = ref_stack_new(n_stacks);
-        }
-        aux.opt = &lo;
-        aux.seq = p->seq;
-        aux.len = (int)p->len;
-        aux.strand = 0;
-        memset(aux.rc_seq, 0, (size_t)max_len);
-        for (int j = 0; j < (int)p->len; ++j) {
-            ubyte_t c = p->seq[p->len - 1 - j];
-            aux.rc_seq[j] = c < 4 ? (ubyte_t)(3 - c) : c;
-        }
-        int na = 0;
-        if (hsa_splice_set_read) hsa_splice_set_read(prefetched ? q : -1);
-        p->aln = bwt_splice_match(&aux, &na);
-        if (hsa_splice_set_read) hsa_splice_set_read(-1);
-        p->n_aln = na;
-        if (na == 0) { free(p->aln); p->aln = NULL; }
-    }
     const double t2 = hsa_now();
-    if (n_sr > 0) {
-        bwt_aln1_t **so = (bwt_aln1_t **)malloc(sizeof(bwt_aln1_t *) * (size_t)n_sr);
-        int *sn = (int *)malloc(sizeof(int) * (size_t)n_sr);
-        const long launches = hsa_splice_run(bi_bwt, arr, max_len, n_stacks, n_sr, sr, so, sn);
-        for (int k = 0; k < n_sr; ++k) {
-            bwa_seq_t *p = seqs + sr_idx[k];
-            p->aln = so[k];
-            p->n_aln = sn[k];
-            if (sn[k] == 0) { free(p->aln); p->aln = NULL; }
+    run_host_reads(&hc, hr, nh_r, prefetched);
+    if (n_guard > 0) {
+        /* the guard: the host's answers for these reads against the device's */
+        int bad = -1;
+        for (int g = 0; g < n_guard && bad < 0; ++g) {
+            const uint32_t *o = dres + (size_t)HSA_SP_RES_WORDS * gd[g];
+            const bwa_seq_t *p = seqs + fb[gd[g]];
+            if (p->n_aln != (int)o[1] || (o[1] > 0 && memcmp(p->aln, o + 2, sizeof(bwt_aln1_t) * o[1]) != 0)) bad = g;
         }
-        if (getenv("HSA_VERBOSE"))
-            fprintf(stderr, "[hsa] splice path: %d reads as coroutines, seed extensions in %ld GPU launches\n", n_sr,
-                    launches);
-        free(so); free(sn);
+        if (bad < 0) g_sp_guard = 1;
+        else {
+            g_sp_guard = -1;
+            fprintf(stderr, "[hsa] the host's bwt_splice_match answers read %d of this batch differently from the "
+                            "splice kernel (bwtgap.c:748): the host's function runs every fallback read from now on\n",
+                    fb[gd[bad]]);
+            /* this batch's device answers go too: the host runs those reads as well */
+            int n2 = 0;
+            int *h2 = (int *)malloc(sizeof(int) * ((size_t)nf + 1));
+            for (int k = 0, g = 0; k < nf; ++k) {
+                if (g < n_guard && gd[g] == k) { ++g; continue; }
+                if (dres[(size_t)HSA_SP_RES_WORDS * k] != HSA_SP_OK) continue;
+                bwa_seq_t *p = seqs + fb[k];
+                free(p->aln);
+                p->aln = NULL; p->n_aln = 0;
+                h2[n2++] = fb[k];
+            }
+            n_dev = 0;
+            int pf2 = 0;
+            if (hc.pf_ok && n2 > 0) {
+                pf_job_init(&pj, bi_bwt, arr, seqs, offs, tot, max_len, h2, n2, &local, sp, n_stacks);
+                pf_job_run(&pj);
+                t_pf += pj.secs;
+                pf_job_free(&pj);
+                pf2 = 1;
+            }
+            run_host_reads(&hc, h2, n2, pf2);
+            free(h2);
+        }
     }
-    free(sr); free(sr_idx);
     if (getenv("HSA_VERBOSE"))
         fprintf(stderr, "[hsa] batch of %d reads: search %.3f s, splice prefetch %.3f s, splice path %.3f s "
                         "(%d fallback reads, %d on the device; per-read outputs %.1f ms%s, %.1f ms waited for)\n",
-                n_seqs, t1 - t0, t_pf, hsa_now() - t2 + (t2 - t1 - t_pf), nf, dev ? nf - nh_r : 0, 1e3 * t_out,
+                n_seqs, t1 - t0, t_pf, hsa_now() - t2 + (t2 - t1 - t_pf), nf, n_dev, 1e3 * t_out,
                 (prefetched || dev) ? " beside the device pass" : "", 1e3 * t_join);
-    if (aux.stack) {
-        free(aux.width_back); free(aux.width_fore); free(aux.width_seed); free(aux.rc_seq);
-        ref_stack_free(aux.stack);
-    }
-    if (prefetched) {
-        if (getenv("HSA_VERBOSE") && hsa_splice_memo_stats) {
-            uint64_t mh = 0, mm = 0, wh = 0, wm = 0, sh = 0, sm = 0;
-            hsa_splice_memo_stats(&mh, &mm);
-            if (hsa_splice_table_stats) hsa_splice_table_stats(&wh, &wm, &sh, &sm);
-            fprintf(stderr, "[hsa] splice prefetch: %llu bwt_match_gap calls answered from the batch, %llu run alone; "
-                            "%llu bwt_cal_width calls from the batch, %llu alone; %llu SA lookups from the batch, %llu "
-                            "not\n", (unsigned long long)mh, (unsigned long long)mm, (unsigned long long)wh,
-                    (unsigned long long)wm, (unsigned long long)sh, (unsigned long long)sm);
-        }
-        hsa_splice_memo_clear();
-    }
-    /* the runner's rounds add their lookups to the SA table: clear it after every batch
-     * that ran the coroutine runner, so it never outgrows a batch */
-    if (n_sr > 0 && hsa_splice_sa_clear) {
-        if (getenv("HSA_VERBOSE") && hsa_splice_sa_stats) {
-            uint64_t sh = 0, sm = 0;
-            hsa_splice_sa_stats(&sh, &sm);
-            fprintf(stderr, "[hsa] splice SA -> position: %llu lookups answered from the batch, %llu in the runner's "
-                            "rounds\n", (unsigned long long)sh, (unsigned long long)sm);
-        }
-        hsa_splice_sa_clear();
-    }
+    free(dres);
+    free(gd);
     if (hr != fb) free(hr);
     free(fb);
     hsa_free(hits);

@@ -1018,15 +1018,23 @@ static int pf_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const hsa_regi
 
 // ---------------------------------------------------------------- hsa_splice_device
 // The fallback reads of a device batch (the main pass flagged them), compacted: their
-// order does not matter, a read's splice path depends on the read alone.
+// order does not matter, a read's splice path depends on the read alone.  A job whose
+// length is outside [3, max_len] (the prefetch's rows and codes are sized from max_len)
+// is not taken: its answer is HSA_SP_WIN (not answered), so a caller runs the host's
+// path for it.
 __global__ void __launch_bounds__(BLOCK) k_sp_prep(const hsa_job_t *jobs, const uint32_t *flags, const int32_t *n_aln,
-                                                   uint32_t n, uint32_t *lens, uint64_t *offs, int32_t *amd, int32_t *idx,
-                                                   unsigned long long *cnt)
+                                                   uint32_t n, uint32_t max_len, uint32_t *res, uint32_t *lens,
+                                                   uint64_t *offs, int32_t *amd, int32_t *idx, unsigned long long *cnt)
 {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n || !(flags[j] & HSA_F_FALLBACK) || n_aln[j] != 0) return;
-    const uint32_t r = (uint32_t)atomicAdd(cnt, 1ull);
     const hsa_job_t J = jobs[j];
+    if (J.len < 3u || J.len > max_len) {
+        res[(size_t)j * HSA_SP_RES_WORDS] = HSA_SP_WIN;
+        res[(size_t)j * HSA_SP_RES_WORDS + 1] = 0u;
+        return;
+    }
+    const uint32_t r = (uint32_t)atomicAdd(cnt, 1ull);
     lens[r] = J.len;
     offs[r] = J.off;
     amd[r] = J.max_diff;
@@ -1117,7 +1125,7 @@ extern "C" int hsa_splice_device(hsa_index_t *ix, const hsa_regime_t *seed_rg, c
     A.prefix = 1;
     const unsigned grid_n = (unsigned)((N + BLOCK - 1) / BLOCK);
     hipLaunchKernelGGL(k_sp_prep, dim3(grid_n), dim3(BLOCK), 0, st, b->d_jobs, b->d_flags, b->d_n_aln, (uint32_t)N,
-                       (uint32_t *)(d + o_lens), (uint64_t *)(d + o_offs), (int32_t *)(d + o_amd), (int32_t *)(d + o_idx),
+                       M, b->d_res, (uint32_t *)(d + o_lens), (uint64_t *)(d + o_offs), (int32_t *)(d + o_amd), (int32_t *)(d + o_idx),
                        rcnt);
     hipLaunchKernelGGL(k_sp_calls, dim3(1), dim3(1), 0, st, (const unsigned long long *)rcnt, scnt);
     HSA_HIP(hipMemsetAsync(d + o_sc, 4, 2 * N * sc + 64, st));         // padding reads as N

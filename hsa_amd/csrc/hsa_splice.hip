@@ -948,6 +948,8 @@ extern "C" int hsa_index_set_text(hsa_index_t *ix, const uint32_t *packed, uint6
     (void)hipFree(ix->d_text);
     ix->d_text = nullptr;
     if (hipMalloc(&ix->d_text, n_words * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        ix->d_text = nullptr;
         hsa_set_error("hsa_index_set_text: hipMalloc of %llu words failed", (unsigned long long)n_words);
         return HSA_E_MEM;
     }

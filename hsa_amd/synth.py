@@ -242,15 +242,18 @@ def make_spliced_reads(genome, records, n: int, L: int, seed: int, rc_frac: floa
     return reads, truth
 
 
-def write_fastq(path: str, reads: np.ndarray, prefix: str = "r") -> None:
+def write_fastq(path: str, reads: np.ndarray, prefix: str = "r", qual_seed: int | None = None) -> None:
+    """FASTQ of the reads; quality 'I' everywhere, or (qual_seed) a random Phred+33 string
+    in '#'..'J' per read (so that a reverse-strand SAM line's reversed quality shows)."""
     n, L = reads.shape
+    quals = None if qual_seed is None else np.random.default_rng(qual_seed).integers(35, 75, (n, L), dtype=np.uint8)
     qual = b"I" * L
     with open(path, "wb") as f:
         for i in range(n):
             f.write(b"@%s%d\n" % (prefix.encode(), i))
             f.write(ACGT[reads[i]].tobytes())
             f.write(b"\n+\n")
-            f.write(qual)
+            f.write(qual if quals is None else quals[i].tobytes())
             f.write(b"\n")
 
 

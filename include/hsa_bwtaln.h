@@ -12,6 +12,7 @@
  *   hsa_gpu_detach       new hook, before BWTFree2BWT (bwtaln.c:527)
  *   hsa_gpu_set_devices  new hook: device slots one call is split over (see below)
  *   bwa_cal_pac_pos      replaces bwtse.c:350 (SAM stage: SA -> position, batched)
+ *   generate_sam_se_core replaces bwtse.c:884 (the SAM stage on host threads)
  *
  * The structs below are declared here only so that the library reads and writes
  * the host's objects at the right offsets; their layouts are those of the
@@ -200,6 +201,17 @@ int  hsa_gpu_set_devices(int n);
  * same order.  Splicing reads keep the host's bwt_aln2pos_splicing (bwtse.c:295).
  * Needs the host's bwa_approx_mapQ, bwa_cal_maxdiff and bwt_aln2pos_splicing. */
 void bwa_cal_pac_pos(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, int max_mm, float fnr);
+
+/* generate_sam_se_core: replaces bwtse.c:884 (declared bwtse.h; called once per batch,
+ * bwtaln.c:514).  The SAM stage of one batch on host threads (HSA_SAM_THREADS, default
+ * the process's CPUs up to 16): the hit choice of bwt_aln2seq_core with each read's
+ * drand48 numbers found by jump-ahead (the process's drand48 state left where the
+ * reference leaves it), bwa_cal_pac_pos (whichever the program links: ours runs the
+ * lookups on the GPU), the host's bwa_refine_gapped on chunks of reads, and
+ * bwa_print_sam1's lines restated into per-chunk buffers written in read order: the
+ * reference's bytes.  The first batch checks the restated printing against the host's
+ * bwa_print_sam1 and falls back to it if they differ (hsa_amd/csrc/bwtsam_gpu.c). */
+void generate_sam_se_core(Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, gap_opt_t *opt, int n_occ);
 
 /* The host's splice fallback (bwtgap.c:748).  Weak: when the host program does
  * not provide it, reads without a hit are left with n_aln = 0. */

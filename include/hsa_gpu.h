@@ -88,7 +88,10 @@ void hsa_index_free(hsa_index_t *ix);
 /* Give back the handle's grown working buffers (search scratch of every capacity pass,
  * the splice prefetch's and splice kernel's buffers) after its stream's work is done;
  * the next call allocates them again.  For a process that hands the GPU's memory to
- * another one between batches (no reference counterpart: the reference has no device). */
+ * another one between batches (no reference counterpart: the reference has no device).
+ * No other call may be in flight on this handle (or use its buffers from another host
+ * thread) while it runs: it waits for the stream's queued work only, not for host threads
+ * that are about to queue more.  The drop-in entry points never call it. */
 int hsa_index_release_scratch(hsa_index_t *ix);
 /* The HIP stream (hipStream_t) the library launches on for this index. */
 void *hsa_index_stream(const hsa_index_t *ix);
@@ -381,7 +384,8 @@ typedef struct {
  * batch, written for those reads only; d_counters (>= 8 u64): [0] reads sent to the
  * splice path, [1] extensions, [2] extension pops, [3] SA lookups, [4] reads not answered,
  * [5] rank queries of the seed and anchor searches with their widths, [6] their hits.
- * Each read's max_diff is its job's; max_len the longest read (3 * 1021 at most). */
+ * Each read's max_diff is its job's; max_len the longest read (3 * 1021 at most): a
+ * fallback job shorter than 3 or longer than max_len is not taken and gets HSA_SP_WIN. */
 typedef struct {
     const hsa_job_t *d_jobs; int n_jobs;
     const uint8_t *d_codes;

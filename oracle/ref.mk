@@ -16,7 +16,7 @@ REFOBJS   = bwtaln bwtgap BWT BWTConstruct utils dictionary DNACount HSP inipars
 OBJS      = $(addprefix $(OUT)/obj/,$(addsuffix .o,$(REFOBJS)))
 
 all: $(OUT)/HSA $(OUT)/ref_probe $(OUT)/ref_mgcap $(OUT)/ref_extcap $(OUT)/HSA_gpu $(OUT)/HSA_gpu_mg $(OUT)/HSA_gpu_all \
-     $(OUT)/ref_probe_gpu
+     $(OUT)/ref_probe_gpu $(OUT)/HSA_sam
 
 $(OUT)/obj/%.o: $(REF)/%.c
 	@mkdir -p $(OUT)/obj
@@ -105,9 +105,10 @@ $(OUT)/HSA_gpu_mg: $(OUT)/obj/main.o $(MGOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPULIB)
 # reference to BWTRetrievePositionFromSAIndex renamed to hsa_splice_sa_position, so the
 # SAM stage keeps the host's own), and the SAM stage's bwa_cal_pac_pos, weakened in bwtse.o, so that
 # generate_sam_se_core (bwtse.c:911) calls OUR bwa_cal_pac_pos (hsa_amd/csrc/bwtse_gpu.c:
-# the batch's SA -> position lookups on the GPU).
+# the batch's SA -> position lookups on the GPU) -- and generate_sam_se_core itself, weakened
+# in bwtse.o too: hsa_amd/csrc/bwtsam_gpu.c runs the SAM stage on host threads.
 $(OUT)/obj/bwtse_weak.o: $(OUT)/obj/bwtse.o
-	objcopy --weaken-symbol=bwa_cal_pac_pos $< $@
+	objcopy --weaken-symbol=bwa_cal_pac_pos --weaken-symbol=generate_sam_se_core $< $@
 
 $(OUT)/obj/bwtaln_weak_all.o: $(OUT)/obj/bwtaln.o
 	objcopy --weaken-symbol=bwa_cal_sa_reg_gap --weaken-symbol=bwt_cal_width $< $@
@@ -119,7 +120,7 @@ $(OUT)/obj/bwtgap_weak_all.o: $(OUT)/obj/bwtgap.o
 
 ALLOBJS   = $(filter-out $(OUT)/obj/bwtaln.o $(OUT)/obj/bwtgap.o $(OUT)/obj/bwtse.o,$(OBJS)) \
             $(OUT)/obj/bwtaln_weak_all.o $(OUT)/obj/bwtgap_weak_all.o $(OUT)/obj/bwtse_weak.o
-GPUOBJ_SA = $(CURDIR)/../hsa_amd/csrc/bwtse_gpu.o
+GPUOBJ_SA = $(CURDIR)/../hsa_amd/csrc/bwtse_gpu.o $(CURDIR)/../hsa_amd/csrc/bwtsam_gpu.o
 GPUOBJ_EX = $(CURDIR)/../hsa_amd/csrc/bwtext_gpu.o
 
 $(OUT)/HSA_gpu_all: $(OUT)/obj/main.o $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) $(GPUOBJ_EX) $(GPULIB)
@@ -132,6 +133,23 @@ $(OUT)/HSA_gpu_all: $(OUT)/obj/main.o $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ
 $(OUT)/ref_probe_gpu: ref_probe.c $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) $(GPUOBJ_EX) $(GPULIB)
 	$(CC) $(REFFLAGS) -DHSA_GPU_PROBE -I$(REF) ref_probe.c $(ALLOBJS) $(GPUOBJ) $(GPUOBJ_MG) $(GPUOBJ_SA) \
 	    $(GPUOBJ_EX) -L$(dir $(GPULIB)) -lhsa_gpu -Wl,-rpath,'$$ORIGIN/../../hsa_amd' -lm -lz -lpthread -o $@
+
+# HSA_sam: the reference's HSA (CPU, its own search and SA -> position) with only the SAM
+# stage replaced: generate_sam_se_core weakened in bwtse.o, hsa_amd/csrc/bwtsam_gpu.c's on
+# host threads (no GPU).  tests/test_sam_cpu.py compares its SAM with the reference's.
+$(OUT)/obj/bwtse_weak_sam.o: $(OUT)/obj/bwtse.o
+	objcopy --weaken-symbol=generate_sam_se_core $< $@
+
+# ... and with bwa_print_sam1 weakened as well (the printing guard's test supplies a host
+# function that prints other bytes)
+$(OUT)/obj/bwtse_weak_sam_print.o: $(OUT)/obj/bwtse.o
+	objcopy --weaken-symbol=generate_sam_se_core --weaken-symbol=bwa_print_sam1 $< $@
+
+SAMOBJS   = $(filter-out $(OUT)/obj/bwtse.o,$(OBJS)) $(OUT)/obj/bwtse_weak_sam.o
+GPUOBJ_SAM = $(CURDIR)/../hsa_amd/csrc/bwtsam_gpu.o
+
+$(OUT)/HSA_sam: $(OUT)/obj/main.o $(SAMOBJS) $(GPUOBJ_SAM) $(OUT)/obj/bwtse_weak_sam_print.o
+	$(CC) $(REFFLAGS) $(OUT)/obj/main.o $(SAMOBJS) $(GPUOBJ_SAM) -lm -lz -lpthread -o $@
 
 clean:
 	rm -rf $(OUT)

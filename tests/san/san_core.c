@@ -361,5 +361,14 @@ int hsa_splice_match_batch(hsa_index_t *ix, const hsa_regime_t *seed_rg, const h
 {
     (void)ix; (void)seed_rg; (void)anchor_rg; (void)ext_rg; (void)n; (void)lens; (void)offs; (void)codes;
     (void)codes_len; (void)anchor_max_diff; (void)pf; (void)res; (void)stats;
+    /* SAN_SPLICE_FAKE=1: a "device" whose answers disagree with the host's bwt_splice_match
+     * (every read answered, with no hit): the drop-in's guard must notice on the first batch
+     * and run the host's function for every fallback read (tests/test_dropin_cpu.py) */
+    const char *fk = getenv("SAN_SPLICE_FAKE");
+    if (fk && atoi(fk) == 1) {
+        memset(res, 0, sizeof(uint32_t) * HSA_SP_RES_WORDS * (size_t)n);
+        if (stats) memset(stats, 0, sizeof *stats);
+        return 0;
+    }
     return HSA_E_ARG;
 }

@@ -104,3 +104,26 @@ def test_reference_hsa_with_dropin_host_c_prints_reference_sam(tmp_path_factory,
             w = [(int(a), int(b)) for a, b in
                  re.findall(r"(\d+) bwt_cal_width calls from the batch, (\d+) alone", err)]
             assert w and sum(a for a, _ in w) > 0 and sum(b for _, b in w) == 0, w
+
+
+@needs_ref
+@pytest.mark.parametrize("name", ["splice_default", "splice_n4o1"])
+def test_splice_guard_follows_the_host(tmp_path_factory, name):
+    """A device whose splice answers disagree with the host's bwt_splice_match (the
+    sanitized core's SAN_SPLICE_FAKE=1: every fallback read answered with no hit): on the
+    first batch the drop-in runs the host's function for its first 64 device-answered
+    reads too, sees the difference, and from then on takes the host's function for every
+    fallback read, this batch's included -- so the SAM is the reference's, and the log
+    says so once."""
+    hsa_bin = hsa_san(tmp_path_factory, "all")
+    idx = os.path.join(GOLD, "index", "tiny.fa")
+    fq = os.path.join(GOLD, MAN["splice_reads"])
+    env = dict(os.environ, HSA_VERBOSE="1", SAN_SPLICE_FAKE="1",
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=23", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([hsa_bin, "aln", *MAN[name]["args"], idx, fq], capture_output=True, timeout=600, env=env)
+    err = r.stderr.decode(errors="replace")
+    assert r.returncode == 0, err[-4000:]
+    assert "runtime error" not in err, err[-4000:]
+    assert err.count("answers read") == 1 and "differently from the splice kernel" in err, err[-3000:]
+    ref = gzip.open(os.path.join(GOLD, f"dropin_ref_{name}.sam.gz")).read()
+    assert r.stdout == ref

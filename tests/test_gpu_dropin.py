@@ -80,7 +80,9 @@ HSA_GPU_ALL = os.path.join(ROOT, "oracle", "_ref", "HSA_gpu_all")
                                              {"HSA_SPLICE_PREFETCH": "0", "HSA_SPLICE_THREADS": "4",
                                               "HSA_SPLICE_DEVICE": "0"}),
                                             ("splice_default", "splice_reads", {"HSA_SPLICE_DEVICE": "0"}),
-                                            ("splice_n4o1", "splice_reads", {"HSA_SPLICE_CAP": "6"})])
+                                            ("splice_n4o1", "splice_reads", {"HSA_SPLICE_CAP": "6"}),
+                                            ("default", "reads", {"HSA_SAM_THREADS": "8", "HSA_SAM_CHUNK": "7"}),
+                                            ("splice_n4o1", "splice_reads", {"HSA_SAM_THREADS": "1"})])
 def test_dropin_all_entry_points_sam_identical(name, reads, env):
     """Every drop-in entry point replaced at once (oracle/ref.mk HSA_gpu_all):
     bwa_cal_sa_reg_gap, bwt_match_gap, and the SAM stage's bwa_cal_pac_pos, whose SA ->
@@ -95,7 +97,10 @@ def test_dropin_all_entry_points_sam_identical(name, reads, env):
     so every seed and anchor search and every width of the splice path is a direct GPU
     call, made from four host threads at once (the calls serialise on slot 0's index).
     HSA_SPLICE_CAP=6: the splice kernel's per-lane stack holds 6 entries, so most reads
-    outgrow it and go to the host's path while the rest are answered on the device."""
+    outgrow it and go to the host's path while the rest are answered on the device.
+    The SAM stage is ours too (generate_sam_se_core, hsa_amd/csrc/bwtsam_gpu.c: drand48 by
+    jump-ahead, refine + print on host threads, spliced reads' positions on the GPU);
+    HSA_SAM_THREADS / HSA_SAM_CHUNK vary its threads and chunks."""
     idx = os.path.join(GOLD, "index", "tiny.fa")
     fq = os.path.join(GOLD, MAN[reads])
     r = subprocess.run([HSA_GPU_ALL, "aln", *MAN[name]["args"], idx, fq], capture_output=True, timeout=120,
