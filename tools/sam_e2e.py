@@ -44,6 +44,7 @@ def say(*a):
 
 def prepare(d):
     """(child process: the only one that touches the GPU) the index files under d/g.index.*"""
+    import hsa_amd  # noqa: F401  (libhsa_gpu.so before torch)
     import bench
     import torch
     t0 = time.time()
