@@ -1097,7 +1097,7 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
     if (pf_async) pthread_join(pth, NULL);
     for (int k = 0; k < n_dj; ++k) if (dev_async[k]) pthread_join(dth[k], NULL);
     const double t_join = hsa_now() - to - t_out;
-    int n_dev = 0, n_guard = 0, *gd = NULL;       /* gd: the guard's reads, their numbers in fb */
+    int n_dev = 0, n_spl = 0, n_guard = 0, *gd = NULL;       /* gd: the guard's reads, their numbers in fb */
     if (dev) {
         int rc = 0;
         hsa_splice_stats_t st;
@@ -1128,12 +1128,12 @@ static void cal_sa_reg_gap_locked(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *
                 if (g_sp_guard == 0 && n_guard < SP_GUARD) { gd[n_guard++] = k; hr[nh_r++] = fb[k]; continue; }
                 put_device_answer(seqs + fb[k], o);
                 ++n_dev;
+                n_spl += o[1] > 0;
             }
             if (getenv("HSA_VERBOSE"))
-                fprintf(stderr, "[hsa] splice kernel: %d reads on %d slot(s), %d answered, %d to the host's path "
-                                "(%d of them the guard's); %llu extensions, %llu pops, %llu SA lookups, %.1f ms of "
-                                "kernel (%.3f s with the prefetch pass)\n", nf, n_dj, nf - (nh_r - n_guard), nh_r,
-                        n_guard, (unsigned long long)st.extensions, (unsigned long long)st.pops,
+                fprintf(stderr, "[hsa] splice kernel: %d reads, %d spliced, %d to the host's path (%d of them the "
+                                "guard's), %d slot(s); %llu extensions, %llu pops, %llu SA lookups, %.1f ms of kernel "
+                                "(%.3f s with the prefetch pass)\n", nf, n_spl, nh_r, n_guard, n_dj, (unsigned long long)st.extensions, (unsigned long long)st.pops,
                         (unsigned long long)st.sa_lookups, st.kernel_ms, dsecs);
         }
         t_pf = dsecs;

@@ -47,6 +47,15 @@ def test_two_ranks_equal_sequential(name, short_reads):
     _two_ranks(name, short_reads, use_gpu=False)
 
 
+@pytest.mark.parametrize("name,short_reads", [("tiny_exact36_n0", False), ("tiny_exact36_n0", True),
+                                              ("tiny_gap100_n4o1_b400", False)])
+def test_three_ranks_ragged_equal_sequential(name, short_reads):
+    """World size 3: 7 batches of 300 reads (the last one 200) give the ranks 3, 2 and 2
+    batches; tiny_gap100 has 3 batches, one per rank, its first with the Q2 regime switch.
+    The fixed-total mode of bench.py (--total-reads) drives this same sharding."""
+    _two_ranks(name, short_reads, use_gpu=False, world=3)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,short_reads", PARAMS)
 def test_two_ranks_gpu_search_equal_sequential(name, short_reads):
