@@ -560,6 +560,170 @@ def reference_legs(T, res, extra, reads_all, opt_args, n_ref, procs, e2e_reads):
         shutil.rmtree(d, ignore_errors=True)
 
 
+class _BatchCodes:
+    """The global read stream's codes as hsa_amd.shard.search_sharded slices them
+    (codes[offs[b0]:offs[b1]]), holding only this rank's batches (fixed_total)."""
+
+    def __init__(self, batches: dict, per_batch_codes: int):
+        self.d, self.m = batches, per_batch_codes
+
+    def __getitem__(self, sl):
+        return self.d[sl.start // self.m].reshape(-1)
+
+
+def fixed_total(a):
+    """--total-reads R: BASELINE configs[2] as it is stated -- R reads in the reference's
+    100 000-read batches (bwtaln.c:477), the batches dealt round-robin to the ranks
+    (hsa_amd.shard.search_sharded: each batch searched with the option state the
+    sequential reference has when it reaches that batch, SURVEY Q2/Q3, plus the one
+    all-reduce), through the drop-in's bwa_cal_sa_reg_gap semantics on host arrays
+    (hsa_cal_sa_reg_gap_flat: H2D reads, search, D2H hits, per-read unpacking), then the
+    hit lists gathered to rank 0 (timed apart: `gather.ms`).  Total work is fixed, so
+    `scaling` is "strong"; `value` = R / the slowest rank's time.  Each rank checks a
+    sample of one steady-state batch (GAPE already cleared) against the restatement."""
+    import hsa_amd  # noqa: F401  (libhsa_gpu.so before torch)
+    import torch
+    import torch.distributed as dist
+    from hsa_amd import _lib, shard, synth
+    from hsa_amd._lib import GapOpt
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("HSA_BENCH_BACKEND", "nccl")
+    comm = torch.device("cpu")
+    if world > 1:
+        gpu = local % torch.cuda.device_count() if backend == "gloo" else local
+        torch.cuda.set_device(gpu)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            comm = torch.device("cuda", gpu)
+    device = torch.cuda.current_device()
+    T = a.genome or GENOME_T
+    R = a.total_reads
+    max_gapo = 0 if a.config == 2 else 1
+    t0 = time.time()
+    gi, res, _ = build_index(T, GENOME_SEED, device)
+    genome = synth.PackedGenome(T, GENOME_SEED)
+    recs = synth.record_layout(T, RECORDS)
+    bounds = shard.batch_bounds(R, REF_BATCH)
+    mine = shard.my_batches(len(bounds), world, rank)
+    seed0 = (6 if a.config == 3 else 5) * 10_000_000            # not the weak mode's read sets
+    reads = {}
+    for b in mine:
+        n = bounds[b][1] - bounds[b][0]
+        if a.config == 3:
+            reads[b], _ = synth.make_reads(genome, recs, n, READ_LEN, seed0 + b, indel=True, max_mm_indel=2)
+        else:
+            reads[b], _ = synth.make_reads(genome, recs, n, READ_LEN, seed0 + b, max_mm=4)
+    log(f"[bench] rank {rank}: index and {len(mine)} batches of {REF_BATCH} reads ready in {time.time() - t0:.1f} s")
+    opt = GapOpt.default()                      # the process's first batch: GAPE still set (SURVEY Q2)
+    opt.max_diff, opt.fnr, opt.max_gapo = 4, -1.0, max_gapo
+    opt0 = opt.as_dict()
+    lens = np.full(R, READ_LEN, np.uint32)
+    codes = _BatchCodes(reads, REF_BATCH * READ_LEN)
+    stats = []
+
+    def search(l, c, o):
+        n_aln, flags, hoff, hits, st = gi.cal_sa_reg_gap(l, c, o)
+        stats.append(st)
+        return n_aln, flags, hoff, hits
+
+    def allreduce_max(x):
+        t = torch.from_numpy(x.astype(np.int64)).to(comm)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.cpu().numpy().astype(np.int32)
+
+    # warm-up (untimed): one steady-state call, kernels loaded and scratch grown
+    wb = mine[0] if mine else 0
+    if mine:
+        gi.cal_sa_reg_gap(lens[:REF_BATCH], reads[wb].reshape(-1), GapOpt.from_dict(shard.opt_entering_batch(opt0, 1,
+                                                                                                              False)))
+    stats.clear()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    info = {}
+    out = shard.search_sharded(search, GapOpt.from_dict, opt0, lens, codes, REF_BATCH, world, rank, allreduce_max, info)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    mine_s = elapsed
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    q = sum(s["rank_queries"] for s in stats)
+    kms = sum(s["kernel_ms"] for s in stats)
+    t1 = time.perf_counter()
+    g = shard.gather_to_root(out, dist, comm, per_batch=True) if world > 1 else \
+        {b: (v[0], v[1], v[3]) for b, v in out.items()}
+    t_gather = time.perf_counter() - t1
+    # parity: a sample of one steady-state batch of this rank against the restatement
+    pb = next((b for b in mine if b > 0), None)
+    par = (rank, 0, 0, None)
+    if pb is not None and a.rank_parity:
+        from oracle_ctypes import default_opt
+        ox = host_oracle_index(res, T)
+        od = default_opt()
+        od.update(max_diff=4, fnr=-1.0, max_gapo=max_gapo, mode=od["mode"] & ~0x01)
+        n = min(a.rank_parity, bounds[pb][1] - bounds[pb][0])
+        o_n, o_f, o_h, _ = oracle_threaded(ox, reads[pb][:n], READ_LEN, od, cpu_info()["threads"])
+        n_aln, flags, hoff, hits = out[pb]
+        bad, first = compare_batch(n_aln[:n], flags[:n], hoff, np.asarray(hits, np.uint32).reshape(-1, 9), o_n, o_f,
+                                   o_h)
+        par = (rank, n, bad, first)
+        del ox
+        log(f"[bench] rank {rank}: parity batch {pb}: {n} reads, {bad} differ from the restatement")
+    pr = [par]
+    roof = [(rank, q, kms, mine_s)]
+    if world > 1:
+        pr, roof = [None] * world, [None] * world
+        dist.all_gather_object(pr, par)
+        dist.all_gather_object(roof, (rank, q, kms, mine_s))
+    if rank == 0:
+        n_got = sum(len(v[0]) for v in g.values())
+        qa, ka = sum(x[1] for x in roof), max(x[2] for x in roof)
+        ach = q * BYTES_PER_QUERY / (kms / 1e3) / 1e9 if kms > 0 else 0.0
+        result = {
+            "metric": METRIC, "value": round(R / elapsed, 1), "unit": "reads/s", "n_gpus": world, "steps": 1,
+            "warmup": 1, "ms_per_step": round(elapsed * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"{R} x {READ_LEN}bp reads fixed total ("
+                                   + ("one 1-3 bp indel + 0-2 substitutions, -n 4 -o 1" if a.config == 3 else
+                                      "0-4 substitutions, -n 4 -o 0")
+                                   + f") in the reference's {REF_BATCH}-read batches dealt round-robin over {world} "
+                                     f"GPU(s), bwa_cal_sa_reg_gap semantics on host arrays (H2D reads, search, D2H "
+                                     f"hits, per-read unpacking), the process's first batch with GAPE set (SURVEY Q2), "
+                                     f"vs synthetic hg19-sized 2BWT ({T} bp) (BASELINE configs[{a.config - 1}])",
+                       "genome_bp": T, "total_reads": R, "batches": len(bounds), "reads_per_batch": REF_BATCH,
+                       "parallelism": f"whole batches over {world} rank(s) (hsa_amd/shard.py), index replicated",
+                       "backend": dist.get_backend() if world > 1 else None},
+            "timing_window": "barrier -> every batch of the rank through hsa_cal_sa_reg_gap_flat (host arrays in and "
+                             "out) + the option-state all-reduce -> barrier, max over ranks; the gather after it",
+            "roofline": {"bound": "hbm", "kernel": "all search kernels of the calls", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms_rank0": round(kms, 1), "kernel_ms_max_rank": round(ka, 1),
+                         "rank_queries_all_ranks": int(qa)},
+            "gather": {"ms": round(t_gather * 1e3, 1), "batches": len(g), "reads": int(n_got),
+                       "complete": n_got == R and len(g) == len(bounds)},
+            "option_state": {"first_sticky_batch": info.get("first_sticky"), "rerun": info.get("rerun")},
+            "per_rank_s": {str(r): round(x[3], 3) for r, x in enumerate(roof)},
+            "parity_ranks": {str(r): {"batch_reads_checked": n, "mismatching_reads": b, "first_mismatch": f}
+                             for r, n, b, f in pr},
+            "parity_against": "oracle (C restatement), the first reads of one steady-state batch per rank"}
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    gi.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -603,6 +767,10 @@ def main():
                     help="also time the steps with the H2D reads and D2H hits inside them (value_with_copies)")
     ap.add_argument("--rank-parity", type=int, default=100_000,
                     help="with N > 1 ranks: reads of each rank's timed batch checked against the restatement")
+    ap.add_argument("--total-reads", type=int, default=0,
+                    help="fixed-total mode (strong scaling, BASELINE configs[2] as stated: e.g. --config 3 "
+                         "--total-reads 10000000): the reads in the reference's 100 000-read batches dealt over the "
+                         "ranks, host-array bwa_cal_sa_reg_gap semantics, gather timed apart (fixed_total)")
     a = ap.parse_args()
     if a.streams <= 0:
         # three handles where three handles' scratch fits: config 2 +1.8 % (profiles/r05_streams3_ab.log),
@@ -610,6 +778,10 @@ def main():
         a.streams = 3 if a.config in (2, 3) else 2
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a.gpus, sys.argv[1:]))
+    if a.total_reads > 0:
+        if a.config not in (2, 3):
+            sys.exit("--total-reads: configs 2 and 3")
+        return fixed_total(a)
 
     import hsa_amd  # noqa: F401  (libhsa_gpu.so before torch)
     import torch
