@@ -367,7 +367,9 @@ static __device__ unsigned long long g_diag[8192 * 4];
 // 9..12 shader cycles per wave in acquisition / control / rank-load wait / apply,
 // 13 gap_shadow calls with last_diff_pos > 0, 14 their summed last_diff_pos,
 // 15 strand starts, 16/17 exact/expand steps on a unique interval (l == k), 18/19
-// width steps on a unique interval / all width steps
+// width steps on a unique interval / all width steps; maxima over the launch's reads
+// (a read = acquisition to finish_job, both strands): 21 rank steps, 22 s_memrealtime
+// ticks (100 MHz), 23 pops
 static __device__ unsigned long long g_dctr[32];
 #define DC(i) (++dc[i])
 #else
@@ -814,6 +816,8 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     uint32_t dc[21] = {0};
     uint64_t tsec[4] = {0, 0, 0, 0};
     uint64_t tt = 0;
+    uint64_t rd_t0 = 0;
+    uint32_t rd_steps = 0, rd_p0 = 0;
 #define TMARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); tsec[k] += t_ - tt; tt = t_; } while (0)
 #endif
 
@@ -936,6 +940,11 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     };
     auto finish_job = [&](uint32_t fl, int na, uint64_t ho) {
         const ColdArgs r = cold_args();
+#ifdef HSA_DIAG
+        atomicMax(&g_dctr[21], (unsigned long long)rd_steps);
+        atomicMax(&g_dctr[22], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rd_t0));
+        atomicMax(&g_dctr[23], (unsigned long long)(st_p - rd_p0));
+#endif
         if (r->split) {                       // one strand of a read: k_split_finalize decides
             const uint32_t pi = qpos * 2u + (1u - C_STRAND(ctl));
             r->sp_n[pi] = (fl & HSA_F_OVERFLOW) ? -1 : na;
@@ -1132,6 +1141,9 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
                     if (j < (unsigned long long)n_jobs << (r->split ? 1 : 0)) {
                         const uint32_t item = (uint32_t)j;
+#ifdef HSA_DIAG
+                        rd_t0 = __builtin_amdgcn_s_memrealtime(); rd_steps = 0; rd_p0 = st_p;
+#endif
                         qpos = r->split ? item >> 1 : item;
                         if (r->perm) qpos = (uint32_t)r->perm[qpos];
                         const int job = r->job_list ? r->job_list[qpos] : (int)qpos;
@@ -1258,6 +1270,9 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         }
 #endif
         uint32_t two = 0;
+#ifdef HSA_DIAG
+        rd_steps += req == 1 ? 1u : 0u;
+#endif
         if (req == 1) {
             two = occ_pair(Ix<IT>::fwd(a), rp1, rp2, oa, ob) - 1u;
             st_q += 2u; st_b += 1u + two;
