@@ -1136,6 +1136,10 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64" if wide else "u32", "data": "synthetic",
+            "timing_window": ("device-resident reads: barrier -> K steps of widths + search kernels (+ the capacity "
+                              "re-runs; config 4: + the splice path) on device batches -> barrier, max over ranks; "
+                              "not SURVEY 8d's window (H2D reads -> kernels -> D2H hits), which value_with_copies "
+                              "times (N = 1)"),
             "config": {"workload": f"{a.batch // 1000}k x {RL}bp reads per step and GPU, "
                                    + {2: "0-4 substitutions", 3: "one 1-3 bp indel + 0-2 substitutions",
                                       4: "spliced (exon 40-110 bp, GT..AG intron 200-5000 bp), main path + the whole "
@@ -1158,6 +1162,14 @@ def main():
                                                f"{np.mean(ovl_w):.3f} ms, k_search {np.mean(ovl_s):.3f} ms per launch "
                                                "there)") if R else "the timed launches",
                          "k_search_frac_of_random_sector": round(ach_search / rand_gbs, 4),
+                         # the same kernel by its counter bytes (the PMC pass's FETCH + WRITE per launch):
+                         # Q credits 64 B to every reference query, while the kernel loads fewer
+                         # blocks (width trie, one block for both ends of a narrow interval, L2 hits)
+                         "k_search_counter_gbs": (round(pk["k_search"] / (ms_search / 1e3) / 1e9, 1)
+                                                  if pk.get("k_search") else None),
+                         "k_search_counter_frac_of_random_sector": (
+                             round(pk["k_search"] / (ms_search / 1e3) / 1e9 / rand_gbs, 4) if pk.get("k_search")
+                             else None),
                          "k_search_frac_of_random_sector_coop": round(ach_search / coop_gbs, 4),
                          "k_widths": {"ms": round(ms_widths, 3), "achieved": round(ach_widths, 1),
                                       "frac": round(ach_widths / HBM_PEAK_GBS, 4),

@@ -369,7 +369,8 @@ static __device__ unsigned long long g_diag[8192 * 4];
 // 15 strand starts, 16/17 exact/expand steps on a unique interval (l == k), 18/19
 // width steps on a unique interval / all width steps; maxima over the launch's reads
 // (a read = acquisition to finish_job, both strands): 21 rank steps, 22 s_memrealtime
-// ticks (100 MHz), 23 pops
+// ticks (100 MHz), 23 pops; 24 / 25 rank steps of the longest item that ended with /
+// without hits (split mode: an item is one strand)
 static __device__ unsigned long long g_dctr[32];
 #define DC(i) (++dc[i])
 #else
@@ -851,10 +852,30 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     // step needs, loaded in the control phase so that its latency overlaps the rank load
     const uint8_t *rowp = nullptr;
     uint32_t cur_c = 0;
+    // 4-bit format: the row word (4 positions) the last base came from, kept in registers.
+    // A strand's steps walk its positions downwards (the virtual top is the child at
+    // i - 1, an exact tail steps pos--), so most bases come from the word already held:
+    // a row load is one L2 request (the rows of the resident waves are far larger than
+    // L2 and mostly missed it), and the search is request-rate bound (config 5: 1.40 L2
+    // requests per rank query with a load per step, 0.97 in config 2's 8-bit rows).
+#ifndef HSA_ROWCACHE
+#define HSA_ROWCACHE 1                     // A/B builds: -DHSA_ROWCACHE=0 loads the byte every step
+#endif
+    uint32_t rw_q = 0xFFFFFFFFu, rw_w = 0;
     // base of the current strand's sequence at p (from the LDS element, or the HBM row)
     auto getc = [&](int p) -> uint32_t {
-        if constexpr (F::NIB) return WFmt<uint8_t>::code(rowp[((uint32_t)p >> 2) * 256u + ((uint32_t)p & 3u)]);
-        else return F::code(WB(p));
+        if constexpr (F::NIB && !HSA_ROWCACHE) {
+            return WFmt<uint8_t>::code(rowp[((uint32_t)p >> 2) * 256u + ((uint32_t)p & 3u)]);
+        } else if constexpr (F::NIB) {
+            const uint32_t q = (uint32_t)p >> 2;
+            if (q != rw_q) {
+                rw_w = *reinterpret_cast<const uint32_t *>(rowp + q * 256u);
+                rw_q = q;
+            }
+            return WFmt<uint8_t>::code((rw_w >> (((uint32_t)p & 3u) * 8u)) & 0xFFu);
+        } else {
+            return F::code(WB(p));
+        }
     };
     // stack bucket of an entry: dense index of its score (bwtgap.c:46-75)
     auto bucket_of = [&](uint32_t m) -> int {
@@ -908,6 +929,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         if constexpr (F::NIB) {
             // two 8-bit words per LDS word, eight loads in flight
             rowp = reinterpret_cast<const uint8_t *>(src);
+            rw_q = 0xFFFFFFFFu;
             auto pack = [&](const uint32_t *row, uint32_t nw, uint32_t *dst, uint32_t cap) {
                 const uint32_t nn = (nw + 1u) / 2u < cap ? (nw + 1u) / 2u : cap;   // LDS words of the row
                 for (uint32_t j = 0; j < nn; j += 4) {
@@ -944,6 +966,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         atomicMax(&g_dctr[21], (unsigned long long)rd_steps);
         atomicMax(&g_dctr[22], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rd_t0));
         atomicMax(&g_dctr[23], (unsigned long long)(st_p - rd_p0));
+        atomicMax(&g_dctr[na > 0 ? 24 : 25], (unsigned long long)rd_steps);
 #endif
         if (r->split) {                       // one strand of a read: k_split_finalize decides
             const uint32_t pi = qpos * 2u + (1u - C_STRAND(ctl));

@@ -15,6 +15,6 @@ make -C $S -s
 SP=$S/hsa_splice.o
 if [ "${VARIANT_SPLICE:-0}" = 1 ]; then /opt/rocm/bin/hipcc $F $X -c $S/hsa_splice.hip -o $D/sp.o & SP=$D/sp.o; fi
 wait
-/opt/rocm/bin/hipcc $F -shared $D/s.o $D/s64.o $S/hsa_index.o $S/hsa_bwt_build.o $S/hsa_sa.o $S/hsa_extend.o $SP $S/bwtaln_gpu.o $S/bwtgap_gpu.o $S/bwtse_gpu.o $S/bwtext_gpu.o -lpthread -lm -o $S/../libhsa_gpu_$N.so
+/opt/rocm/bin/hipcc $F -shared $D/s.o $D/s64.o $S/hsa_index.o $S/hsa_bwt_build.o $S/hsa_sa.o $S/hsa_extend.o $SP $S/bwtaln_gpu.o $S/bwtgap_gpu.o $S/bwtse_gpu.o $S/bwtsam_gpu.o $S/bwtext_gpu.o -lpthread -lm -o $S/../libhsa_gpu_$N.so
 rm -rf $D
 echo built hsa_amd/libhsa_gpu_$N.so

@@ -62,9 +62,11 @@ def main():
         wall = time.perf_counter() - t0
         L.hsa_diag_counters(buf, 0)
         steps, ticks, pops = int(buf[21]), int(buf[22]), int(buf[23])
+        steps_hit, steps_nohit = int(buf[24]), int(buf[25])
         rec = {"call_wall_ms": round(wall * 1e3, 2), "kernels_ms": round(st["kernel_ms"], 3),
                "main_pass_ms": round(st["main_kernel_ms"], 3),
-               "slowest_read_steps": steps, "slowest_read_pops": pops, "slowest_read_us": round(ticks / 100.0, 1),
+               "slowest_read_steps": steps, "slowest_read_pops": pops,
+               "slowest_item_with_hits_steps": steps_hit, "slowest_item_without_hits_steps": steps_nohit, "slowest_read_us": round(ticks / 100.0, 1),
                "ns_per_step_on_the_longest_read": round(ticks * 10.0 / max(steps, 1), 1),
                "rank_steps_mean_per_read": round(st["rank_queries"] / 2 / a.reads, 1),
                "mapped": int((n_aln > 0).sum())}
