@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2, choices=(2, 3))
     ap.add_argument("--batches", type=int, default=10)
+    ap.add_argument("--first", type=int, default=0, help="global index of the first batch (a run split over calls)")
     ap.add_argument("--batch", type=int, default=1_000_000)
     ap.add_argument("--max-seconds", type=float, default=0, help="stop after the batch that passes this wall time")
     ap.add_argument("--out", default=None)
@@ -76,7 +77,7 @@ def main():
     per = []
     tot = dict(reads=0, mismatching_reads=0, mapped=0, fallback=0, hits=0, rank_queries_gpu=0, rank_queries_oracle=0,
                gpu_s=0.0, oracle_s=0.0)
-    for j in range(a.batches):
+    for j in range(a.first, a.first + a.batches):
         t0 = time.perf_counter()
         if a.config == 2:
             reads, _ = synth.make_reads(genome, recs, N, RL, 5 * 1_000_000 + j, max_mm=4)
