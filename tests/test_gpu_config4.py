@@ -7,7 +7,7 @@ against the reference itself (oracle/_ref/ref_probe, compiled from its sources) 
 same index files, in the same batches: n_aln and every bwt_aln1_t word of every hit,
 splice-path hits included, in order.
 
-Both runs use batches of 1 250 reads (`-B`): the reference runs 16 processes of one
+Both runs use batches of N_READS / 16 reads (`-B`; 1 250 by default): the reference runs 16 processes of one
 batch each, so a batch's option regimes (the first fallback read switches aux->opt,
 bwtaln.c:363) are the same on both sides."""
 import os
@@ -25,8 +25,10 @@ REF = os.path.join(ROOT, "oracle", "_ref")
 
 pytestmark = pytest.mark.gpu
 
-N_READS = 20000
-CHUNK = 1250
+# HSA_C4_READS scales the run (the round-6 check ran 200 000: profiles/r06_config4_200k_dropin.log);
+# the reference always runs as 16 processes of one batch each
+N_READS = int(os.environ.get("HSA_C4_READS", "20000")) // 16 * 16
+CHUNK = N_READS // 16
 
 
 @pytest.mark.skipif(not (os.path.exists(os.path.join(REF, "ref_probe")) and
