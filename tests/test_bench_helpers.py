@@ -138,3 +138,29 @@ def test_parse_batch_stages_sums_the_calls():
     assert abs(search_s - 0.353) < 1e-9 and abs(prefetch_s - 0.330) < 1e-9 and abs(splice_s - 0.006) < 1e-9
     assert len(calls) == 2 and abs(calls[0] - 0.448) < 1e-9 and abs(calls[1] - 0.241) < 1e-9
     assert bench.parse_batch_stages("no stage lines\n") == (0.0, 0.0, 0.0, 0, [])
+
+
+def test_fixed_total_batch_codes_follow_search_sharded():
+    """bench.py --total-reads: shard.search_sharded slices the global codes by batch
+    (codes[offs[b0]:offs[b1]]); _BatchCodes holds only this rank's batches and hands each
+    slice its batch.  With world 3 and a ragged 7-batch stream, rank 1 searches batches 1
+    and 4 with the option state the sequential reference has there."""
+    from hsa_amd import shard
+    L, B, R, world, rank = 5, 4, 26, 3, 1
+    bounds = shard.batch_bounds(R, B)
+    mine = shard.my_batches(len(bounds), world, rank)
+    assert len(bounds) == 7 and mine == [1, 4]
+    reads = {b: np.full((bounds[b][1] - bounds[b][0], L), b, np.uint8) for b in mine}
+    codes = bench._BatchCodes(reads, B * L)
+    seen = []
+
+    def search(lens, c, o):
+        seen.append((int(c[0]), len(lens), len(c), o.mode & 1))
+        return np.zeros(len(lens), np.int32), np.zeros(len(lens), np.uint32), np.zeros(len(lens), np.uint64), \
+            np.zeros((0, 9), np.uint32)
+
+    opt0 = {"mode": 0x03, "seed_len": 32}
+    from types import SimpleNamespace
+    out = shard.search_sharded(search, lambda d: SimpleNamespace(**d), opt0, np.full(R, L, np.uint32), codes, B, world, rank, lambda x: x)
+    assert sorted(out) == [1, 4]
+    assert seen == [(1, 4, 20, 0), (4, 4, 20, 0)]      # batch 1 and 4: GAPE already cleared (SURVEY Q2)
