@@ -200,8 +200,8 @@ def host_oracle_index(res, T):
 # its "step" mode, which sums the main path's and the splice seeds' kernels); the
 # kernel-trace summaries next to them (tools/trace_summary.py) give the same runs'
 # per-launch durations
-TRAFFIC_SRCS = {2: "profiles/r05_pmc_summary_config2.json", 3: "profiles/r05_pmc_summary_config3.json",
-                4: "profiles/r05_pmc_summary_config4.json", 5: "profiles/r05_pmc_summary_config5.json"}
+TRAFFIC_SRCS = {2: "profiles/r06_pmc_summary_config2.json", 3: "profiles/r05_pmc_summary_config3.json",
+                4: "profiles/r05_pmc_summary_config4.json", 5: "profiles/r06_pmc_summary_config5.json"}
 
 
 def traffic_per_kernel(config):
