@@ -470,16 +470,35 @@ __device__ __forceinline__ WRow width_row(const SearchArgs &a, uint32_t R, uint3
     WChain<IT> f{0, Ix<IT>::T(a), 0, 0, 0, 0, 0}, sd{0, Ix<IT>::T(a), 0, 0, 0, 0, 0};
     uint32_t st_q = 0, st_b = 0, st_t = 0;
     const uint32_t s0 = len - slen;
-    auto base = [&](uint32_t sp) -> uint32_t {
-        const uint32_t c = a.codes[off + (strand ? len - 1u - sp : sp)];
+#ifndef HSA_CODECACHE
+#define HSA_CODECACHE 1                    // A/B builds: -DHSA_CODECACHE=0 loads a byte every step
+#endif
+    // Each chain walks its read one position per step (forwards, or backwards on the rc
+    // strand), so the 4-byte word of its last base is kept in registers and a load goes
+    // out every fourth step.  The codes buffer is 4-byte aligned and padded past its last
+    // read (hsa_device_batch_t.d_codes), so the word load stays inside it.
+    uint32_t cq[2] = {0xFFFFFFFFu, 0xFFFFFFFFu}, cword[2] = {0u, 0u};
+    auto base = [&](uint32_t sp, int ch) -> uint32_t {
+        const uint64_t ix = off + (strand ? len - 1u - sp : sp);
+        uint32_t c;
+        if constexpr (HSA_CODECACHE) {
+            const uint32_t wq = (uint32_t)(ix >> 2);
+            if (wq != cq[ch]) {
+                cword[ch] = *reinterpret_cast<const uint32_t *>(a.codes + (ix & ~(uint64_t)3));
+                cq[ch] = wq;
+            }
+            c = (cword[ch] >> (((uint32_t)ix & 3u) * 8u)) & 0xFFu;
+        } else {
+            c = a.codes[ix];
+        }
         return strand && c < 4 ? 3u - c : c;
     };
     for (uint32_t t = 0; t <= len; ++t) {
-        const uint32_t cf = t < len ? base(t) : 4u;
+        const uint32_t cf = t < len ? base(t, 0) : 4u;
         // the read's elements also carry the strand sequence's base (k_search's getc)
         width_step<WT, IT>(a, f, t, len, cf, t < len ? F::code_bits(cf) : 0u, brow, wrow, st_q, st_b, st_t);
         if (has_seed && t <= slen) {
-            const uint32_t cs = t < slen ? base(s0 + t) : 4u;
+            const uint32_t cs = t < slen ? base(s0 + t, 1) : 4u;
             width_step<WT, IT>(a, sd, t, slen, cs, 0u, srow, nullptr, st_q, st_b, st_t);
         }
     }
