@@ -198,8 +198,10 @@ int  hsa_gpu_set_devices(int n);
  * value bwtse.c:146 and every other hit position bwtse.c:362) run as one GPU batch
  * (hsa_sa_position_batch: BWTSaValue + BWTRetrievePositionFromSAIndex), then the same
  * per-read updates (mapQ, seq_id/ori_pos/occ_pos, duplicate-position filter) in the
- * same order.  Splicing reads keep the host's bwt_aln2pos_splicing (bwtse.c:295).
- * Needs the host's bwa_approx_mapQ, bwa_cal_maxdiff and bwt_aln2pos_splicing. */
+ * same order.  A splicing read's lookups (the first 50 rows of both segments,
+ * bwtse.c:320) join the same batch, and its segment pairing (bwt_aln2pos_splicing /
+ * bwt_combine_segment_splice, bwtse.c:295-348, :197-235) is restated.
+ * Needs the host's bwa_approx_mapQ and bwa_cal_maxdiff. */
 void bwa_cal_pac_pos(const Idx2BWT *bi_bwt, int n_seqs, bwa_seq_t *seqs, int max_mm, float fnr);
 
 /* generate_sam_se_core: replaces bwtse.c:884 (declared bwtse.h; called once per batch,
