@@ -598,13 +598,6 @@ struct PfArgs {
 
 __device__ __forceinline__ uint32_t pf_n(const PfArgs &a) { return a.d_n ? (uint32_t)*a.d_n : a.n; }
 
-__device__ __forceinline__ uint32_t pf_base(const PfArgs &a, uint32_t r, uint32_t s, uint32_t p)
-{
-    const uint32_t L = a.lens[r];
-    const uint32_t c = a.codes[a.offs[r] + (s ? L - 1u - p : p)];
-    return s && c < 4 ? 3u - c : c;         // the reverse complement (bwtaln.c:326-333)
-}
-
 // thread (r, s, kind): kind 0 bwt_cal_width type 1 of the whole strand (and the strand's
 // codes), 1 type 1 of its last 12 bases, 2 type 0 of the whole strand (bwtaln.c:73-116;
 // the same chains as k_width / k_width0)
@@ -614,15 +607,29 @@ __global__ void __launch_bounds__(BLOCK) k_pf_rows(PfArgs a)
     const uint32_t r = t / 6u, s = (t % 6u) & 1u, kind = (t % 6u) >> 1;
     if (r >= pf_n(a)) return;
     const uint32_t L = a.lens[r];
+    const uint64_t off = a.offs[r];
     int32_t *const o = a.rows + 2 * ((size_t)r * 6u + kind * 2u + s) * a.rs;
     uint32_t k = 0, l = a.T, bid = 0;
+    // the strand's base at p from the 4-byte code word of the last one, held in
+    // registers: a chain walks its read one position per step (the codes are 4-byte
+    // aligned and padded past the last read)
+    uint32_t cq = 0xFFFFFFFFu, cword = 0;
+    auto base = [&](uint32_t p) -> uint32_t {
+        const uint64_t ix = off + (s ? L - 1u - p : p);
+        if ((uint32_t)(ix >> 2) != cq) {
+            cword = *reinterpret_cast<const uint32_t *>(a.codes + (ix & ~(uint64_t)3));
+            cq = (uint32_t)(ix >> 2);
+        }
+        const uint32_t c = (cword >> (((uint32_t)ix & 3u) * 8u)) & 0xFFu;
+        return s && c < 4 ? 3u - c : c;     // the reverse complement (bwtaln.c:326-333)
+    };
     if (kind == 0 || kind == 1) {
         if (kind == 1 && L < 12u) return;
         const uint32_t p0 = kind == 1 ? L - 12u : 0u, n = kind == 1 ? 12u : L;
         uint8_t *const sc = a.scodes + (size_t)(2u * r + s) * a.sc;
         uint32_t tl = 0, tix = 0;            // characters since the last reset and their trie node
         for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t c = pf_base(a, r, s, p0 + i);
+            const uint32_t c = base(p0 + i);
             if (kind == 0) sc[i] = (uint8_t)c;
             if (c < 4) {
                 if (tl < a.ktd) {            // the same forward extension, from the width trie
@@ -638,16 +645,14 @@ __global__ void __launch_bounds__(BLOCK) k_pf_rows(PfArgs a)
                 }
             }
             if (k > l || c > 3) { k = 0; l = a.T; ++bid; tl = 0; tix = 0; }
-            o[2 * i] = (int32_t)(l - k + 1u);
-            o[2 * i + 1] = (int32_t)bid;
+            *reinterpret_cast<int2 *>(o + 2 * i) = make_int2((int32_t)(l - k + 1u), (int32_t)bid);
         }
-        o[2 * n] = 0;
-        o[2 * n + 1] = (int32_t)(bid + 1u);
+        *reinterpret_cast<int2 *>(o + 2 * n) = make_int2(0, (int32_t)(bid + 1u));
         return;
     }
-    o[0] = 0; o[1] = 0;                      // entry 0: never written by the reference
+    *reinterpret_cast<int2 *>(o) = make_int2(0, 0);       // entry 0: never written by the reference
     for (uint32_t i = L - 1u; i > 0 && L > 0; --i) {
-        const uint32_t c = pf_base(a, r, s, i);
+        const uint32_t c = base(i);
         if (c < 4) {
             uint32_t ok, ol;
             hsa_occ1_pair(a.fwd, k, l + 1u, c, ok, ol);
@@ -656,11 +661,9 @@ __global__ void __launch_bounds__(BLOCK) k_pf_rows(PfArgs a)
             l = cc + ol;
         }
         if (k > l || c > 3) { k = 0; l = a.T; ++bid; }
-        o[2 * i] = (int32_t)(l - k + 1u);
-        o[2 * i + 1] = (int32_t)bid;
+        *reinterpret_cast<int2 *>(o + 2 * i) = make_int2((int32_t)(l - k + 1u), (int32_t)bid);
     }
-    o[2 * L] = 0;
-    o[2 * L + 1] = (int32_t)(bid + 1u);
+    *reinterpret_cast<int2 *>(o + 2 * L) = make_int2(0, (int32_t)(bid + 1u));
 }
 
 // thread (r, call 0..5): seed t of strand s (bwtgap.c:797-812): the strand [t sl, t sl + la)
