@@ -967,7 +967,7 @@ def main():
     n_pt = len(w_ms)
     splice_ms = float(np.mean(kms[-n_pt:]) - np.mean(w_ms) - np.mean(s_ms)) if a.config == 4 else None
     log(f"[bench] rank {rank}: per-step kernels: k_widths {np.mean(w_ms):.2f} ms, k_search {np.mean(s_ms):.2f} ms"
-        + (f", splice path {splice_ms:.2f} ms" if a.config == 4 else ""))
+        + (f", splice path {splice_ms:.2f} ms" if a.config == 4 and S == 1 else ""))
     if os.environ.get("HSA_DIAG_OUT"):
         diag_dump(os.environ["HSA_DIAG_OUT"])
     log(f"[bench] rank {rank}: per-step device ms {[round(x, 2) for x in kms]}, wall {elapsed * 1e3:.1f} ms")
@@ -979,11 +979,18 @@ def main():
     roof_sets = [(a.warmup + s) % nd for s in range(a.steps)]
     if R:
         torch.cuda.synchronize()
+        evr = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(R)]
         for s in range(R):
+            evr[s][0].record(lib_streams[0])
             launch(a.warmup + s, 0)
+            evr[s][1].record(lib_streams[0])
         torch.cuda.synchronize()
         w_ms, s_ms = (x.astype(float) for x in handles[0].pass_times(min(R, PASS_RING)))
         roof_sets = [(a.warmup + s) % nd for s in range(R)][-len(w_ms):]
+        if a.config == 4:       # the splice path of a step alone: the serialized step less its two kernels
+            step_ser = [e0.elapsed_time(e1) for e0, e1 in evr][-len(w_ms):]
+            splice_ms = float(np.mean(step_ser) - np.mean(w_ms) - np.mean(s_ms))
+            log(f"[bench] rank {rank}: splice path of a serialized step: {splice_ms:.2f} ms")
         log(f"[bench] rank {rank}: {R} serialized steps: k_widths {np.mean(w_ms):.2f} ms, k_search "
             f"{np.mean(s_ms):.2f} ms (overlapped in the timed region: {np.mean(ovl_w):.2f} / {np.mean(ovl_s):.2f} ms)")
     # The same K steps with the PCIe copies inside each step (SURVEY §8d's timing window:
