@@ -79,6 +79,20 @@ void OR(depth_hist)(uint64_t *out, int reset)
 #define hist_pair(w, a, b, c) ((void)0)
 #endif
 
+#ifdef OR_DUP_STATS
+/* Experiment build only (liboracle_dup.so, tools/dup_stats.py): how many expansions of a
+ * bwt_match_gap search repeat one already made in the same search -- the same node
+ * (i, k, l, rk, state) with the same counts (exact), or with counts >= an earlier one's
+ * (dominated) -- split by whether the search ends with hits.  [0] expansions, [1] exact
+ * repeats, [2] dominated ones, of searches with hits; [3]-[5] of searches without. */
+static __thread uint64_t tl_dup[6];
+void OR(dup_stats)(uint64_t *out, int reset)
+{
+    memcpy(out, tl_dup, sizeof tl_dup);
+    if (reset) memset(tl_dup, 0, sizeof tl_dup);
+}
+#endif
+
 struct or_index {
     or_bwt_t f, r;
     int unused;
@@ -516,6 +530,15 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
     out->n = 0;
     stack_reset(st);
     push(st, len, 0, T, 0, T, 0, 0, 0, 0, 0, opt);
+#ifdef OR_DUP_STATS
+    /* the search's expanded nodes: (i, k, l, rk, state) -> counts, open addressing */
+    enum { DUPCAP = 1 << 18 };
+    typedef struct { uint64_t key, key2; uint32_t cnt; uint32_t used; } dupe_t;
+    static __thread dupe_t *dtab;
+    if (!dtab) dtab = (dupe_t *)calloc(DUPCAP, sizeof(dupe_t));
+    else memset(dtab, 0, sizeof(dupe_t) * DUPCAP);
+    uint64_t d_exp = 0, d_ex = 0, d_dom = 0;
+#endif
     while (st->n_entries) {
         ent_t e;
         int i, m, m_seed = 0, hit = 0, allow_diff, allow_M, tmp;
@@ -569,6 +592,30 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
             }
             continue;
         }
+#ifdef OR_DUP_STATS
+        {
+            const uint64_t key = (uint64_t)k << 32 | (uint64_t)l, key2 = (uint64_t)rk << 32 | (uint64_t)i << 4 | e.state;
+            const uint32_t cnt = (uint32_t)e.n_mm | (uint32_t)e.n_gapo << 8 | (uint32_t)e.n_gape << 16;
+            uint64_t h = (key * 0x9E3779B97F4A7C15ull) ^ (key2 * 0xC2B2AE3D27D4EB4Full);
+            int exact = 0, dom = 0;
+            /* every earlier expansion of this node (several count triples may share it) */
+            for (uint32_t j = (uint32_t)(h >> 46) & (DUPCAP - 1); dtab[j].used; j = (j + 1) & (DUPCAP - 1)) {
+                if (dtab[j].key != key || dtab[j].key2 != key2) continue;
+                const uint32_t c = dtab[j].cnt;
+                if (c == cnt) exact = 1;
+                else if ((c & 255) <= (cnt & 255) && ((c >> 8) & 255) <= ((cnt >> 8) & 255) && (c >> 16) <= (cnt >> 16))
+                    dom = 1;
+            }
+            ++d_exp;
+            if (exact) ++d_ex;
+            else if (dom) ++d_dom;
+            if (!exact && d_exp < DUPCAP / 2) {
+                uint32_t j = (uint32_t)(h >> 46) & (DUPCAP - 1);
+                while (dtab[j].used) j = (j + 1) & (DUPCAP - 1);
+                dtab[j].key = key; dtab[j].key2 = key2; dtab[j].cnt = cnt; dtab[j].used = 1;
+            }
+        }
+#endif
         --i;
         HIST_DEPTH(len - i);
         step_all(ix, k, l, rk, rl, sk, sl, srk, srl);
@@ -620,6 +667,12 @@ static void match_gap(or_index_t *ix, stack_t_ *st, const or_opt_t *opt, const u
                 push(st, i, sk[c], sl[c], srk[c], srl[c], e.n_mm, e.n_gapo, e.n_gape, ST_M, 0, opt);
         }
     }
+#ifdef OR_DUP_STATS
+    {
+        const int o = n_aln > 0 ? 0 : 3;
+        tl_dup[o] += d_exp; tl_dup[o + 1] += d_ex; tl_dup[o + 2] += d_dom;
+    }
+#endif
 }
 
 /* bwt_match_gap (bwtgap.c:118-331) called directly, as bwt_splice_match does
