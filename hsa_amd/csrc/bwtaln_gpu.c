@@ -652,21 +652,26 @@ static void search_warm(const Idx2BWT *bi)
     }
 }
 
-/* HSA_SPLICE_WARM=1: the device splice path once at attach, on a batch the size of a
- * host's batch of 150 bp reads (131 072 random reads; answers discarded), so that the
- * prefetch pass's and the splice kernel's buffers exist before the first batch (their
- * first allocation is ~0.2 s of the first call).  Opt-in: the buffers it sizes for a
- * full-chip pass stay allocated, which raised the footprint enough to slow a second
- * process sharing the GPU (the bench's end-to-end leg beside the bench itself) from
- * 0.26 s to 11 s per call.  Non-fatal: a failure is logged under HSA_VERBOSE. */
+/* The device splice path once at attach, on synthetic reads (answers discarded), so that
+ * the first batch does not pay for its kernels' first launches and first buffers.  By
+ * default 4 096 reads: the prefetch pass's and the splice kernel's first launches, and
+ * buffers for the few thousand fallback reads of a 100 000-read batch of unspliced reads
+ * (the first call's device splice pass: 23 -> 13 ms with 64 reads).  HSA_SPLICE_WARM=1: a
+ * batch the size of a host's batch of 150 bp reads (131 072 reads), so that the full-chip
+ * buffers exist before the first batch too (their first allocation is ~0.2 s of the
+ * first call); opt-in because those buffers stay allocated, which raised the footprint
+ * enough to slow a second process sharing the GPU (the bench's end-to-end leg beside the
+ * bench itself) from 0.26 s to 11 s per call.  HSA_SPLICE_WARM=0: none.  Non-fatal: a
+ * failure is logged under HSA_VERBOSE. */
 static void splice_device_warm(const Idx2BWT *bi)
 {
     const char *sde = getenv("HSA_SPLICE_DEVICE"), *w = getenv("HSA_SPLICE_WARM");
-    if ((sde && atoi(sde) == 0) || !w || atoi(w) == 0) return;
+    if ((sde && atoi(sde) == 0) || (w && atoi(w) == 0) || bwt_splice_match == NULL) return;
     int n_slots = 0;
     hsa_index_t *const *slots = hsa_gpu_slots_of(bi, &n_slots);
     if (n_slots < 1) return;
-    enum { N_WARM = 131072, L_WARM = 150 };
+    enum { L_WARM = 150 };
+    const int N_WARM = w && atoi(w) == 1 ? 131072 : 4096;
     uint32_t *lens = (uint32_t *)malloc(sizeof(uint32_t) * N_WARM);
     uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * N_WARM);
     int32_t *amd = (int32_t *)malloc(sizeof(int32_t) * N_WARM);
@@ -695,9 +700,11 @@ static void splice_device_warm(const Idx2BWT *bi)
         hsa_splice_pf_t pf;
         hsa_splice_stats_t st;
         const double t0 = hsa_now();
+        int rc = 0;
         hsa_gpu_lock();
-        const int rc = hsa_splice_match_batch(slots[0], &srg, &arg_, &erg, N_WARM, lens, offs, codes,
-                                              (size_t)N_WARM * L_WARM, amd, &pf, res, &st);
+        for (int k = 0; k < n_slots && !rc; ++k)     /* each device loads the kernels */
+            rc = hsa_splice_match_batch(slots[k], &srg, &arg_, &erg, N_WARM, lens, offs, codes,
+                                        (size_t)N_WARM * L_WARM, amd, &pf, res, &st);
         hsa_gpu_unlock();
         if (getenv("HSA_VERBOSE"))
             fprintf(stderr, "[hsa] splice path warm-up: %d reads, %.3f s%s%s\n", N_WARM, hsa_now() - t0,
