@@ -121,9 +121,9 @@ extern "C" int hsa_index_release_scratch(hsa_index_t *ix)
     (void)hipSetDevice(ix->device);
     HSA_HIP(hipStreamSynchronize(ix->stream));
     hsa_scratch_free(ix->main); hsa_scratch_free(ix->big); hsa_scratch_free(ix->huge);
-    void **bufs[] = {&ix->d_pf, &ix->d_pf2, &ix->d_sp, &ix->d_any, &ix->d_any_aux};
-    size_t *caps[] = {&ix->d_pf_cap, &ix->d_pf2_cap, &ix->d_sp_cap, &ix->d_any_cap, &ix->d_any_aux_cap};
-    for (int i = 0; i < 5; ++i) {
+    void **bufs[] = {&ix->d_pf, &ix->d_pf2, &ix->d_sp, &ix->d_any, &ix->d_any_aux, &ix->d_help};
+    size_t *caps[] = {&ix->d_pf_cap, &ix->d_pf2_cap, &ix->d_sp_cap, &ix->d_any_cap, &ix->d_any_aux_cap, &ix->d_help_cap};
+    for (int i = 0; i < 6; ++i) {
         if (*bufs[i]) (void)hipFree(*bufs[i]);
         *bufs[i] = nullptr;
         *caps[i] = 0;
@@ -529,6 +529,7 @@ extern "C" void hsa_index_free(hsa_index_t *ix)
     if (ix->d_any) (void)hipFree(ix->d_any);
     if (ix->d_any_aux) (void)hipFree(ix->d_any_aux);
     if (ix->d_split) (void)hipFree(ix->d_split);
+    if (ix->d_help) (void)hipFree(ix->d_help);
     if (ix->d_fwd) (void)hipFree(ix->d_fwd);
     if (ix->d_pf) (void)hipFree(ix->d_pf);
     if (ix->d_pf2) (void)hipFree(ix->d_pf2);

@@ -62,6 +62,7 @@ struct hsa_index {
     void *d_any = nullptr; size_t d_any_cap = 0;
     void *d_any_aux = nullptr; size_t d_any_aux_cap = 0;
     void *d_split = nullptr; size_t d_split_cap = 0;   // strand-split items' results (k_split_finalize)
+    void *d_help = nullptr; size_t d_help_cap = 0;     // strand-split tails: the shared frontier (k_search helpers)
     void *d_fwd = nullptr; size_t d_fwd_cap = 0;       // lazy forward rows: count + reads for the forward pass
     // hsa_splice_prefetch_batch: inputs, calls and outputs; its SA lookups; the pinned
     // host copy of the outputs the caller's tables point into
@@ -90,6 +91,7 @@ struct hsa_index {
     int staged_valid = 0;
     bool staged_mmb = false;            // staged regimes: bucket == n_mm (see mm_buckets)
     int staged_ntab = 128;              // staged regimes: score table entries per regime (k_search LDS)
+    int staged_min_entries = 0;         // staged regimes: the smallest max_entries (helpers need > the pool)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evm = nullptr;           // between k_widths and k_search of the last pass (timing split)
     hipEvent_t ev_sp = nullptr;         // after the splice kernel (hsa_splice_match_batch: ev1 .. ev_sp)

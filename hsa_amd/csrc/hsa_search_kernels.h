@@ -56,7 +56,7 @@
 #define MAXB 128          // dense buckets per regime (BMask<2>)
 #define MAXS 512          // score table length per regime (n_stacks <= MAXS)
 
-enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END };
+enum : uint32_t { PH_IDLE = 0, PH_POP, PH_EXACT, PH_EXPAND, PH_EXIT, PH_END, PH_WAIT };
 
 struct SearchArgs {
     RankDir fwd, rev;
@@ -137,7 +137,29 @@ struct SearchArgs {
     // forward row (when computed) at row rmap[q], so every width lane stores coalesced;
     // null: row q * 2 + strand
     int32_t *rmap;
+    // strand-split tails (helpers, k_search): a strand search with no hit yet that has run
+    // fr_budget pops while more lanes wait for work than the shared frontier holds offers
+    // its live entries there; waiting lanes search them (each entry a sub-search rooted at
+    // it) and report only whether the item has a hit.  The owner keeps searching in the
+    // reference's order; when every sub-search of its frontier ended without a hit it stops
+    // with no hits, which is its own search's answer: before a hit, a strand search expands
+    // the same entries in any order ("Helpers").  fr_budget 0: off.
+    uint32_t fr_budget, fr_demand, fr_cap;
+    uint32_t *fr_ent;              // published chunks: FR_CH entries of FR_EW words each
+    uint32_t *fr_tag;              // per chunk: entries << 26 | (item + 1)
+    uint32_t *fr_rq;               // ready queue: chunk + 1 once the chunk is complete (0 before)
+    uint32_t *fr_st;               // per item: chunks not yet searched | FR_DONE | FR_HIT
+    unsigned long long *fr_q, *fr_p;   // per item: its sub-searches' rank queries and pops
+    unsigned long long *fr_c;      // [0] chunks reserved [1] ready-queue head (taken) [2] items finished
+                                   // [3] lanes waiting [4] offers [5] offers refused (capacity) [6] sub-
+                                   // searches ended [7] owners answered by their helpers [8] sub-searches'
+                                   // rank queries [9] ready-queue tail
 };
+#define FR_HIT 0x80000000u
+#define FR_DONE 0x40000000u
+#define FR_EW 8u                   // words per published entry (32- and 64-bit intervals)
+#define FR_CH 16u                  // entries per chunk: one sub-search searches a chunk's sub-trees
+#define FR_WALK 1024u              // largest stack a strand offers (the walk is a chain of dependent loads)
 
 // The kernel's arguments re-read from the kernarg segment where a rare path uses them
 // (strand start and end, next read, hit staging): the asm barrier keeps the compiler
@@ -831,6 +853,13 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     // VGPRs: wave-uniform accumulators pushed the kernel's SGPRs into spills
     uint32_t st_p = 0, st_wq = 0, st_q = 0, st_b = 0;
     uint32_t sq0 = 0, sp0 = 0;            // split mode: the counters when the item started
+    // helpers (SearchArgs::fr_*): frs bit 0 the strand offered its frontier (owner), bit 1
+    // this lane runs a sub-search, bit 2 no more offers from this strand; fr_p0 the pops at
+    // the strand's start, then at the offer (owner) or the sub-search's start (helper), with
+    // fr_q0 the rank queries at that point
+    uint32_t frs = 0, fr_p0 = 0, fr_q0 = 0;
+    uint32_t fr_tick = 0;          // the wave's iterations (waiting lanes poll every 128)
+    uint32_t st_hs = 0, st_hq = 0; // sub-searches this lane ran, and their rank queries
     const uint32_t n_jobs = a.n_dev ? (uint32_t)*a.n_dev : (uint32_t)a.n_jobs;
 #ifdef HSA_DIAG
     uint32_t dc[21] = {0};
@@ -928,8 +957,11 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         e = E{0, TT, 0, meta_pack((uint32_t)C_LEN(ctl), ST_M, 0, 0, 0, 0)};   // root (bwtgap.c:142)
         ctl |= 1u << 6;
         n_entries = 1;
+        frs = 0; fr_p0 = st_p;
         SET_PH(ctl, PH_POP);
     };
+    // the item number of the strand this lane searches (split mode: list position * 2 + 1 for fwd)
+    auto fr_key = [&]() -> uint32_t { return qpos * 2u + (1u - C_STRAND(ctl)); };
     // width row of the current strand: row qpos * 2 + strand, 64 rows interleaved
     auto row_base = [&](uint32_t cap_words) -> size_t {
         const int32_t *const rm = cold_args()->rmap;
@@ -994,6 +1026,13 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             r->sp_q[pi] = st_q - sq0;
             r->sp_p[pi] = st_p - sp0;
             st_q = sq0; st_p = sp0;
+            if constexpr (!HUGE) {
+                if (a.fr_budget) {
+                    if (frs & 1u) atomicOr(&r->fr_st[pi], FR_DONE);   // its helpers stop
+                    atomicAdd(&r->fr_c[2], 1ull);                      // items finished (the exit test)
+                    frs = 0;
+                }
+            }
             SET_PH(ctl, PH_IDLE);
             return;
         }
@@ -1012,7 +1051,24 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         r->hit_off[job] = ho;
         SET_PH(ctl, PH_IDLE);
     };
+    // a sub-search ends (no hit, a hit, its item decided, or its entries offered on): its
+    // work goes to the item's sums, then its count leaves the item's open sub-searches
+    auto help_done = [&]() {
+        const ColdArgs r = cold_args();
+        const uint32_t key = fr_key();
+        const unsigned long long dq = st_q - fr_q0, dp = st_p - fr_p0;
+        st_q = fr_q0; st_p = fr_p0;
+        const unsigned long long o1 = atomicAdd(&r->fr_q[key], dq), o2 = atomicAdd(&r->fr_p[key], dp);
+        asm volatile("s_waitcnt vmcnt(0)" :: "v"(o1), "v"(o2) : "memory");   // the sums land first
+        atomicSub(&r->fr_st[key], 1u);
+        ++st_hs; st_hq += (uint32_t)dq;
+        frs = 0;
+        SET_PH(ctl, PH_IDLE);
+    };
     auto end_strand = [&]() {
+        if constexpr (!HUGE) {
+            if (frs & 2u) { help_done(); return; }
+        }
         if (n_aln > 0) {
             const ColdArgs r = cold_args();
             const unsigned long long o = atomicAdd(&r->ctr[1], (unsigned long long)n_aln);
@@ -1070,6 +1126,12 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     // returns false when the search must stop
     auto on_hit = [&](IT k, IT l, IT rk, IT rl) -> bool {
         const ColdArgs r = cold_args();
+        if constexpr (!HUGE) {
+            if (frs & 3u) {
+                atomicOr(&r->fr_st[fr_key()], FR_HIT);   // the item has a hit: its sub-searches stop
+                if (frs & 2u) return false;              // a helper records nothing
+            }
+        }
         const uint32_t m = e.w;
         const int score = SCORE(M_MM(m), M_GO(m), M_GE(m));
         if (n_aln == 0) {
@@ -1150,10 +1212,170 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         return mm;
     };
 
+    // start work item `item` (a read, a strand in split mode, or a direct call)
+    auto begin_item = [&](uint32_t item) {
+        const ColdArgs r = cold_args();
+#ifdef HSA_DIAG
+        rd_t0 = __builtin_amdgcn_s_memrealtime(); rd_steps = 0; rd_p0 = st_p;
+#endif
+        qpos = r->split ? item >> 1 : item;
+        if (r->perm) qpos = (uint32_t)r->perm[qpos];
+        const int job = r->job_list ? r->job_list[qpos] : (int)qpos;
+        const hsa_job_t J = r->jobs[job];
+        opt_max_diff = J.max_diff;
+        const uint32_t len = J.len;
+        if (r->mg) {
+            // one direct bwt_match_gap call: its strand, its width_seed kind
+            // (host-checked: 0 <= seed_len <= len when width_seed is given)
+            const hsa_mg_job_t M = r->mg[job];
+            const uint32_t has_seed = M.seed != HSA_SEED_NONE;
+            ctl = (uint32_t)(M.strand & 1) << 3 | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 |
+                  (M.seed == HSA_SEED_ALIAS ? 1u : 0u) << 7 | len << 10 |
+                  (has_seed ? (uint32_t)J.seed_len : 0u) << 20;
+        } else {
+            const uint32_t has_seed = (int)len > J.seed_len;
+            ctl = 8u | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 | len << 10 |
+                  (has_seed ? (uint32_t)J.seed_len : 0u) << 20;     // strand 1 (rc first, bwtaln.c:343)
+            if ((r->split && (item & 1u)) || r->fwd_only) ctl &= ~8u;   // split: odd items search fwd
+            sq0 = st_q; sp0 = st_p;
+        }
+        const hsa_regime_t *R = s_reg + (J.regime & 1);
+        pen = (uint32_t)R->s_mm | (uint32_t)R->s_gapo << 10 | (uint32_t)R->s_gape << 20;
+        rmode = (uint32_t)R->mode | (uint32_t)R->max_gapo << 8 | (uint32_t)R->max_gape << 16;
+        if (opt_max_diff > R->max_diff) ctl |= 2u << 8;
+        start_strand();
+    };
+    // helpers: publish this strand's live entries -- the virtual top, then every bucket's
+    // list -- as sub-search roots of its item.  An entry's words are stored at agent scope
+    // and its tag after a release, and the item's open-sub-search count is raised first, so
+    // the count never reaches zero while one of them is unsearched.  False (nothing
+    // published): the frontier is full, or the lists do not add up to n_entries.
+    auto fr_offer = [&]() -> bool {
+        const ColdArgs r = cold_args();
+        const uint32_t cnt = (uint32_t)n_entries, nch = (cnt + FR_CH - 1u) / FR_CH;
+        unsigned long long o = __hip_atomic_load(&r->fr_c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (;;) {                                       // reserve nch chunks (no walk when they do not fit)
+            if (o + nch > (unsigned long long)r->fr_cap) { atomicAdd(&r->fr_c[5], 1ull); return false; }
+            const unsigned long long w = atomicCAS(&r->fr_c[0], o, o + nch);
+            if (w == o) break;
+            o = w;
+        }
+        const uint32_t key = fr_key();
+        const unsigned int pend = atomicAdd(&r->fr_st[key], nch);     // before any chunk is published
+        asm volatile("s_waitcnt vmcnt(0)" :: "v"(pend) : "memory");
+        auto put = [&](uint32_t j, const E &v) {      // two 16-byte stores (the release below covers them)
+            uint4 *d = reinterpret_cast<uint4 *>(r->fr_ent + ((o + j / FR_CH) * FR_CH + j % FR_CH) * FR_EW);
+            if constexpr (sizeof(IT) == 4) {
+                d[0] = make_uint4(v.x, v.y, v.z, v.w);
+            } else {
+                d[0] = make_uint4((uint32_t)v.x, (uint32_t)(v.x >> 32), (uint32_t)v.y, v.w);
+                d[1] = make_uint4((uint32_t)(v.y >> 32), (uint32_t)v.z, (uint32_t)(v.z >> 32), 0u);
+            }
+        };
+        uint32_t j = 0;
+        if (C_VT(ctl)) put(j++, e);
+        {
+            BMask<MW> mm = mask;
+            while (mm.any() && j < cnt) {
+                const int b = mm.lowest();
+                mm.reset(b);
+                for (uint32_t sl = HEAD(b); sl != NIL && j < cnt; sl = NXT(sl)) put(j++, ent_load<IT>(a.pool, pbase, sl));
+            }
+        }
+        // the lists must hold exactly n_entries: otherwise publish what was written, and mark
+        // the item as having a hit, so that nothing is concluded from its sub-searches
+        if (j != cnt) atomicOr(&r->fr_st[key], FR_HIT);
+        for (uint32_t c = 0; c < nch; ++c) {
+            const uint32_t in = j > c * FR_CH ? (j - c * FR_CH < FR_CH ? j - c * FR_CH : FR_CH) : 0u;
+            r->fr_tag[o + c] = in << 26 | (key + 1u);
+        }
+        // complete chunks only enter the ready queue: a taker never waits on a walk
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long q0 = atomicAdd(&r->fr_c[9], (unsigned long long)nch);
+        for (uint32_t c = 0; c < nch; ++c)
+            __hip_atomic_store(&r->fr_rq[q0 + c], (uint32_t)(o + c) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&r->fr_c[4], 1ull);
+        return true;
+    };
+    // helpers: a waiting lane starts a sub-search at ready-queue position qp: the chunk's
+    // entries go to the lane's own stack (their order does not matter before a hit), under
+    // its item's row and regime.  The queue slot is written right after the tail moved; the
+    // chunk itself was released before that (agent-scope acquire, then plain loads).
+    auto help_start = [&](unsigned long long qp) {
+        const ColdArgs r = cold_args();
+        uint32_t c1;
+        while ((c1 = __hip_atomic_load(&r->fr_rq[qp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const size_t c = c1 - 1u;
+        const uint32_t t = r->fr_tag[c];
+        begin_item((t & 0x3FFFFFFu) - 1u);               // its strand's row and regime, a fresh stack
+        ctl &= ~(1u << 6);                               // no virtual top: every entry from the pool
+        const uint32_t in = t >> 26;
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(r->fr_ent + c * FR_CH * FR_EW);
+        for (uint32_t q = 0; q < in; ++q) {
+            const uint4 u = s4[2 * q], w = s4[2 * q + 1];
+            E v;
+            if constexpr (sizeof(IT) == 4) {
+                v.x = u.x; v.y = u.y; v.z = u.z;
+            } else {
+                v.x = (uint64_t)u.x | (uint64_t)u.y << 32;
+                v.y = (uint64_t)u.z | (uint64_t)w.x << 32;
+                v.z = (uint64_t)w.y | (uint64_t)w.z << 32;
+            }
+            v.w = u.w;
+            flush(v, bucket_of(v.w));
+        }
+        n_entries = (int)in;
+        frs = 2u; fr_p0 = st_p; fr_q0 = st_q;
+    };
+    // helpers: the waiting lanes of the wave take published chunks (one CAS for the wave), or
+    // leave once every item has finished and every chunk was taken (a sub-search still
+    // running then belongs to a finished item, and stops at its next poll)
+    auto fr_take = [&]() {
+        const uint64_t wb = __ballot(C_PH(ctl) == PH_WAIT);
+        if (!wb) return;
+        const ColdArgs r = cold_args();
+        const int leader = __ffsll((unsigned long long)wb) - 1;
+        unsigned long long t0 = 0;
+        uint32_t k = 0, fin = 0;
+        if (lane == leader) {
+            const unsigned long long want = (unsigned long long)__popcll(wb);
+            unsigned long long tk = __hip_atomic_load(&r->fr_c[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long rs = __hip_atomic_load(&r->fr_c[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk < rs) {
+                for (int tries = 0; tries < 4 && tk < rs; ++tries) {     // (lost races: the next poll)
+                    const unsigned long long kk = rs - tk < want ? rs - tk : want;
+                    const unsigned long long w = atomicCAS(&r->fr_c[1], tk, tk + kk);
+                    if (w == tk) { t0 = tk; k = (uint32_t)kk; break; }
+                    tk = w;
+                }
+                if (k) atomicSub(&r->fr_c[3], (unsigned long long)k);
+            } else if (__hip_atomic_load(&r->fr_c[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                           (unsigned long long)n_jobs * 2ull &&
+                       __hip_atomic_load(&r->fr_c[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                           __hip_atomic_load(&r->fr_c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                // every item has finished (none can offer more) and every reserved chunk was taken
+                fin = 1;
+                atomicSub(&r->fr_c[3], want);
+            }
+        }
+        t0 = __shfl(t0, leader); k = __shfl(k, leader); fin = __shfl(fin, leader);
+        if (C_PH(ctl) == PH_WAIT) {
+            const uint32_t rank = (uint32_t)__popcll(wb & ((1ull << lane) - 1ull));
+            if (rank < k) help_start(t0 + rank);
+            else if (fin) SET_PH(ctl, PH_EXIT);
+        }
+    };
+
 #ifdef HSA_DIAG
     tt = __builtin_amdgcn_s_memtime();
 #endif
     for (;;) {
+        ++fr_tick;
         // ---------------- (A) strand ends and read acquisition, batched per wave.
         // The rare steps of a read -- copying its hits out (end_strand), the switch to
         // the forward strand with its row DMA, taking the next read -- are long code
@@ -1167,8 +1389,9 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         // for hundreds of iterations.
         const uint64_t wm = __ballot(C_PH(ctl) == PH_IDLE || C_PH(ctl) == PH_END);
         idle_acc += (uint32_t)__popcll(wm);
-        if (wm && (idle_acc >= a.batch_idle || (uint32_t)__popcll(wm) >= a.batch_k ||
-                   __ballot(C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END) == 0)) {
+        const bool none_searching = __ballot(C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END &&
+                                             C_PH(ctl) != PH_WAIT) == 0;
+        if (wm && (idle_acc >= a.batch_idle || (uint32_t)__popcll(wm) >= a.batch_k || none_searching)) {
             idle_acc = 0;
             if (C_PH(ctl) == PH_END) end_strand();
             const bool need = C_PH(ctl) == PH_IDLE;
@@ -1179,46 +1402,37 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 const ColdArgs r = cold_args();
                 if (lane == leader) base = atomicAdd(&r->ctr[r->qctr], (unsigned long long)__popcll(mb));
                 base = __shfl(base, leader);
-                if (need) {
+                {
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
-                    if (j < (unsigned long long)n_jobs << (r->split ? 1 : 0)) {
-                        const uint32_t item = (uint32_t)j;
-#ifdef HSA_DIAG
-                        rd_t0 = __builtin_amdgcn_s_memrealtime(); rd_steps = 0; rd_p0 = st_p;
-#endif
-                        qpos = r->split ? item >> 1 : item;
-                        if (r->perm) qpos = (uint32_t)r->perm[qpos];
-                        const int job = r->job_list ? r->job_list[qpos] : (int)qpos;
-                        const hsa_job_t J = r->jobs[job];
-                        opt_max_diff = J.max_diff;
-                        const uint32_t len = J.len;
-                        if (r->mg) {
-                            // one direct bwt_match_gap call: its strand, its width_seed kind
-                            // (host-checked: 0 <= seed_len <= len when width_seed is given)
-                            const hsa_mg_job_t M = r->mg[job];
-                            const uint32_t has_seed = M.seed != HSA_SEED_NONE;
-                            ctl = (uint32_t)(M.strand & 1) << 3 | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 |
-                                  (M.seed == HSA_SEED_ALIAS ? 1u : 0u) << 7 | len << 10 |
-                                  (has_seed ? (uint32_t)J.seed_len : 0u) << 20;
-                        } else {
-                            const uint32_t has_seed = (int)len > J.seed_len;
-                            ctl = 8u | has_seed << 4 | (uint32_t)(J.regime & 1) << 5 | len << 10 |
-                                  (has_seed ? (uint32_t)J.seed_len : 0u) << 20;     // strand 1 (rc first, bwtaln.c:343)
-                            if ((r->split && (item & 1u)) || r->fwd_only) ctl &= ~8u;   // split: odd items search fwd
-                            sq0 = st_q; sp0 = st_p;
+                    const bool got = need && j < (unsigned long long)n_jobs << (r->split ? 1 : 0);
+                    if constexpr (!HUGE) {
+                        if (a.fr_budget) {             // the lanes that found the queue empty wait for entries
+                            const uint32_t nf = (uint32_t)(__popcll(mb) - __popcll(__ballot(got)));
+                            if (lane == leader && nf) atomicAdd(&r->fr_c[3], (unsigned long long)nf);
                         }
-                        const hsa_regime_t *R = s_reg + (J.regime & 1);
-                        pen = (uint32_t)R->s_mm | (uint32_t)R->s_gapo << 10 | (uint32_t)R->s_gape << 20;
-                        rmode = (uint32_t)R->mode | (uint32_t)R->max_gapo << 8 | (uint32_t)R->max_gape << 16;
-                        if (opt_max_diff > R->max_diff) ctl |= 2u << 8;
-                        start_strand();
-                    } else {
-                        SET_PH(ctl, PH_EXIT);
+                    }
+                    if (need) {
+                        if (got) begin_item((uint32_t)j);
+                        else SET_PH(ctl, (!HUGE && a.fr_budget) ? PH_WAIT : PH_EXIT);
                     }
                 }
             }
+            if constexpr (!HUGE) {
+                if (a.fr_budget) fr_take();
+            }
+        } else if constexpr (!HUGE) {
+            // waiting lanes beside searching ones look for entries every 128 iterations (a poll
+            // is a dependent load the whole wave waits for); a wave with none searching, every
+            // iteration, after a sleep
+            if (a.fr_budget && (none_searching || (fr_tick & 127u) == 64u)) fr_take();
         }
         if (__all(C_PH(ctl) == PH_EXIT)) break;
+        if constexpr (!HUGE) {
+            if (a.fr_budget && __ballot(C_PH(ctl) != PH_WAIT && C_PH(ctl) != PH_EXIT) == 0) {
+#pragma unroll
+                for (int z = 0; z < 4; ++z) __builtin_amdgcn_s_sleep(127);
+            }
+        }
 
 #ifdef HSA_DIAG
         TMARK(0);
@@ -1233,11 +1447,18 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         // One control pass per iteration: a lane whose pop needs no rank step (pruned,
         // hit, strand change) just skips this iteration's step instead of making the whole
         // wave run the control code again.
-        if (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END) do {
+        if (C_PH(ctl) != PH_EXIT && C_PH(ctl) != PH_IDLE && C_PH(ctl) != PH_END && C_PH(ctl) != PH_WAIT) do {
 #ifdef HSA_DIAG
             { const uint64_t em = __ballot(1); if (lane == __ffsll((unsigned long long)em) - 1) DC(7); }
 #endif
             if (C_OVF(ctl)) {
+                if constexpr (!HUGE) {
+                    if (frs & 2u) {       // a sub-search outgrew the lane: no proof, the owner searches on
+                        atomicOr(&cold_args()->fr_st[fr_key()], FR_HIT);
+                        help_done();
+                        break;
+                    }
+                }
                 if (C_OVF(ctl) > 1) atomicAdd(&cold_args()->ctr[5], 1ull);
                 finish_job(HSA_F_OVERFLOW, 0, 0);
                 break;
@@ -1257,6 +1478,49 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             }
             // PH_POP: bwtgap.c:144-186
             if (n_entries == 0 || n_entries > RG(max_entries)) { SET_PH(ctl, PH_END); continue; }
+            if constexpr (!HUGE) {
+                // helpers, every 16 pops of a strand: a sub-search stops once its item is decided
+                // (a hit, or its owner ended); an owner whose offered entries have all been
+                // searched without a hit has its answer -- no hit -- and its work: what it did
+                // before the offer plus its sub-searches'.  Every 64 pops past fr_budget, a strand
+                // with no hit yet offers its entries while more lanes wait than entries do.
+                // (the polls run on the wave's iteration count, so that all its lanes load
+                // together: a lane's own cadence made some lane of the wave wait on a load
+                // nearly every iteration)
+                const uint32_t ps = st_p - fr_p0;
+                if (a.fr_budget && (fr_tick & 31u) == 0u) {
+                    const ColdArgs r = cold_args();
+                    bool stop = false;
+                    if (frs & 3u) {
+                        const uint32_t key = fr_key();
+                        const uint32_t sv = __hip_atomic_load(&r->fr_st[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (frs & 2u) {
+                            stop = (sv & (FR_HIT | FR_DONE)) != 0u;
+                        } else if (sv == 0u && n_aln == 0) {
+                            st_q = fr_q0 + (uint32_t)atomicAdd(&r->fr_q[key], 0ull);
+                            st_p = fr_p0 + (uint32_t)atomicAdd(&r->fr_p[key], 0ull);
+                            atomicAdd(&r->fr_c[7], 1ull);
+                            stop = true;
+                        }
+                    }
+                    // one offer per wave per 64 iterations, by its first eligible lane (an offer
+                    // walks the lane's lists: the wave waits for it)
+                    const bool elig = !stop && !(frs & 5u) && n_aln == 0 && !C_OVF(ctl) && n_entries > 1 &&
+                                      n_entries <= (int)FR_WALK && ps >= a.fr_budget && (fr_tick & 63u) == 0u;
+                    const uint64_t em = __ballot(elig);
+                    if (elig && lane == __ffsll((unsigned long long)em) - 1) {
+                        const unsigned long long wt = __hip_atomic_load(&r->fr_c[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const unsigned long long rs = __hip_atomic_load(&r->fr_c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const unsigned long long tk = __hip_atomic_load(&r->fr_c[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (wt > rs - tk + a.fr_demand) {     // more lanes wait than chunks do
+                            if (!fr_offer()) frs |= 4u;
+                            else if (frs & 2u) stop = true;      // a helper hands its rest on and ends
+                            else { frs |= 1u; fr_p0 = st_p; fr_q0 = st_q; }
+                        }
+                    }
+                    if (stop) { SET_PH(ctl, PH_END); continue; }
+                }
+            }
             if (C_VT(ctl)) {
                 DC(3);
                 ctl &= ~(1u << 6);                                        // e already holds it
@@ -1527,6 +1791,13 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         for (int i = 0; i < 4; ++i) atomicAdd(&g_dctr[9 + i], (unsigned long long)tsec[i]);
 #endif
     // statistics
+    if constexpr (!HUGE) {
+        if (a.fr_budget) {
+            unsigned long long hs = st_hs, hq = st_hq;
+            for (int d = 32; d >= 1; d >>= 1) { hs += __shfl_xor(hs, d); hq += __shfl_xor(hq, d); }
+            if (lane == 0) { atomicAdd(&a.fr_c[6], hs); atomicAdd(&a.fr_c[8], hq); }
+        }
+    }
     atomicAdd(&a.ctr[2], (unsigned long long)st_q);
     atomicAdd(&a.ctr[3], (unsigned long long)st_b);
     atomicAdd(&a.ctr[4], (unsigned long long)st_p);
@@ -1862,6 +2133,8 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
     A.ktd = tr ? ix->trie_depth : 0u;
     A.wkey = nullptr; A.perm = nullptr; A.okey = 0;
     A.fwd_list = nullptr; A.fwd_n = nullptr; A.fwd_only = 0; A.rmap = nullptr;
+    A.fr_budget = 0; A.fr_demand = 0; A.fr_cap = 0;
+    A.fr_ent = nullptr; A.fr_tag = nullptr; A.fr_rq = nullptr; A.fr_st = nullptr; A.fr_q = nullptr; A.fr_p = nullptr; A.fr_c = nullptr;
     A.mg = mg ? mg->d_mg : nullptr;
     A.cw = mg ? mg->d_cw : nullptr;
     A.wbid = mg ? reinterpret_cast<int32_t *>(wr + rows * (rb + rs + WGB * (size_t)rg)) : nullptr;
@@ -1873,12 +2146,58 @@ static SearchArgs pass_args(hsa_index *ix, const LaunchPlan &P, SearchScratch &S
 // lanes when both fit on the chip at once (HSA_SPLIT=0/1 forces it off/on).  A read's
 // search chain halves (rc and fwd side by side); the fwd strand's work is speculative, so
 // large batches, which fill every lane anyway, keep one read per lane.
+// Helpers are opt-in (HSA_HELP=1): exact, but measured slower on the drop-in's 100 000-read
+// calls ("Helpers")
+static bool use_help()
+{
+    const char *e = getenv("HSA_HELP");
+    return e && atoi(e) != 0;
+}
+
 static bool use_split(const LaunchPlan &P, int n, const unsigned long long *n_dev, const MgPass *mg, uint32_t qctr)
 {
     if (mg || n_dev || qctr != 0 || P.huge || n <= 0) return false;
     const char *e = getenv("HSA_SPLIT");
     if (e) return atoi(e) != 0;
-    return 2 * (size_t)n <= P.resident;
+    // with helpers, also batches of up to one read per resident lane: their tails are the
+    // long strand searches the waiting lanes then share
+    return (use_help() ? (size_t)n : 2 * (size_t)n) <= P.resident;
+}
+
+// Helpers of a strand-split pass (SearchArgs::fr_*): the shared frontier and the per-item
+// state in ix->d_help, zeroed on the pass's stream.  HSA_HELP=0: off; HSA_HELP_BUDGET pops
+// before a strand may offer its entries (default 512); HSA_HELP_DEMAND waiting lanes beyond
+// the unsearched chunks before it does (default: half the pass's lanes, so that only the
+// strands still running when half the chip waits -- the launch's tail -- offer); HSA_HELP_CAP
+// chunks of FR_CH entries (default 1 Mi: 512 MB).
+// Off when a regime's max_entries does not exceed the pool: then the main pass's stack
+// stays below the reference's max_entries break (bwtgap.c:150-151) whenever it completes,
+// and a strand its helpers answer counts the reference's rank queries and pops.
+template <typename IT>
+static int help_args(hsa_index *ix, SearchArgs &A, size_t items, const LaunchPlan &P, hipStream_t st)
+{
+    if (!use_help() || ix->staged_min_entries <= (int)P.pcap + 16) return 0;
+    auto env = [](const char *k, long d) { const char *v = getenv(k); return v ? atol(v) : d; };
+    const long budget = env("HSA_HELP_BUDGET", 512), demand = env("HSA_HELP_DEMAND", (long)(P.lanes / 2));
+    const long cap = env("HSA_HELP_CAP", 1l << 20);
+    if (budget <= 0 || cap <= 0 || cap > (1l << 24) || demand < 0 || items >= (1u << 26)) return 0;
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t o_st = 256, o_q = o_st + al(items * 4), o_p = o_q + al(items * 8), o_tag = o_p + al(items * 8);
+    const size_t o_rq = o_tag + al((size_t)cap * 4);
+    const size_t o_ent = o_rq + al((size_t)cap * 4), total = o_ent + (size_t)cap * FR_CH * FR_EW * 4;
+    int rc = hsa_grow(&ix->d_help, &ix->d_help_cap, total);
+    if (rc) return rc;
+    char *d = (char *)ix->d_help;
+    HSA_HIP(hipMemsetAsync(d, 0, o_ent, st));       // counters, item state and sums, tags, ready queue
+    A.fr_budget = (uint32_t)budget; A.fr_demand = (uint32_t)demand; A.fr_cap = (uint32_t)cap;
+    A.fr_c = (unsigned long long *)d;
+    A.fr_st = (uint32_t *)(d + o_st);
+    A.fr_q = (unsigned long long *)(d + o_q);
+    A.fr_p = (unsigned long long *)(d + o_p);
+    A.fr_tag = (uint32_t *)(d + o_tag);
+    A.fr_rq = (uint32_t *)(d + o_rq);
+    A.fr_ent = (uint32_t *)(d + o_ent);
+    return 0;
 }
 
 // The pass's search scratch (per-lane pools, links, staged hits), sized to what the
@@ -1978,6 +2297,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
         A.sp_n = (int32_t *)(d + al);
         A.sp_q = (uint32_t *)(d + al + al / 2);
         A.sp_p = (uint32_t *)(d + 2 * al);
+        if (!P.huge && (rc = help_args<IT>(ix, A, m, P, st))) return rc;
     }
     if (qctr == 0) HSA_HIP(hipMemsetAsync(d_ctr, 0, 16 * sizeof(unsigned long long), st));   // not on a re-run
     // cost order: the main pass of a batch with more reads than the chip has lanes
@@ -2067,7 +2387,16 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
         const unsigned nb = (unsigned)(((size_t)n + BLOCK - 1) / BLOCK);
         hipLaunchKernelGGL(k_split_finalize, dim3(nb), dim3(BLOCK), 0, st, A);
         HSA_HIP(hipGetLastError());
-        if (getenv("HSA_VERBOSE")) fprintf(stderr, "[hsa] strand-split main pass: %d reads on %zu lanes\n", n, P.lanes);
+        if (getenv("HSA_VERBOSE")) {
+            fprintf(stderr, "[hsa] strand-split main pass: %d reads on %zu lanes\n", n, P.lanes);
+            if (A.fr_c) {
+                unsigned long long c[9];
+                HSA_HIP(hipMemcpyAsync(c, A.fr_c, sizeof c, hipMemcpyDeviceToHost, st));
+                HSA_HIP(hipStreamSynchronize(st));
+                fprintf(stderr, "[hsa] helpers: %llu offers (%llu refused), %llu chunks, %llu sub-searches, %llu strands "
+                                "answered by them, %llu rank queries in sub-searches\n", c[4], c[5], c[0], c[6], c[7], c[8]);
+            }
+        }
     }
     return 0;
 }
@@ -2128,6 +2457,9 @@ static int stage_regimes(hsa_index *ix, const hsa_regime_t *regimes, int n_regim
     if (nb > MAXB) { hsa_set_error("%d reachable scores: at most %d stack buckets", nb, MAXB); return HSA_E_ARG; }
     ix->staged_ntab = (ntab + 7) / 8 * 8;
     ix->staged_mmb = mm_buckets(regimes, n_regimes, host + 256);
+    ix->staged_min_entries = regimes[0].max_entries;
+    for (int r = 1; r < n_regimes; ++r)
+        if (regimes[r].max_entries < ix->staged_min_entries) ix->staged_min_entries = regimes[r].max_entries;
     if (!force && ix->staged_valid && memcmp(ix->staged, host, sizeof host) == 0) return 0;
     memcpy(ix->staged, host, sizeof host);
     ix->staged_valid = 1;

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-6 A/B of the drop-in end-to-end leg (the reference's driver with our entry points,
 # 100 000-read calls): the default small splice warm-up at attach vs none (config 2), and
-# the strand-split main pass forced on (HSA_SPLIT=1) vs the default (configs 3 and 4).
+# the strand-split main pass forced on (HSA_SPLIT=1) vs the default (configs 3 and 4), and
+# the strand-split pass's helpers (HSA_HELP) off vs on (configs 2-4).
 # Run on the GPU box from the repo root: bash tools/r06_e2e_ab.sh <set>
 set -e
 export TMPDIR=/tmp
@@ -25,4 +26,13 @@ c4)   EXTRA="--config 4"
 c3)   EXTRA="--config 3"
       run c3_split_default HSA_SPLIT_UNSET=1
       run c3_split1 HSA_SPLIT=1 ;;
+help4) EXTRA="--config 4"
+      run c4_help0 HSA_HELP=0
+      run c4_help1 HSA_HELP=1 ;;
+help3) EXTRA="--config 3"
+      run c3_help0 HSA_HELP=0
+      run c3_help1 HSA_HELP=1 ;;
+help2) EXTRA="--config 2"
+      run c2_help0 HSA_HELP=0
+      run c2_help1 HSA_HELP=1 ;;
 esac
