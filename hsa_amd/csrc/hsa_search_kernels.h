@@ -160,6 +160,9 @@ struct SearchArgs {
 #define FR_EW 8u                   // words per published entry (32- and 64-bit intervals)
 #define FR_CH 16u                  // entries per chunk: one sub-search searches a chunk's sub-trees
 #define FR_WALK 1024u              // largest stack a strand offers (the walk is a chain of dependent loads)
+#ifndef HSA_HELPERS
+#define HSA_HELPERS 1              // A/B builds: -DHSA_HELPERS=0 compiles the helpers out of k_search
+#endif
 
 // The kernel's arguments re-read from the kernarg segment where a rare path uses them
 // (strand start and end, next read, hit staging): the asm barrier keeps the compiler
@@ -786,6 +789,10 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     const IT TT = Ix<IT>::T(a);
     const IT *const CC = Ix<IT>::C(a);
     using LT = typename std::conditional<HUGE, uint32_t, uint16_t>::type;   // pool link
+    // the helpers' code (SearchArgs::fr_*): gapped 32-bit searches only (configs 3 and 4, whose
+    // small calls end in long strands); the other kernels stay as they were (their registers:
+    // the 64-bit 4-bit-row kernels spilled with it)
+    constexpr bool FRH = !HUGE && HSA_HELPERS && GAPS && sizeof(IT) == 4 && !WFmt<WT>::NIB;
     constexpr uint32_t NIL = HUGE ? 0xFFFFFFFFu : (uint32_t)NIL16;
 #ifdef HSA_DIAG
     if (threadIdx.x == 0 && blockIdx.x < 8192) {
@@ -1026,7 +1033,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             r->sp_q[pi] = st_q - sq0;
             r->sp_p[pi] = st_p - sp0;
             st_q = sq0; st_p = sp0;
-            if constexpr (!HUGE) {
+            if constexpr (FRH) {
                 if (a.fr_budget) {
                     if (frs & 1u) atomicOr(&r->fr_st[pi], FR_DONE);   // its helpers stop
                     atomicAdd(&r->fr_c[2], 1ull);                      // items finished (the exit test)
@@ -1066,7 +1073,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         SET_PH(ctl, PH_IDLE);
     };
     auto end_strand = [&]() {
-        if constexpr (!HUGE) {
+        if constexpr (FRH) {
             if (frs & 2u) { help_done(); return; }
         }
         if (n_aln > 0) {
@@ -1126,7 +1133,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
     // returns false when the search must stop
     auto on_hit = [&](IT k, IT l, IT rk, IT rl) -> bool {
         const ColdArgs r = cold_args();
-        if constexpr (!HUGE) {
+        if constexpr (FRH) {
             if (frs & 3u) {
                 atomicOr(&r->fr_st[fr_key()], FR_HIT);   // the item has a hit: its sub-searches stop
                 if (frs & 2u) return false;              // a helper records nothing
@@ -1405,7 +1412,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                 {
                     const unsigned long long j = base + (unsigned long long)__popcll(mb & ((1ull << lane) - 1ull));
                     const bool got = need && j < (unsigned long long)n_jobs << (r->split ? 1 : 0);
-                    if constexpr (!HUGE) {
+                    if constexpr (FRH) {
                         if (a.fr_budget) {             // the lanes that found the queue empty wait for entries
                             const uint32_t nf = (uint32_t)(__popcll(mb) - __popcll(__ballot(got)));
                             if (lane == leader && nf) atomicAdd(&r->fr_c[3], (unsigned long long)nf);
@@ -1413,21 +1420,21 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
                     }
                     if (need) {
                         if (got) begin_item((uint32_t)j);
-                        else SET_PH(ctl, (!HUGE && a.fr_budget) ? PH_WAIT : PH_EXIT);
+                        else SET_PH(ctl, (FRH && a.fr_budget) ? PH_WAIT : PH_EXIT);
                     }
                 }
             }
-            if constexpr (!HUGE) {
+            if constexpr (FRH) {
                 if (a.fr_budget) fr_take();
             }
-        } else if constexpr (!HUGE) {
+        } else if constexpr (FRH) {
             // waiting lanes beside searching ones look for entries every 128 iterations (a poll
             // is a dependent load the whole wave waits for); a wave with none searching, every
             // iteration, after a sleep
             if (a.fr_budget && (none_searching || (fr_tick & 127u) == 64u)) fr_take();
         }
         if (__all(C_PH(ctl) == PH_EXIT)) break;
-        if constexpr (!HUGE) {
+        if constexpr (FRH) {
             if (a.fr_budget && __ballot(C_PH(ctl) != PH_WAIT && C_PH(ctl) != PH_EXIT) == 0) {
 #pragma unroll
                 for (int z = 0; z < 4; ++z) __builtin_amdgcn_s_sleep(127);
@@ -1452,7 +1459,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             { const uint64_t em = __ballot(1); if (lane == __ffsll((unsigned long long)em) - 1) DC(7); }
 #endif
             if (C_OVF(ctl)) {
-                if constexpr (!HUGE) {
+                if constexpr (FRH) {
                     if (frs & 2u) {       // a sub-search outgrew the lane: no proof, the owner searches on
                         atomicOr(&cold_args()->fr_st[fr_key()], FR_HIT);
                         help_done();
@@ -1478,7 +1485,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
             }
             // PH_POP: bwtgap.c:144-186
             if (n_entries == 0 || n_entries > RG(max_entries)) { SET_PH(ctl, PH_END); continue; }
-            if constexpr (!HUGE) {
+            if constexpr (FRH) {
                 // helpers, every 16 pops of a strand: a sub-search stops once its item is decided
                 // (a hit, or its owner ended); an owner whose offered entries have all been
                 // searched without a hit has its answer -- no hit -- and its work: what it did
@@ -1791,7 +1798,7 @@ __global__ void __launch_bounds__(NT, HSA_WAVES_SIMD) k_search(SearchArgs a)
         for (int i = 0; i < 4; ++i) atomicAdd(&g_dctr[9 + i], (unsigned long long)tsec[i]);
 #endif
     // statistics
-    if constexpr (!HUGE) {
+    if constexpr (FRH) {
         if (a.fr_budget) {
             unsigned long long hs = st_hs, hq = st_hq;
             for (int d = 32; d >= 1; d >>= 1) { hs += __shfl_xor(hs, d); hq += __shfl_xor(hq, d); }
@@ -2154,14 +2161,19 @@ static bool use_help()
     return e && atoi(e) != 0;
 }
 
-static bool use_split(const LaunchPlan &P, int n, const unsigned long long *n_dev, const MgPass *mg, uint32_t qctr)
+// (helpers run in gapped 32-bit kernels only, k_search's FRH)
+template <typename IT>
+static bool help_kernel(const LaunchPlan &P) { return use_help() && HSA_HELPERS && P.gaps && sizeof(IT) == 4; }
+
+static bool use_split(const LaunchPlan &P, int n, const unsigned long long *n_dev, const MgPass *mg, uint32_t qctr,
+                      bool help)
 {
     if (mg || n_dev || qctr != 0 || P.huge || n <= 0) return false;
     const char *e = getenv("HSA_SPLIT");
     if (e) return atoi(e) != 0;
     // with helpers, also batches of up to one read per resident lane: their tails are the
     // long strand searches the waiting lanes then share
-    return (use_help() ? (size_t)n : 2 * (size_t)n) <= P.resident;
+    return (help ? (size_t)n : 2 * (size_t)n) <= P.resident;
 }
 
 // Helpers of a strand-split pass (SearchArgs::fr_*): the shared frontier and the per-item
@@ -2176,7 +2188,7 @@ static bool use_split(const LaunchPlan &P, int n, const unsigned long long *n_de
 template <typename IT>
 static int help_args(hsa_index *ix, SearchArgs &A, size_t items, const LaunchPlan &P, hipStream_t st)
 {
-    if (!use_help() || ix->staged_min_entries <= (int)P.pcap + 16) return 0;
+    if (!help_kernel<IT>(P) || ix->staged_min_entries <= (int)P.pcap + 16) return 0;
     auto env = [](const char *k, long d) { const char *v = getenv(k); return v ? atol(v) : d; };
     const long budget = env("HSA_HELP_BUDGET", 512), demand = env("HSA_HELP_DEMAND", (long)(P.lanes / 2));
     const long cap = env("HSA_HELP_CAP", 1l << 20);
@@ -2245,7 +2257,7 @@ static int launch_pass(hsa_index *ix, const LaunchPlan &P0, SearchScratch &S, co
                        int32_t *ovf_list = nullptr, const unsigned long long *n_dev = nullptr, uint32_t qctr = 0,
                        const MgPass *mg = nullptr, uint32_t ovf_ctr = 8)
 {
-    const bool split = use_split(P0, n, n_dev, mg, qctr);
+    const bool split = use_split(P0, n, n_dev, mg, qctr, help_kernel<IT>(P0));
     LaunchPlan P = P0;
     if (split) {                                        // lanes for 2 n items
         const size_t need = (2 * (size_t)n + P.nt - 1) / P.nt, cap = P.resident / P.nt;

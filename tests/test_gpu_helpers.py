@@ -8,7 +8,7 @@ demand threshold, so that nearly every strand offers its entries at once."""
 import numpy as np
 import pytest
 
-from golden_io import cases, load_case, split_hits
+from golden_io import cases, load_case, parse_opts, split_hits
 
 pytestmark = pytest.mark.gpu
 
@@ -24,9 +24,16 @@ def _force(monkeypatch, budget="16"):
     monkeypatch.setenv("HSA_VERBOSE", "1")
 
 
+def _gapped(name):
+    """Helpers run in the gapped 32-bit kernels only (k_search's FRH): gap opens allowed
+    (max_gapo > 0, and max_diff not 0, which clears them, bwtaln.c:256)."""
+    from oracle_ctypes import default_opt
+    o = parse_opts(load_case(name)["args"], default_opt())
+    return o["max_gapo"] > 0 and o["max_diff"] != 0
+
+
 def _helper_stats(err):
     lines = [ln for ln in err.splitlines() if ln.startswith("[hsa] helpers:")]
-    assert lines, "no helper statistics: the strand-split pass did not run with helpers"
     tot = np.zeros(6, np.int64)
     for ln in lines:
         w = ln.replace("(", " ").replace(")", " ").replace(",", " ").split()
@@ -43,7 +50,7 @@ def test_helpers_match_reference(name, monkeypatch, capfd):
     _force(monkeypatch)
     _compare(name)
     st = _helper_stats(capfd.readouterr().err)
-    if name.startswith(("tiny_gap", "rep_gap", "rep_mm", "rep_deep", "tiny_mm")):
+    if name.startswith(("tiny_gap", "rep_gap", "rep_mm", "rep_deep")):   # deep enough to outlast the budget
         assert st["offers"] > 0 and st["subsearches"] > 0, st
 
 
@@ -66,8 +73,9 @@ def test_helpers_keep_rank_queries_and_pops(case, monkeypatch, capfd):
     assert int(got["c"][4]) == int(st[1]), ("gap_pop count", hs)
     print(case, hs)
     # (whether an owner is answered by its helpers before it ends by itself depends on
-    # timing; test_gpu_config4 and the drop-in's long no-hit searches exercise that path)
-    assert hs["offers"] > 0 and hs["subsearches"] > 0, hs
+    # timing; the drop-in's long no-hit searches answer thousands: profiles/r06_helpers_ab.log)
+    if _gapped(case):
+        assert hs["offers"] > 0 and hs["subsearches"] > 0, hs
 
 
 @pytest.mark.parametrize("budget", ["1", "64"])
